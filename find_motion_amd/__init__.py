@@ -1,0 +1,28 @@
+"""find_motion_amd — MI355X-native hot path of find_motion's per-frame motion chain.
+
+The package mirrors the reference's surface (find_motion/find_motion.py):
+VideoMotion / VideoFrame with the same constructor and methods, the same CLI
+flags, and run_vid / run for embedding.  The per-frame cv2 chain
+(blur_frame, mask_off_areas, find_diff) runs as HIP kernels for gfx950
+through the C ABI in include/find_motion_amd.h; there is no CPU fallback.
+"""
+__version__ = "0.1.0"
+
+from ._native import (  # noqa: F401
+    Contour,
+    FMError,
+    MotionEngine,
+    NativeLibraryMissing,
+    rasterize_masks,
+)
+
+
+def make_gaussian(box_size: int, blur_scale: int) -> int:
+    """VideoMotion._make_gaussian (fm.py:478-484): odd kernel size from the box size."""
+    k = int(box_size / blur_scale)
+    return k + 1 if k % 2 == 0 else k
+
+
+def work_height(src_h: int, src_w: int, box_size: int) -> int:
+    """imutils.resize(width=box) height rule (fm.py:492)."""
+    return int(src_h * (box_size / float(src_w)))

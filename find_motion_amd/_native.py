@@ -1,0 +1,256 @@
+"""ctypes binding of include/find_motion_amd.h (libfm_hip.so, built in-tree).
+
+This is the only way the package reaches the hot path: there is no CPU
+fallback.  If the HIP library is missing, importing the engine raises
+NativeLibraryMissing with the build command.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libfm_hip.so")
+
+FM_OK, FM_EINVAL, FM_EHIP, FM_ENOMEM, FM_ESTATE, FM_ENOTSUP = 0, -1, -2, -3, -4, -5
+FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE = 0x1, 0x2
+PLANE_GRAY, PLANE_BLUR, PLANE_DELTA = 0, 1, 2
+
+EXPORTED = (
+    "fm_abi_version", "fm_create", "fm_destroy", "fm_last_error", "fm_work_size", "fm_set_mask",
+    "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
+    "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
+    "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks",
+)
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+class FMError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"find_motion_amd error {code}: {msg}")
+        self.code = code
+
+
+class FMParams(C.Structure):
+    _fields_ = [("device", C.c_int), ("n_streams", C.c_int), ("src_w", C.c_int), ("src_h", C.c_int),
+                ("box_size", C.c_int), ("ksize", C.c_int), ("threshold", C.c_int), ("avg", C.c_double),
+                ("max_batch", C.c_int), ("max_contours", C.c_int), ("flags", C.c_uint)]
+
+
+class FMContour(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("w", C.c_int32), ("h", C.c_int32),
+                ("origin_x", C.c_int32), ("origin_y", C.c_int32), ("reserved0", C.c_int32),
+                ("reserved1", C.c_int32)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libfm_hip.so (raises NativeLibraryMissing if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found: build the HIP extension with "
+            f"`make -C {os.path.join(_PKG, 'csrc')}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u8p = C.c_void_p, C.c_int, C.c_void_p
+    L.fm_abi_version.restype = i32
+    L.fm_create.argtypes = [C.POINTER(vp), C.POINTER(FMParams)]
+    L.fm_destroy.argtypes = [vp]
+    L.fm_destroy.restype = None
+    L.fm_last_error.argtypes = [vp]
+    L.fm_last_error.restype = C.c_char_p
+    L.fm_work_size.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
+    L.fm_set_mask.argtypes = [vp, i32, u8p]
+    L.fm_reset_stream.argtypes = [vp, i32]
+    L.fm_submit.argtypes = [vp, vp, i32, i32]
+    L.fm_wait.argtypes = [vp]
+    L.fm_get_counts.argtypes = [vp, vp]
+    L.fm_get_contours.argtypes = [vp, i32, i32, vp, i32]
+    L.fm_read_mask.argtypes = [vp, i32, i32, vp]
+    L.fm_read_plane.argtypes = [vp, i32, i32, i32, vp]
+    L.fm_read_background.argtypes = [vp, i32, vp]
+    L.fm_write_background.argtypes = [vp, i32, vp]
+    L.fm_set_hip_stream.argtypes = [vp, vp]
+    L.fm_kernel_times.argtypes = [vp, vp, vp, vp, i32]
+    L.fm_reset_kernel_times.argtypes = [vp]
+    L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
+    for name in EXPORTED:
+        if name not in ("fm_destroy", "fm_last_error", "fm_abi_version"):
+            getattr(L, name).restype = i32
+    _lib = L
+    return L
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def rasterize_masks(h: int, w: int, scale: float, polygons) -> np.ndarray:
+    """mask_off_areas (fm.py:611-636) rasterised once: keep-mask (1 = keep, 0 = masked)."""
+    L = load()
+    polys = [list(p) for p in (polygons or [])]
+    keep = np.empty((h, w), np.uint8)
+    npts = np.array([len(p) for p in polys], np.int32)
+    xy = np.array([c for p in polys for pt in p for c in pt], np.int32) if polys else np.zeros(2, np.int32)
+    rc = L.fm_rasterize_masks(h, w, float(scale), _ptr(xy), _ptr(npts) if polys else None, len(polys), _ptr(keep))
+    if rc != FM_OK:
+        raise FMError(rc, "invalid mask polygons (each needs >= 2 points)")
+    return keep
+
+
+@dataclass
+class Contour:
+    """One external contour of VideoFrame.contours (fm.py:269-276).
+
+    bbox is cv2.boundingRect's (x, y, w, h) (fm.py:792); origin is the border
+    start (the component's raster-first pixel)."""
+    x: int
+    y: int
+    w: int
+    h: int
+    origin: tuple
+
+    @property
+    def bbox(self):
+        return (self.x, self.y, self.w, self.h)
+
+
+class MotionEngine:
+    """One fm_ctx: n_streams background models on one HIP device."""
+
+    def __init__(self, *, n_streams: int, src_w: int, src_h: int, box_size: int, ksize: int,
+                 threshold: int, avg: float, max_batch: int = 1, max_contours: int = 4096,
+                 keep_planes: bool = False, profile: bool = False, device: int = 0):
+        self._L = load()
+        p = FMParams(device, n_streams, src_w, src_h, box_size, ksize, int(threshold), float(avg),
+                     max_batch, max_contours,
+                     (FM_FLAG_KEEP_PLANES if keep_planes else 0) | (FM_FLAG_PROFILE if profile else 0))
+        h = C.c_void_p()
+        rc = self._L.fm_create(C.byref(h), C.byref(p))
+        if rc != FM_OK:
+            raise FMError(rc, self._L.fm_last_error(None).decode())
+        self._h = h
+        self.params = p
+        hh, ww = C.c_int(), C.c_int()
+        self._check(self._L.fm_work_size(h, C.byref(hh), C.byref(ww)))
+        self.work_shape = (hh.value, ww.value)
+        self.n_streams = n_streams
+        self.src_shape = (src_h, src_w, 3)
+        self.max_batch = max_batch
+        self.max_contours = max_contours
+        self.last_batch = 0
+        self._inflight = None  # keeps host frames alive until wait()
+
+    # -- plumbing ------------------------------------------------------------
+    def _check(self, rc: int) -> int:
+        if rc < 0:
+            raise FMError(rc, self._L.fm_last_error(self._h).decode())
+        return rc
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.fm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- state ---------------------------------------------------------------
+    def set_mask(self, stream: int, keep: np.ndarray | None) -> None:
+        if keep is None:
+            self._check(self._L.fm_set_mask(self._h, stream, None))
+            return
+        keep = np.ascontiguousarray(keep, dtype=np.uint8)
+        if keep.shape != self.work_shape:
+            raise ValueError(f"keep-mask shape {keep.shape} != work shape {self.work_shape}")
+        self._check(self._L.fm_set_mask(self._h, stream, _ptr(keep)))
+
+    def reset(self, stream: int) -> None:
+        self._check(self._L.fm_reset_stream(self._h, stream))
+
+    def background(self, stream: int) -> np.ndarray:
+        out = np.empty(self.work_shape, np.float64)
+        self._check(self._L.fm_read_background(self._h, stream, _ptr(out)))
+        return out
+
+    def set_background(self, stream: int, bg: np.ndarray) -> None:
+        bg = np.ascontiguousarray(bg, dtype=np.float64)
+        if bg.shape != self.work_shape:
+            raise ValueError(f"background shape {bg.shape} != work shape {self.work_shape}")
+        self._check(self._L.fm_write_background(self._h, stream, _ptr(bg)))
+
+    def set_hip_stream(self, stream_handle: int | None) -> None:
+        self._check(self._L.fm_set_hip_stream(self._h, stream_handle))
+
+    # -- hot path ------------------------------------------------------------
+    def submit(self, frames: np.ndarray) -> None:
+        """frames: uint8 [n][n_streams][H][W][3] (or [n_streams][H][W][3] for n = 1), host memory."""
+        f = np.ascontiguousarray(frames, dtype=np.uint8)
+        if f.ndim == 4:
+            f = f[None]
+        if f.shape[1:] != (self.n_streams,) + self.src_shape:
+            raise ValueError(f"frames shape {f.shape} != [n][{self.n_streams}]{self.src_shape}")
+        self._check(self._L.fm_submit(self._h, _ptr(f), f.shape[0], 0))
+        self._inflight = f
+        self._pending_n = f.shape[0]
+
+    def submit_device(self, ptr: int, n_frames: int) -> None:
+        """Frames already in device memory (e.g. a torch CUDA tensor's data_ptr())."""
+        self._check(self._L.fm_submit(self._h, C.c_void_p(ptr), n_frames, 1))
+        self._inflight = None
+        self._pending_n = n_frames
+
+    def wait(self) -> None:
+        self._check(self._L.fm_wait(self._h))
+        self._inflight = None
+        self.last_batch = getattr(self, "_pending_n", 0)
+
+    def counts(self) -> np.ndarray:
+        out = np.zeros((self.last_batch, self.n_streams), np.int32)
+        self._check(self._L.fm_get_counts(self._h, _ptr(out)))
+        return out
+
+    def contours(self, frame: int, stream: int) -> list:
+        buf = (FMContour * self.max_contours)()
+        n = self._check(self._L.fm_get_contours(self._h, frame, stream, C.cast(buf, C.c_void_p), self.max_contours))
+        return [Contour(c.x, c.y, c.w, c.h, (c.origin_x, c.origin_y)) for c in buf[: min(n, self.max_contours)]]
+
+    def mask(self, frame: int, stream: int) -> np.ndarray:
+        out = np.empty(self.work_shape, np.uint8)
+        self._check(self._L.fm_read_mask(self._h, frame, stream, _ptr(out)))
+        return out
+
+    def plane(self, which: int, frame: int, stream: int) -> np.ndarray:
+        out = np.empty(self.work_shape, np.uint8)
+        self._check(self._L.fm_read_plane(self._h, which, frame, stream, _ptr(out)))
+        return out
+
+    def kernel_times(self) -> dict:
+        names = (C.c_char_p * 32)()
+        ms = (C.c_double * 32)()
+        n_l = (C.c_int64 * 32)()
+        n = self._check(self._L.fm_kernel_times(self._h, C.cast(names, C.c_void_p), C.cast(ms, C.c_void_p),
+                                                C.cast(n_l, C.c_void_p), 32))
+        return {names[i].decode(): (ms[i], n_l[i]) for i in range(min(n, 32))}
+
+    def reset_kernel_times(self) -> None:
+        self._check(self._L.fm_reset_kernel_times(self._h))

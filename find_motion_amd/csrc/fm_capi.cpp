@@ -1,0 +1,598 @@
+// fm_capi.cpp — C ABI of the MI355X motion-detection hot path (include/find_motion_amd.h).
+//
+// Owns the per-context device state (background models, masks, batch
+// buffers), builds the host-side tables OpenCV builds per call (INTER_AREA
+// taps, fixed-point Gaussian taps) once at fm_create, and sequences the
+// kernels of fm_kernels.hip on one HIP stream per context.
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "fm_internal.h"
+
+namespace fm {
+hipError_t launch_pixel_pp(hipStream_t st, const PixelArgs& a, const double* bg_in, double* bg_out);
+int pixel_lds_bytes(int ksize);
+}  // namespace fm
+
+using namespace fm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+enum class ResizeMode { Identity, Fast, General };
+
+}  // namespace
+
+struct fm_ctx {
+    fm_params p{};
+    int h = 0, w = 0;
+    size_t src_frame_bytes = 0, work_plane = 0;
+    ResizeMode rmode = ResizeMode::Identity;
+    int fast_sx = 1, fast_sy = 1;
+    AreaAxis ax, ay;
+    std::vector<int32_t> coef;
+
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    KernelTimer timer;
+
+    // device buffers
+    uint8_t* d_in = nullptr;      // host-fed staging [T][S][H][W][3]
+    uint8_t* d_work = nullptr;    // resized BGR [T][S][h][w][3]
+    double* d_bg[2] = {nullptr, nullptr};
+    int bg_cur = 0;
+    uint8_t* d_keep = nullptr;    // [S][h*w]
+    uint8_t* d_has_keep = nullptr;
+    uint8_t* d_init = nullptr;
+    uint8_t* d_mask = nullptr;    // [T][S][h*w]
+    uint8_t* d_planes = nullptr;  // [3][T][S][h*w]
+    int32_t* d_label = nullptr;
+    int32_t* d_cid = nullptr;
+    uint8_t* d_outer = nullptr;
+    int32_t* d_count = nullptr;
+    int32_t* d_rec = nullptr;
+    int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
+    float *d_xwt = nullptr, *d_ywt = nullptr;
+
+    // host state
+    std::vector<uint8_t> bg_init, has_keep;
+    uint8_t* h_init = nullptr;    // pinned
+    int32_t* h_count = nullptr;   // pinned [T*S]
+    int32_t* h_rec = nullptr;     // pinned [T*S*cap*5]
+    int pending = 0;              // frames in flight (0 = idle)
+    int ready = 0;                // frames with readable results
+    std::vector<std::vector<fm_contour>> contours;  // per (t*S+s), sorted
+    std::string err;
+};
+
+namespace {
+
+int fail(fm_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess) return fail(ctx, FM_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+// computeResizeAreaTab (OpenCV imgproc resize.cpp) restated on the product
+// side: for each destination index the weights over consecutive source
+// indices, in the order OpenCV accumulates them.
+bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A) {
+    A.n_dst = dsize;
+    std::vector<std::vector<std::pair<int, float>>> taps(dsize);
+    for (int dx = 0; dx < dsize; dx++) {
+        const double fsx1 = dx * scale, fsx2 = fsx1 + scale;
+        const double cell = std::min(scale, ssize - fsx1);
+        int sx1 = (int)std::ceil(fsx1), sx2 = (int)std::floor(fsx2);
+        sx2 = std::min(sx2, ssize - 1);
+        sx1 = std::min(sx1, sx2);
+        auto& t = taps[dx];
+        if (sx1 - fsx1 > 1e-3) t.emplace_back(sx1 - 1, (float)((sx1 - fsx1) / cell));
+        for (int sx = sx1; sx < sx2; sx++) t.emplace_back(sx, (float)(1.0 / cell));
+        if (fsx2 - sx2 > 1e-3) t.emplace_back(sx2, (float)(std::min(std::min(fsx2 - sx2, 1.), cell) / cell));
+    }
+    A.max_taps = 1;
+    for (auto& t : taps) A.max_taps = std::max<int>(A.max_taps, (int)t.size());
+    A.ofs.assign(dsize, 0);
+    A.cnt.assign(dsize, 0);
+    A.wt.assign((size_t)dsize * A.max_taps, 0.f);
+    for (int d = 0; d < dsize; d++) {
+        auto& t = taps[d];
+        if (t.empty()) return false;
+        A.ofs[d] = t[0].first;
+        A.cnt[d] = (int)t.size();
+        for (size_t j = 0; j < t.size(); j++) {
+            if (t[j].first != t[0].first + (int)j) return false;  // taps must be consecutive
+            A.wt[(size_t)d * A.max_taps + j] = t[j].second;
+        }
+    }
+    return true;
+}
+
+// getGaussianKernelBitExact + getGaussianKernelFixedPoint_ED (OpenCV imgproc
+// smooth.dispatch.cpp) restated: the 8-bit fixed-point taps GaussianBlur
+// uses for CV_8U with sigma = 0.
+bool gaussian_taps(int n, std::vector<int32_t>& out) {
+    if (n < 1 || (n & 1) == 0 || n > kMaxK) return false;
+    std::vector<double> kd(n);
+    switch (n) {
+        case 1: kd = {1.0}; break;
+        case 3: kd = {0.25, 0.5, 0.25}; break;
+        case 5: kd = {0.0625, 0.25, 0.375, 0.25, 0.0625}; break;
+        case 7: kd = {0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125}; break;
+        case 9: kd = {4 / 256., 13 / 256., 30 / 256., 51 / 256., 60 / 256., 51 / 256., 30 / 256., 13 / 256., 4 / 256.}; break;
+        default: {
+            const double sigma = std::fma((double)n, 0.15, 0.35);
+            const double scale2 = -0.125 / (sigma * sigma);
+            const int half = (n - 1) / 2;
+            std::vector<double> v(half);
+            double sum = 0;
+            for (int i = 0, x = 1 - n; i < half; i++, x += 2) {
+                v[i] = std::exp((double)(x * x) * scale2);
+                sum += v[i];
+            }
+            sum = sum * 2 + 1;
+            for (int i = 0; i < half; i++) kd[i] = kd[n - 1 - i] = v[i] / sum;
+            kd[half] = 1 / sum;
+        }
+    }
+    out.assign(n, 0);
+    const int half = n / 2;
+    double err = 0;
+    int64_t s = 0;
+    for (int i = 0; i < half; i++) {
+        const double adj = kd[i] * 256 + err;
+        const int64_t v0 = (int64_t)std::nearbyint(adj);
+        err = adj - (double)v0;
+        out[i] = out[n - 1 - i] = (int32_t)v0;
+        s += v0;
+    }
+    out[half] = (int32_t)(256 - 2 * s);
+    return true;
+}
+
+template <class T>
+int dalloc(fm_ctx* c, T** p, size_t count) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+    if (e != hipSuccess) return fail(c, FM_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+    return FM_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+int check_idle(fm_ctx* c) {
+    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
+    return FM_OK;
+}
+
+int check_frame(fm_ctx* c, int frame, int stream) {
+    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
+    if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
+    if (frame < 0 || frame >= c->ready) return fail(c, FM_EINVAL, "frame %d not in the last batch (%d frames)", frame, c->ready);
+    return FM_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// KernelTimer
+namespace fm {
+int KernelTimer::begin(const char* name) {
+    if (!enabled) return -1;
+    int id = -1;
+    for (size_t i = 0; i < names.size(); i++)
+        if (names[i] == name || std::strcmp(names[i], name) == 0) id = (int)i;
+    if (id < 0) {
+        names.push_back(name);
+        ms.push_back(0);
+        launches.push_back(0);
+        id = (int)names.size() - 1;
+    }
+    hipEvent_t a, b;
+    if (pool.size() >= 2) {
+        a = pool.back(); pool.pop_back();
+        b = pool.back(); pool.pop_back();
+    } else {
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
+    }
+    (void)hipEventRecord(a, stream);
+    pending.push_back({id, a, b});
+    return (int)pending.size() - 1;
+}
+void KernelTimer::end(int token) {
+    if (token < 0 || token >= (int)pending.size()) return;
+    (void)hipEventRecord(pending[token].b, stream);
+}
+void KernelTimer::collect() {
+    for (auto& r : pending) {
+        float t = 0;
+        if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+            ms[r.id] += t;
+            launches[r.id] += 1;
+        }
+        pool.push_back(r.a);
+        pool.push_back(r.b);
+    }
+    pending.clear();
+}
+void KernelTimer::reset() {
+    std::fill(ms.begin(), ms.end(), 0.0);
+    std::fill(launches.begin(), launches.end(), 0);
+}
+KernelTimer::~KernelTimer() {
+    for (auto& r : pending) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+}
+}  // namespace fm
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int fm_abi_version(void) { return FM_ABI_VERSION; }
+
+const char* fm_last_error(const fm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_last_error.c_str(); }
+
+int fm_create(fm_ctx** out, const fm_params* prm) {
+    if (!out || !prm) return fail(nullptr, FM_EINVAL, "null argument");
+    *out = nullptr;
+    const fm_params& p = *prm;
+    if (p.n_streams < 1 || p.src_w < 1 || p.src_h < 1 || p.box_size < 1 || p.max_batch < 1 || p.max_contours < 1)
+        return fail(nullptr, FM_EINVAL, "invalid geometry (streams %d, src %dx%d, box %d, batch %d, contours %d)",
+                    p.n_streams, p.src_w, p.src_h, p.box_size, p.max_batch, p.max_contours);
+    if (p.ksize < 1 || (p.ksize & 1) == 0 || p.ksize > kMaxK)
+        return fail(nullptr, FM_EINVAL, "ksize %d must be odd and in [1, %d]", p.ksize, kMaxK);
+    if (!(p.avg == p.avg)) return fail(nullptr, FM_EINVAL, "avg is NaN");
+
+    std::unique_ptr<fm_ctx> c(new fm_ctx());
+    c->p = p;
+    c->w = p.box_size;
+    c->h = (int)(p.src_h * ((double)p.box_size / (double)p.src_w));  // imutils.resize
+    if (c->h < 1) return fail(nullptr, FM_EINVAL, "work height is 0 (box %d, src %dx%d)", p.box_size, p.src_w, p.src_h);
+    if ((int64_t)c->h * c->w >= (1ll << 31) / 2) return fail(nullptr, FM_ENOTSUP, "work image too large");
+
+    // resize mode (cv::resize: copy if same size; INTER_AREA needs scale >= 1)
+    if (c->h == p.src_h && c->w == p.src_w) {
+        c->rmode = ResizeMode::Identity;
+    } else {
+        const double sx = 1. / ((double)c->w / p.src_w), sy = 1. / ((double)c->h / p.src_h);
+        if (!(sx >= 1 && sy >= 1))
+            return fail(nullptr, FM_ENOTSUP, "box_size %d > frame width %d: INTER_AREA upscaling is bilinear in OpenCV, not supported",
+                        p.box_size, p.src_w);
+        const int isx = (int)std::lrint(sx), isy = (int)std::lrint(sy);
+        if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16) {
+            c->rmode = ResizeMode::Fast;
+            c->fast_sx = isx;
+            c->fast_sy = isy;
+        } else {
+            c->rmode = ResizeMode::General;
+            if (!build_area_axis(p.src_w, c->w, sx, c->ax) || !build_area_axis(p.src_h, c->h, sy, c->ay))
+                return fail(nullptr, FM_ENOTSUP, "INTER_AREA table with non-consecutive taps");
+        }
+    }
+    if (!gaussian_taps(p.ksize, c->coef)) return fail(nullptr, FM_EINVAL, "bad ksize %d", p.ksize);
+    if (pixel_lds_bytes(p.ksize) > 160 * 1024) return fail(nullptr, FM_ENOTSUP, "ksize %d too large for the LDS tile", p.ksize);
+
+    fm_ctx* cp = c.get();
+    HIP_TRY(cp, hipSetDevice(p.device));
+    HIP_TRY(cp, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
+    c->timer.enabled = (p.flags & FM_FLAG_PROFILE) != 0;
+    c->timer.stream = c->stream;
+
+    const size_t S = p.n_streams, T = p.max_batch;
+    c->work_plane = (size_t)c->h * c->w;
+    c->src_frame_bytes = (size_t)p.src_h * p.src_w * 3;
+    const size_t frames = S * T, px = frames * c->work_plane;
+    int rc;
+    if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &c->d_work, px * 3))) return rc;
+    for (int i = 0; i < 2; i++)
+        if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
+    if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
+        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, px)) || (rc = dalloc(cp, &c->d_label, px)) ||
+        (rc = dalloc(cp, &c->d_cid, px)) || (rc = dalloc(cp, &c->d_outer, px)) || (rc = dalloc(cp, &c->d_count, frames)) ||
+        (rc = dalloc(cp, &c->d_rec, frames * p.max_contours * 5)))
+        return rc;
+    if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &c->d_planes, px * 3))) return rc;
+    HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
+    HIP_TRY(cp, hipMemset(c->d_bg[0], 0, S * c->work_plane * sizeof(double)));
+    HIP_TRY(cp, hipMemset(c->d_bg[1], 0, S * c->work_plane * sizeof(double)));
+    if (c->rmode == ResizeMode::General) {
+        auto up = [&](auto** d, const auto& v) -> int {
+            int r = dalloc(cp, d, v.size());
+            if (r) return r;
+            hipError_t e = hipMemcpy(*d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice);
+            return e == hipSuccess ? 0 : fail(cp, FM_EHIP, "hipMemcpy tables: %s", hipGetErrorString(e));
+        };
+        if ((rc = up(&c->d_xofs, c->ax.ofs)) || (rc = up(&c->d_xcnt, c->ax.cnt)) || (rc = up(&c->d_xwt, c->ax.wt)) ||
+            (rc = up(&c->d_yofs, c->ay.ofs)) || (rc = up(&c->d_ycnt, c->ay.cnt)) || (rc = up(&c->d_ywt, c->ay.wt)))
+            return rc;
+    }
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_init, S));
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_count, frames * sizeof(int32_t)));
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_rec, frames * p.max_contours * 5 * sizeof(int32_t)));
+    c->bg_init.assign(S, 0);
+    c->has_keep.assign(S, 0);
+    *out = c.release();
+    return FM_OK;
+}
+
+void fm_destroy(fm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->p.device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_in); dfree(c->d_work); dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep);
+    dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask); dfree(c->d_planes); dfree(c->d_label);
+    dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec);
+    dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
+    if (c->h_init) (void)hipHostFree(c->h_init);
+    if (c->h_count) (void)hipHostFree(c->h_count);
+    if (c->h_rec) (void)hipHostFree(c->h_rec);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int fm_work_size(const fm_ctx* c, int* h, int* w) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (h) *h = c->h;
+    if (w) *w = c->w;
+    return FM_OK;
+}
+
+int fm_set_mask(fm_ctx* c, int stream, const uint8_t* keep) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (int rc = check_idle(c)) return rc;
+    if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    const uint8_t flag = keep ? 1 : 0;
+    if (keep)
+        HIP_TRY(c, hipMemcpyAsync(c->d_keep + (size_t)stream * c->work_plane, keep, c->work_plane,
+                                  hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_has_keep + stream, &flag, 1, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->has_keep[stream] = flag;
+    return FM_OK;
+}
+
+int fm_reset_stream(fm_ctx* c, int stream) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (int rc = check_idle(c)) return rc;
+    if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
+    c->bg_init[stream] = 0;
+    return FM_OK;
+}
+
+int fm_set_hip_stream(fm_ctx* c, void* s) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (int rc = check_idle(c)) return rc;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->timer.stream = c->stream;
+    return FM_OK;
+}
+
+int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (int rc = check_idle(c)) return rc;
+    if (!frames || n < 1 || n > c->p.max_batch)
+        return fail(c, FM_EINVAL, "n_frames %d outside [1, max_batch=%d] or null frames", n, c->p.max_batch);
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    const int S = c->p.n_streams;
+    const size_t F = (size_t)n * S;
+    const uint8_t* src = frames;
+    if (!on_device) {
+        if (!c->d_in) {
+            int rc = dalloc(c, &c->d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
+            if (rc) return rc;
+        }
+        HIP_TRY(c, hipMemcpyAsync(c->d_in, frames, F * c->src_frame_bytes, hipMemcpyHostToDevice, c->stream));
+        src = c->d_in;
+    }
+    const uint8_t* work = src;
+    if (c->rmode == ResizeMode::General) {
+        int tok = c->timer.begin("resize_area");
+        HIP_TRY(c, launch_resize_area(c->stream, src, c->d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w,
+                                      c->d_xofs, c->d_xcnt, c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt,
+                                      c->d_ywt, c->ay.max_taps));
+        c->timer.end(tok);
+        work = c->d_work;
+    } else if (c->rmode == ResizeMode::Fast) {
+        int tok = c->timer.begin("resize_area_fast");
+        HIP_TRY(c, launch_resize_area_fast(c->stream, src, c->d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w,
+                                           c->fast_sx, c->fast_sy));
+        c->timer.end(tok);
+        work = c->d_work;
+    }
+    bool any_init = false;
+    for (int s = 0; s < S; s++) {
+        c->h_init[s] = c->bg_init[s] ? 0 : 1;
+        any_init |= c->h_init[s] != 0;
+    }
+    if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, c->h_init, S, hipMemcpyHostToDevice, c->stream));
+
+    PixelArgs a{};
+    a.bg = nullptr;
+    a.keep = c->d_keep;
+    a.has_keep = c->d_has_keep;
+    a.S = S;
+    a.h = c->h;
+    a.w = c->w;
+    a.ksize = c->p.ksize;
+    a.thresh = c->p.threshold;
+    a.alpha = c->p.avg;
+    a.beta = 1.0 - c->p.avg;
+    const long long npx = (long long)c->work_plane;
+    a.acc_vec_end = npx - npx % 16;
+    a.cvt_simd = npx >= 16;
+    for (int i = 0; i < c->p.ksize; i++) a.coef[i] = c->coef[i];
+    const size_t step_px = (size_t)S * c->work_plane;
+    for (int t = 0; t < n; t++) {
+        a.src = work + (size_t)t * step_px * 3;  // work image is [T][S][h][w][3] in every resize mode
+        a.init = (t == 0 && any_init) ? c->d_init : nullptr;
+        a.mask_out = c->d_mask + (size_t)t * step_px;
+        if (c->d_planes) {
+            a.gray_out = c->d_planes + (size_t)t * step_px;
+            a.blur_out = c->d_planes + F * c->work_plane + (size_t)t * step_px;
+            a.delta_out = c->d_planes + 2 * F * c->work_plane + (size_t)t * step_px;
+        }
+        int tok = c->timer.begin("pixel");
+        HIP_TRY(c, launch_pixel_pp(c->stream, a, c->d_bg[c->bg_cur], c->d_bg[c->bg_cur ^ 1]));
+        c->timer.end(tok);
+        c->bg_cur ^= 1;
+    }
+    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, F * sizeof(int32_t), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, F * c->work_plane, c->stream));
+    CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count, c->d_rec, (int)F, c->h, c->w, c->p.max_contours};
+    HIP_TRY(c, launch_ccl(c->stream, ca, &c->timer));
+    HIP_TRY(c, hipMemcpyAsync(c->h_count, c->d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_rec, c->d_rec, F * c->p.max_contours * 5 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    for (int s = 0; s < S; s++) c->bg_init[s] = 1;
+    c->pending = n;
+    c->ready = 0;
+    return FM_OK;
+}
+
+int fm_wait(fm_ctx* c) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (!c->pending) return FM_OK;
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        c->pending = 0;
+        return fail(c, FM_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    }
+    c->timer.collect();
+    const int n = c->pending, S = c->p.n_streams, cap = c->p.max_contours;
+    c->contours.assign((size_t)n * S, {});
+    for (size_t f = 0; f < (size_t)n * S; f++) {
+        const int cnt = std::min(c->h_count[f], cap);
+        auto& v = c->contours[f];
+        v.resize(cnt);
+        std::vector<std::pair<int32_t, int>> order(cnt);
+        const int32_t* r = c->h_rec + f * cap * 5;
+        for (int i = 0; i < cnt; i++) order[i] = {r[i * 5], i};
+        std::sort(order.begin(), order.end());
+        for (int i = 0; i < cnt; i++) {
+            const int32_t* q = r + order[i].second * 5;
+            fm_contour& o = v[i];
+            o.x = q[1];
+            o.y = q[2];
+            o.w = q[3] - q[1] + 1;
+            o.h = q[4] - q[2] + 1;
+            o.origin_x = q[0] % c->w;
+            o.origin_y = q[0] / c->w;
+            o.reserved0 = o.reserved1 = 0;
+        }
+    }
+    c->ready = n;
+    c->pending = 0;
+    return FM_OK;
+}
+
+int fm_get_counts(fm_ctx* c, int32_t* counts) {
+    if (!c || !counts) return fail(c, FM_EINVAL, "null argument");
+    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
+    std::memcpy(counts, c->h_count, (size_t)c->ready * c->p.n_streams * sizeof(int32_t));
+    return FM_OK;
+}
+
+int fm_get_contours(fm_ctx* c, int frame, int stream, fm_contour* out, int cap) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (int rc = check_frame(c, frame, stream)) return rc;
+    const size_t f = (size_t)frame * c->p.n_streams + stream;
+    const auto& v = c->contours[f];
+    const int m = out ? std::min<int>(cap, (int)v.size()) : 0;
+    for (int i = 0; i < m; i++) out[i] = v[i];
+    return c->h_count[f];
+}
+
+int fm_read_mask(fm_ctx* c, int frame, int stream, uint8_t* out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    if (int rc = check_frame(c, frame, stream)) return rc;
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    const size_t f = (size_t)frame * c->p.n_streams + stream;
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FM_OK;
+}
+
+int fm_read_plane(fm_ctx* c, int plane, int frame, int stream, uint8_t* out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    if (!c->d_planes) return fail(c, FM_ESTATE, "planes not kept: create with FM_FLAG_KEEP_PLANES");
+    if (plane < 0 || plane > 2) return fail(c, FM_EINVAL, "plane %d", plane);
+    if (int rc = check_frame(c, frame, stream)) return rc;
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    const size_t f = (size_t)frame * c->p.n_streams + stream;
+    const size_t Fcur = (size_t)c->ready * c->p.n_streams;
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_planes + ((size_t)plane * Fcur + f) * c->work_plane, c->work_plane,
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FM_OK;
+}
+
+int fm_read_background(fm_ctx* c, int stream, double* out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    if (int rc = check_idle(c)) return rc;
+    if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
+    if (!c->bg_init[stream]) return fail(c, FM_ESTATE, "stream %d has no background yet", stream);
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_bg[c->bg_cur] + (size_t)stream * c->work_plane, c->work_plane * sizeof(double),
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FM_OK;
+}
+
+int fm_write_background(fm_ctx* c, int stream, const double* in) {
+    if (!c || !in) return fail(c, FM_EINVAL, "null argument");
+    if (int rc = check_idle(c)) return rc;
+    if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    HIP_TRY(c, hipMemcpyAsync(c->d_bg[c->bg_cur] + (size_t)stream * c->work_plane, in, c->work_plane * sizeof(double),
+                              hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->bg_init[stream] = 1;
+    return FM_OK;
+}
+
+int fm_kernel_times(fm_ctx* c, const char** names, double* ms, int64_t* launches, int cap) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    const int n = (int)c->timer.names.size();
+    for (int i = 0; i < std::min(n, cap); i++) {
+        if (names) names[i] = c->timer.names[i];
+        if (ms) ms[i] = c->timer.ms[i];
+        if (launches) launches[i] = c->timer.launches[i];
+    }
+    return n;
+}
+
+int fm_reset_kernel_times(fm_ctx* c) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    c->timer.reset();
+    return FM_OK;
+}
+
+}  // extern "C"

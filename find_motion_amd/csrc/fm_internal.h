@@ -1,0 +1,86 @@
+// fm_internal.h — shared declarations between the C ABI (fm_capi.cpp) and the
+// gfx950 kernels (fm_kernels.hip).  Not part of the public boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/find_motion_amd.h"
+
+namespace fm {
+
+constexpr int kMaxK = 255;        // largest Gaussian size handled by the tiled kernel
+constexpr int kCclBlock = 32;     // CCL block edge (pixels)
+
+// Host-built INTER_AREA tables (computeResizeAreaTab restated in fm_capi.cpp).
+// Per destination index d: taps start at src index ofs[d], cnt[d] taps, weights
+// wt[d * max_taps + j] (float32 exactly as OpenCV stores DecimateAlpha::alpha).
+struct AreaAxis {
+    int n_dst = 0, max_taps = 0;
+    std::vector<int32_t> ofs, cnt;
+    std::vector<float> wt;
+};
+
+// Everything the per-frame pixel kernel needs for one batch step.
+struct PixelArgs {
+    const uint8_t* src;          // work-size BGR for this batch frame t: [S][h][w][3]
+    double* bg;                  // [S][h*w]
+    const uint8_t* keep;         // [S][h*w] (only read where has_keep[s])
+    const uint8_t* has_keep;     // [S]
+    const uint8_t* init;         // [S] 1 => bg := blur before the diff (first frame), or nullptr
+    uint8_t* mask_out;           // dilated threshold [S][h*w]
+    uint8_t* gray_out;           // optional planes [S][h*w] (nullptr when not kept)
+    uint8_t* blur_out;
+    uint8_t* delta_out;
+    int S, h, w;
+    int ksize;
+    int thresh;
+    double alpha, beta;          // beta = 1 - alpha
+    long long acc_vec_end;       // h*w - (h*w % 16): AVX2 fma body vs scalar tail
+    int cvt_simd;                // h*w >= 16: f64->f32->rne path of convertScaleAbs
+    int32_t coef[kMaxK];         // fixed-point Gaussian taps (sum 256)
+};
+
+struct CclArgs {
+    const uint8_t* mask;         // [F][h*w]
+    int32_t* label;              // [F][h*w]
+    uint8_t* outer;              // [F][h*w]
+    int32_t* cid;                // [F][h*w]
+    int32_t* count;              // [F]
+    int32_t* rec;                // [F][cap][5]: first, minx, miny, maxx, maxy
+    int F, h, w, cap;
+};
+
+// Kernel launchers (fm_kernels.hip).  All asynchronous on `st`.
+hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
+                              int h, int w, const int32_t* xofs, const int32_t* xcnt, const float* xwt,
+                              int xtaps, const int32_t* yofs, const int32_t* ycnt, const float* ywt,
+                              int ytaps);
+hipError_t launch_resize_area_fast(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
+                                   int h, int w, int sx, int sy);
+hipError_t launch_pixel(hipStream_t st, const PixelArgs& a);
+struct KernelTimer;
+hipError_t launch_ccl(hipStream_t st, const CclArgs& a, KernelTimer* timer);
+
+// Optional per-kernel event timing (FM_FLAG_PROFILE): events are recorded on
+// the launch stream around each kernel and read back after the stream syncs.
+struct KernelTimer {
+    bool enabled = false;
+    hipStream_t stream = nullptr;
+    struct Rec { int id; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    std::vector<const char*> names;
+    std::vector<double> ms;
+    std::vector<int64_t> launches;
+    int begin(const char* name);   // returns a token for end(), -1 when disabled
+    void end(int token);
+    void collect();                // after the stream has synchronised
+    void reset();
+    ~KernelTimer();
+};
+
+}  // namespace fm

@@ -1,0 +1,145 @@
+/*
+ * find_motion_amd.h — C ABI of the MI355X motion-detection hot path.
+ *
+ * The reference (dmiruke/find_motion, find_motion/find_motion.py = "fm.py")
+ * has no FFI: its hot path is a chain of cv2 calls made from three
+ * VideoMotion methods in the frame loop (fm.py:866-868):
+ *
+ *   blur_frame()      fm.py:487-494  imutils.resize -> cvtColor -> GaussianBlur
+ *   mask_off_areas()  fm.py:619-636  rectangle / fillConvexPoly onto frame.blur
+ *   find_diff()       fm.py:638-662  convertScaleAbs+absdiff, threshold,
+ *                                    accumulateWeighted, dilate, findContours
+ *
+ * This header is the boundary a binding (ctypes / cffi / pybind11) would bind
+ * to replace those three methods; find_motion_amd/motion.py is that binding.
+ * Every entry point is a plain C function over plain pointers and sizes.
+ * Status codes: 0 = OK, negative = error (see FM_E*); fm_last_error() gives
+ * the message.  No C++ exception crosses this boundary.
+ *
+ * Threading: one fm_ctx per host thread; contexts are independent and bound
+ * to one HIP device (one process per GPU in the multi-GPU runner).
+ */
+#ifndef FIND_MOTION_AMD_H
+#define FIND_MOTION_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FM_ABI_VERSION 1
+
+/* status codes */
+#define FM_OK 0
+#define FM_EINVAL -1   /* bad argument */
+#define FM_EHIP -2     /* HIP runtime error */
+#define FM_ENOMEM -3   /* allocation failed */
+#define FM_ESTATE -4   /* call out of order (e.g. results before fm_wait) */
+#define FM_ENOTSUP -5  /* configuration outside the restated OpenCV path */
+
+/* fm_params.flags */
+#define FM_FLAG_KEEP_PLANES 0x1u /* keep gray/blur/frame_delta per frame (show/debug, fm.py:907-926) */
+#define FM_FLAG_PROFILE 0x2u     /* time every kernel launch with HIP events */
+
+/* planes for fm_read_plane */
+#define FM_PLANE_GRAY 0  /* VideoFrame.gray        (fm.py:493) */
+#define FM_PLANE_BLUR 1  /* VideoFrame.blur, masked (fm.py:494, 619-636) */
+#define FM_PLANE_DELTA 2 /* VideoFrame.frame_delta (fm.py:250) */
+
+typedef struct fm_ctx fm_ctx;
+
+/* Construction parameters: the VideoMotion constructor arguments that reach
+ * the hot path (fm.py:299-307) plus the batch geometry. */
+typedef struct fm_params {
+    int device;       /* HIP device ordinal */
+    int n_streams;    /* independent videos/cameras, one background model each */
+    int src_w, src_h; /* decoded frame size (fm.py:433-435) */
+    int box_size;     /* -B / box_size: processing width (fm.py:492, 1474) */
+    int ksize;        /* odd Gaussian size from _make_gaussian (fm.py:478-484) */
+    int threshold;    /* -t / threshold (fm.py:256, 1476) */
+    double avg;       /* -a / avg, accumulateWeighted alpha (fm.py:659, 1479) */
+    int max_batch;    /* max frames per stream per fm_submit */
+    int max_contours; /* capacity of the per-frame contour records */
+    unsigned flags;   /* FM_FLAG_* */
+} fm_params;
+
+/* One external contour (an element of VideoFrame.contours, fm.py:269-276). */
+typedef struct fm_contour {
+    int32_t x, y, w, h;          /* cv2.boundingRect (fm.py:792) */
+    int32_t origin_x, origin_y;  /* border start = raster-first pixel of the component */
+    int32_t reserved0, reserved1;
+} fm_contour;
+
+/* Library version (FM_ABI_VERSION) */
+int fm_abi_version(void);
+
+/* Create / destroy a context.  Allocates all device state. */
+int fm_create(fm_ctx** out, const fm_params* params);
+void fm_destroy(fm_ctx* ctx);
+
+/* Last error message for ctx (or the calling thread's last error if ctx is NULL). */
+const char* fm_last_error(const fm_ctx* ctx);
+
+/* Working image size (h = int(src_h * box/src_w), w = box; imutils rule, fm.py:492). */
+int fm_work_size(const fm_ctx* ctx, int* h, int* w);
+
+/* Static keep-mask for one stream: h*w bytes, 0 = masked off (mask_off_areas,
+ * fm.py:619-636, rasterised once per video).  NULL clears the mask. */
+int fm_set_mask(fm_ctx* ctx, int stream, const uint8_t* keep_hw);
+
+/* Forget the background model: the next frame re-initialises it
+ * (VideoMotion.ref_frame = None, fm.py:414, 651-652). */
+int fm_reset_stream(fm_ctx* ctx, int stream);
+
+/* Run the hot path on n_frames consecutive frames of every stream.
+ * frames: BGR u8, layout [n_frames][n_streams][src_h][src_w][3], C-contiguous;
+ * host memory (on_device = 0, copied with hipMemcpyAsync) or device memory
+ * (on_device = 1, read in place).  Asynchronous: host buffers must stay valid
+ * until fm_wait returns. */
+int fm_submit(fm_ctx* ctx, const uint8_t* frames, int n_frames, int on_device);
+
+/* Wait for the last submit; makes its results readable. */
+int fm_wait(fm_ctx* ctx);
+
+/* External-contour counts of the last batch, layout [n_frames][n_streams]
+ * (len(VideoFrame.contours), the quantity find_movement counts, fm.py:674-695). */
+int fm_get_counts(fm_ctx* ctx, int32_t* counts);
+
+/* Contours of one (frame, stream) of the last batch, in raster order of their
+ * start pixels.  Returns the count (records written: min(count, cap)). */
+int fm_get_contours(fm_ctx* ctx, int frame, int stream, fm_contour* out, int cap);
+
+/* Dilated threshold mask (VideoFrame.thresh after find_contours, fm.py:266), h*w bytes. */
+int fm_read_mask(fm_ctx* ctx, int frame, int stream, uint8_t* out);
+
+/* gray / blur / frame_delta planes (needs FM_FLAG_KEEP_PLANES), h*w bytes. */
+int fm_read_plane(fm_ctx* ctx, int plane, int frame, int stream, uint8_t* out);
+
+/* Background model (VideoMotion.ref_frame, float64, fm.py:652, 659), h*w doubles. */
+int fm_read_background(fm_ctx* ctx, int stream, double* out);
+int fm_write_background(fm_ctx* ctx, int stream, const double* in);
+
+/* Launch on the caller's HIP stream (hipStream_t) instead of the context's own
+ * stream; NULL restores the context stream. */
+int fm_set_hip_stream(fm_ctx* ctx, void* hip_stream);
+
+/* FM_FLAG_PROFILE: per-kernel accumulated device time since the last reset.
+ * names[i] (static strings), ms[i], launches[i] for i < returned count. */
+int fm_kernel_times(fm_ctx* ctx, const char** names, double* ms, int64_t* launches, int cap);
+int fm_reset_kernel_times(fm_ctx* ctx);
+
+/* Rasterise mask polygons to a keep-mask (mask_off_areas, fm.py:611-636):
+ * each polygon's points are scaled by int(v * scale) (scale_area, fm.py:616);
+ * 2 points -> filled rectangle (cv2.rectangle FILLED), >= 3 points ->
+ * cv2.fillConvexPoly.  xy: all points (x0,y0,x1,y1,...), npts: points per
+ * polygon.  keep (h*w) is set to 1 everywhere, then 0 inside the polygons. */
+int fm_rasterize_masks(int h, int w, double scale, const int32_t* xy, const int32_t* npts,
+                       int n_polys, uint8_t* keep);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FIND_MOTION_AMD_H */

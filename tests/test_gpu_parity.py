@@ -1,0 +1,113 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): threshold/dilate masks bit-exact, background
+within 1e-4 (it is in fact compared exactly here), contour count exact and
+bounding boxes exact (the bar allows +-1 px).  Frames are the seeded
+synthetic streams of find_motion_amd.synthetic; sizes are chosen so the
+oracle finishes in seconds.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from find_motion_amd import MotionEngine, make_gaussian, rasterize_masks
+from find_motion_amd._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY
+from find_motion_amd.synthetic import batch
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pair(W, H, box, blur_scale=20, ksize=None, S=1, T=3, n_batches=2, thresh=12, alpha=0.1,
+             masks=None, keep_planes=True, start=0, frames=None):
+    k = ksize if ksize is not None else make_gaussian(box, blur_scale)
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=thresh, avg=alpha,
+                       max_batch=T, keep_planes=keep_planes)
+    h, w = eng.work_shape
+    cfg = oracle.OracleConfig(H=H, W=W, box=box, ksize=k, thresh=thresh, alpha=alpha)
+    assert (cfg.h, cfg.w) == (h, w)
+    keeps = [None] * S
+    if masks:
+        for s in range(S):
+            keeps[s] = rasterize_masks(h, w, box / W, masks)
+            eng.set_mask(s, keeps[s])
+    orc = [oracle.OracleStream(cfg, keeps[s]) for s in range(S)]
+    for b in range(n_batches):
+        fr = frames[b] if frames is not None else batch(W, H, S, start + b * T, T)
+        eng.submit(fr)
+        eng.wait()
+        counts = eng.counts()
+        for t in range(fr.shape[0]):
+            for s in range(S):
+                ref = orc[s].step(fr[t, s])
+                tag = f"batch {b} frame {t} stream {s}"
+                if keep_planes:
+                    np.testing.assert_array_equal(eng.plane(PLANE_GRAY, t, s), ref["gray"], err_msg="gray " + tag)
+                    np.testing.assert_array_equal(eng.plane(PLANE_BLUR, t, s), ref["blur"], err_msg="blur " + tag)
+                    np.testing.assert_array_equal(eng.plane(PLANE_DELTA, t, s), ref["delta"], err_msg="delta " + tag)
+                np.testing.assert_array_equal(eng.mask(t, s), ref["mask"], err_msg="mask " + tag)
+                assert counts[t, s] == ref["count"], tag
+                got = [c.bbox for c in eng.contours(t, s)]
+                assert got == ref["boxes"], tag
+                assert [c.origin for c in eng.contours(t, s)] == ref["origins"], tag
+        for s in range(S):
+            bg = eng.background(s)
+            np.testing.assert_allclose(bg, orc[s].bg, rtol=0, atol=1e-4)
+            assert np.array_equal(bg, orc[s].bg), "background not bit-identical"
+    eng.close()
+
+
+def test_mode_f_small():
+    run_pair(160, 120, 160, blur_scale=32)  # k=5
+
+
+def test_mode_d_640x480_config1():
+    run_pair(640, 480, 100)  # 75x100, k=5: configs[0] geometry
+
+
+def test_mode_d_1080p():
+    run_pair(1920, 1080, 100, T=4, n_batches=2)
+
+
+def test_mode_f_1080p_k5():
+    run_pair(1920, 1080, 1920, blur_scale=384, T=2, n_batches=2)
+
+
+def test_fast_area_2x_and_4x():
+    run_pair(160, 120, 80, blur_scale=20)   # 2x2 integer path, k=5
+    run_pair(160, 120, 40, blur_scale=10)   # 4x4 integer path, k=5
+
+
+def test_odd_sizes_and_large_k():
+    run_pair(37, 23, 37, ksize=21)          # k larger than the image: REFLECT_101 repeats
+    run_pair(101, 67, 101, ksize=9)
+    run_pair(7, 5, 7, ksize=3)              # < 16 pixels: scalar convertScaleAbs / accumulate tails
+
+
+def test_multi_stream_masks():
+    masks = [((0, 0), (60, 40)), ((150, 110), (110, 119), (159, 80))]
+    run_pair(160, 120, 160, blur_scale=32, S=3, T=2, masks=masks)
+
+
+def test_4k_k21_masks_config5_geometry():
+    masks = [((0, 0), (639, 359)), ((3839, 2159), (3200, 2159), (3839, 1600))]
+    run_pair(3840, 2160, 3840, blur_scale=183, T=1, n_batches=2, masks=masks, keep_planes=False)
+
+
+def test_thresholds_and_alpha():
+    run_pair(160, 120, 160, blur_scale=32, thresh=0, alpha=0.5)
+    run_pair(160, 120, 160, blur_scale=32, thresh=-1, alpha=0.02)
+    run_pair(160, 120, 160, blur_scale=32, thresh=255, alpha=1.0)
+
+
+def test_random_masks_contours():
+    """Random binary-ish content with holes and nesting: stresses the CCL external test."""
+    rng = np.random.default_rng(5)
+    H, W = 96, 128
+    fr = []
+    for b in range(3):
+        f = np.zeros((2, 1, H, W, 3), np.uint8)
+        for t in range(2):
+            img = (rng.random((H, W)) < 0.35).astype(np.uint8) * 255
+            f[t, 0] = img[..., None]
+        fr.append(f)
+    run_pair(W, H, W, ksize=1, T=2, n_batches=3, thresh=20, alpha=0.5, frames=fr)
