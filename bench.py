@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py — frames/s of the MI355X motion hot path on synthetic 1080p.
+
+Workload (BASELINE.json configs[1]): one 1080p stream per GPU through the
+fused pixel kernel in "mode F" (-B 1920 -b 384: box = frame width, 5x5
+Gaussian), the reference's CLI defaults otherwise (-t 12 -a 0.1).  A "step"
+is one fm_submit + fm_wait of --batch consecutive frames per stream, read
+from a device-resident ring of synthetic frames (the background model keeps
+evolving across the ring).  Multi-GPU: one process per GPU (torchrun), each
+on its own streams; no collective on the data path (the reference's only
+parallelism is one video per worker, find_motion.py:1071-1075).  RCCL is used
+only for the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line on rank 0 (driver contract), with a "roofline" object
+for the dominant kernel (HIP-event timing inside the library, on the stream
+the kernels run on) and a "cpu_baseline" object (the C restatement in
+oracle/, OpenMP, one thread per stream, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "frames/sec on 1080p synthetic video at 1/2/4/8 MI355X; achieved HBM GB/s %peak"
+
+
+def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
+    """Algorithmic HBM bytes of ONE launch of `kernel` (DESIGN.md 'Kernels')."""
+    S, T = cfg["streams_per_gpu"], cfg["frames_per_step"]
+    H, W, h, w = cfg["H"], cfg["W"], cfg["h"], cfg["w"]
+    if kernel == "pixel":
+        # one launch = one frame of every stream: BGR read 3 B + mask write 1 B + f64 background r/w 16 B
+        return S * h * w * (3 + 1 + 16)
+    if kernel in ("resize_area", "resize_area_fast"):
+        return S * T * (H * W * 3 + h * w * 3)
+    return None
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg: dict, frames_host: np.ndarray, n_frames: int) -> dict:
+    """The oracle (C restatement, not OpenCV) on a bounded sample of the same workload."""
+    import oracle
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    ocfg = oracle.OracleConfig(H=cfg["H"], W=cfg["W"], box=cfg["box"], ksize=cfg["ksize"],
+                               thresh=cfg["threshold"], alpha=cfg["avg"])
+    seq = np.ascontiguousarray(frames_host[:n_frames])
+    oracle.run_streams(ocfg, seq[:2], threads, n_streams=threads)  # warm-up (page-in, OpenMP pool)
+    t0 = time.perf_counter()
+    _, used = oracle.run_streams(ocfg, seq, threads, n_streams=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(threads * n_frames / dt, 2), "unit": "frames/s", "cores": used, "kind": "port",
+            "sample": f"{threads} streams x {n_frames} frames {cfg['W']}x{cfg['H']} box {cfg['box']} k {cfg['ksize']}, "
+                      f"C restatement of the OpenCV chain (oracle/fm_oracle.c, -O2, one OpenMP thread per stream; "
+                      f"not OpenCV, which is not installed), {dt:.2f}s wall, CPU: {cpu_model()}"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=["F", "D"], default="F",
+                    help="F: -B 1920 -b 384 (full-resolution fused kernel); D: reference default -B 100 -b 20")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
+    ap.add_argument("--batch", type=int, default=16, help="frames per stream per step")
+    ap.add_argument("--ring", type=int, default=32, help="device-resident frames per stream")
+    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from find_motion_amd import MotionEngine, make_gaussian, work_height
+    from find_motion_amd.synthetic import SyntheticVideo
+
+    W, H = args.width, args.height
+    box, blur_scale = (W, W // 5) if args.mode == "F" else (100, 20)
+    if args.mode == "F" and W == 1920:
+        blur_scale = 384
+    k = make_gaussian(box, blur_scale)
+    S, T = args.streams, args.batch
+    R = max(args.ring - args.ring % T, T)
+    cfg = {"workload": f"configs[1]: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
+                       f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring",
+           "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
+           "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
+
+    # synthetic ring [R][S][H][W][3], distinct streams per rank
+    vids = [SyntheticVideo(W, H, stream=rank * S + s) for s in range(S)]
+    host = np.empty((R, S, H, W, 3), np.uint8)
+    for t in range(R):
+        for s in range(S):
+            host[t, s] = vids[s].frame(t)
+    ring = torch.from_numpy(host).to(f"cuda:{local}")
+    frame_bytes = S * H * W * 3
+
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
+                       max_batch=T, max_contours=1 << 14, profile=True, device=local)
+    base = ring.data_ptr()
+    n_batches = R // T
+
+    def step(i: int) -> None:
+        eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
+        eng.wait()
+
+    for i in range(args.warmup):
+        step(i)
+    eng.reset_kernel_times()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    ktimes = eng.kernel_times()
+    total_frames = world * S * T * args.steps
+    value = total_frames / elapsed
+
+    # roofline of the dominant kernel
+    dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+    roof = None
+    kernels = {}
+    for name, (ms, n) in ktimes.items():
+        kernels[name] = {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3)}
+    if dom is not None:
+        ms, n = ktimes[dom]
+        avg_s = ms / 1e3 / max(n, 1)
+        nbytes = algorithmic_bytes(dom, cfg)
+        if nbytes is not None and avg_s > 0:
+            ach = nbytes / avg_s / 1e9
+            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3)}
+
+    # measured device copy peak (for reference beside the spec)
+    try:
+        a = torch.empty(1 << 28, dtype=torch.uint8, device=f"cuda:{local}")
+        b = torch.empty_like(a)
+        for _ in range(3):
+            b.copy_(a)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        copy_gbs = 10 * 2 * a.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9
+        if roof is not None:
+            roof["copy_peak_measured"] = round(copy_gbs, 1)
+        del a, b
+    except Exception:
+        pass
+
+    if args.host_fed:
+        host_batch = np.ascontiguousarray(host[:T])
+        t0 = time.perf_counter()
+        for _ in range(5):
+            eng.submit(host_batch)
+            eng.wait()
+        hf = 5 * S * T / (time.perf_counter() - t0)
+        print(f"[bench] host-fed (pageable H2D inclusive) frames/s per GPU: {hf:.1f}", file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, host.reshape(R * S, H, W, 3), min(args.cpu_frames, R * S))
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
+               "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kernels}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

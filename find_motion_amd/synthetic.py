@@ -3,7 +3,7 @@
 No video files or decoders are available offline, so streams are generated:
 a static per-stream gradient background, U[-3,3] per-pixel noise, four
 bouncing filled rectangles, a +-2 level illumination drift over 120 frames
-and a 3-frame full-frame flash every 97 frames.  Frames are BGR uint8
+and a 3-frame full-frame flash every 97 frames (frames 94-96 mod 97).  Frames are BGR uint8
 HWC C-contiguous, the layout cv2.VideoCapture.read returns (fm.py:501).
 Any frame can be generated independently (random access by index).
 """
@@ -48,7 +48,7 @@ class SyntheticVideo:
         img = self.background.copy()
         drift = int(round(2 * np.sin(2 * np.pi * i / 120.0)))
         img += drift
-        if i % 97 in (0, 1, 2) and i > 0:
+        if i % 97 >= 94:  # frames 94-96, 191-193, ...: 3-frame flash every 97 frames
             img += 60
         for (ow, oh, col, x0, y0, vx, vy) in self.objects:
             x = _bounce(x0, vx, i, self.W - ow)

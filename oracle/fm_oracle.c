@@ -492,9 +492,10 @@ int fmo_process_frame(const fmo_cfg* c, const uint8_t* bgr, const uint8_t* keep,
 
 /* CPU baseline: S independent streams x F frames, one OpenMP thread per      */
 /* stream (mirrors run_pool's one-video-per-worker, fm.py:1071-1075).          */
-/* frames layout [S][F][H][W][3]; counts [S][F].  Returns threads used.        */
+/* frames layout [S][F][H][W][3], or [F][H][W][3] shared by every stream when  */
+/* shared != 0; counts [S][F].  Returns threads used.                         */
 int fmo_run_streams(const fmo_cfg* c, const uint8_t* frames, int S, int F, int nthreads,
-                    int32_t* counts)
+                    int32_t* counts, int shared)
 {
     int used = 1;
 #ifdef _OPENMP
@@ -512,7 +513,7 @@ int fmo_run_streams(const fmo_cfg* c, const uint8_t* frames, int S, int F, int n
         int init = 0;
         int32_t rec[7 * 64];
         for (int f = 0; f < F; f++) {
-            const uint8_t* fr = frames + ((size_t)s * F + f) * (size_t)c->H * c->W * 3;
+            const uint8_t* fr = frames + ((size_t)(shared ? 0 : s) * F + f) * (size_t)c->H * c->W * 3;
             counts[(size_t)s * F + f] = fmo_process_frame(c, fr, 0, bg, &init, 0, 0, 0, 0, rec, 0, 64);
         }
         free(bg);

@@ -50,7 +50,7 @@ def lib():
             C.c_void_p, u8p, C.c_void_p, f64p, C.POINTER(C.c_int),
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, i32p, f64p, C.c_int,
         ]
-        L.fmo_run_streams.argtypes = [C.c_void_p, u8p, C.c_int, C.c_int, C.c_int, i32p]
+        L.fmo_run_streams.argtypes = [C.c_void_p, u8p, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
         _lib = L
     return _lib
 
@@ -213,10 +213,16 @@ class OracleStream:
                 "boxes": boxes, "origins": origins, "areas": areas[: min(n, cap)].copy()}
 
 
-def run_streams(cfg: OracleConfig, frames: np.ndarray, nthreads: int = 0):
-    """CPU baseline: frames [S][F][H][W][3]; one thread per stream. Returns (counts[S][F], threads)."""
-    S, F = frames.shape[:2]
+def run_streams(cfg: OracleConfig, frames: np.ndarray, nthreads: int = 0, n_streams: int | None = None):
+    """CPU baseline, one thread per stream.  frames [S][F][H][W][3], or
+    [F][H][W][3] replayed by each of n_streams streams.  Returns (counts[S][F], threads)."""
+    shared = frames.ndim == 4
+    if shared:
+        S, F = int(n_streams or 1), frames.shape[0]
+    else:
+        S, F = frames.shape[:2]
     counts = np.zeros((S, F), np.int32)
     c = cfg._c()
-    used = lib().fmo_run_streams(C.byref(c), np.ascontiguousarray(frames), S, F, int(nthreads), counts)
+    used = lib().fmo_run_streams(C.byref(c), np.ascontiguousarray(frames), S, F, int(nthreads), counts,
+                                 1 if shared else 0)
     return counts, int(used)
