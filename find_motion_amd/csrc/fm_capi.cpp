@@ -56,7 +56,15 @@ struct fm_ctx {
     int32_t* d_cid = nullptr;
     uint8_t* d_outer = nullptr;
     int32_t* d_count = nullptr;
-    int32_t* d_rec = nullptr;
+    int32_t* d_rec = nullptr;       // device alias of h_rec (mapped)
+    int32_t* d_rec_dev = nullptr;   // device-resident records for the pixel-level CCL (uses atomics)
+    // tile-summary CCL (fused path)
+    bool use_fused = false;
+    int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;
+    TileRec* d_tiles = nullptr;
+    uint64_t* d_bits = nullptr;
+    NodeRec* d_nodes = nullptr;
+    int32_t* h_overflow = nullptr;  // pinned [T*S]
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
     float *d_xwt = nullptr, *d_ywt = nullptr;
 
@@ -312,9 +320,29 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
-        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, px)) || (rc = dalloc(cp, &c->d_label, px)) ||
-        (rc = dalloc(cp, &c->d_cid, px)) || (rc = dalloc(cp, &c->d_outer, px)) || (rc = dalloc(cp, &c->d_count, frames)) ||
-        (rc = dalloc(cp, &c->d_rec, frames * p.max_contours * 5)))
+        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, px)) ||
+        (rc = dalloc(cp, &c->d_count, 2 * frames)))
+        return rc;
+    // contour records: mapped pinned host memory written directly by the
+    // kernels (only the records that exist cross PCIe; no D2H copy of the
+    // capacity-sized buffer)
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
+    HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
+    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024;
+    if (c->use_fused) {
+        c->ntx = (c->w + 63) / 64;
+        c->nty = (c->h + 63) / 64;
+        c->ntiles = c->ntx * c->nty;
+        c->nnodes = c->ntiles * kTileMaxRuns;
+        if ((rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64)) || (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
+            return rc;
+    }
+    // pixel-level CCL buffers: the whole batch on the v1 path, one frame for the
+    // fused path's overflow fallback
+    const size_t ccl_px = c->use_fused ? c->work_plane : px;
+    if ((rc = dalloc(cp, &c->d_label, ccl_px)) || (rc = dalloc(cp, &c->d_cid, ccl_px)) ||
+        (rc = dalloc(cp, &c->d_outer, ccl_px)) ||
+        (rc = dalloc(cp, &c->d_rec_dev, (c->use_fused ? 1 : frames) * (size_t)p.max_contours * 5)))
         return rc;
     if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &c->d_planes, px * 3))) return rc;
     HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
@@ -333,7 +361,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     }
     HIP_TRY(cp, hipHostMalloc((void**)&c->h_init, S));
     HIP_TRY(cp, hipHostMalloc((void**)&c->h_count, frames * sizeof(int32_t)));
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_rec, frames * p.max_contours * 5 * sizeof(int32_t)));
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_overflow, frames * sizeof(int32_t)));
     c->bg_init.assign(S, 0);
     c->has_keep.assign(S, 0);
     *out = c.release();
@@ -347,7 +375,9 @@ void fm_destroy(fm_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_in); dfree(c->d_work); dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep);
     dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask); dfree(c->d_planes); dfree(c->d_label);
-    dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec);
+    dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec_dev); c->d_rec = nullptr;
+    dfree(c->d_tiles); dfree(c->d_bits); dfree(c->d_nodes);
+    if (c->h_overflow) (void)hipHostFree(c->h_overflow);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     if (c->h_init) (void)hipHostFree(c->h_init);
     if (c->h_count) (void)hipHostFree(c->h_count);
@@ -433,6 +463,43 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     }
     if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, c->h_init, S, hipMemcpyHostToDevice, c->stream));
 
+    const long long npx = (long long)c->work_plane;
+    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, 2 * F * sizeof(int32_t), c->stream));
+    if (c->use_fused) {
+        FusedArgs fa{};
+        fa.src = work;
+        fa.bg_in = c->d_bg[c->bg_cur];
+        fa.bg_out = c->d_bg[c->bg_cur ^ 1];
+        fa.keep = c->d_keep;
+        fa.has_keep = c->d_has_keep;
+        fa.init = any_init ? c->d_init : nullptr;
+        fa.mask_out = c->d_mask;
+        fa.planes = c->d_planes;
+        fa.bits = c->d_bits;
+        fa.tiles = c->d_tiles;
+        fa.nodes = c->d_nodes;
+        fa.count = c->d_count;
+        fa.rec = c->d_rec;
+        fa.T = n;
+        fa.S = S;
+        fa.h = c->h;
+        fa.w = c->w;
+        fa.ksize = c->p.ksize;
+        fa.thresh = c->p.threshold;
+        fa.ntx = c->ntx;
+        fa.nty = c->nty;
+        fa.ntiles = c->ntiles;
+        fa.nnodes = c->nnodes;
+        fa.cap = c->p.max_contours;
+        fa.cvt_simd = npx >= 16;
+        fa.alpha = c->p.avg;
+        fa.beta = 1.0 - c->p.avg;
+        fa.acc_vec_end = npx - npx % 16;
+        for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
+        HIP_TRY(c, launch_fused(c->stream, fa, &c->timer));
+        c->bg_cur ^= 1;
+        HIP_TRY(c, hipMemcpyAsync(c->h_overflow, c->d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    } else {
     PixelArgs a{};
     a.bg = nullptr;
     a.keep = c->d_keep;
@@ -444,7 +511,6 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     a.thresh = c->p.threshold;
     a.alpha = c->p.avg;
     a.beta = 1.0 - c->p.avg;
-    const long long npx = (long long)c->work_plane;
     a.acc_vec_end = npx - npx % 16;
     a.cvt_simd = npx >= 16;
     for (int i = 0; i < c->p.ksize; i++) a.coef[i] = c->coef[i];
@@ -463,13 +529,14 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         c->timer.end(tok);
         c->bg_cur ^= 1;
     }
-    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, F * sizeof(int32_t), c->stream));
     HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, F * c->work_plane, c->stream));
-    CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count, c->d_rec, (int)F, c->h, c->w, c->p.max_contours};
+    CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count, c->d_rec_dev, (int)F, c->h, c->w, c->p.max_contours};
     HIP_TRY(c, launch_ccl(c->stream, ca, &c->timer));
-    HIP_TRY(c, hipMemcpyAsync(c->h_count, c->d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->h_rec, c->d_rec, F * c->p.max_contours * 5 * sizeof(int32_t), hipMemcpyDeviceToHost,
+    HIP_TRY(c, hipMemcpyAsync(c->h_rec, c->d_rec_dev, F * c->p.max_contours * 5 * sizeof(int32_t), hipMemcpyDeviceToHost,
                               c->stream));
+    std::memset(c->h_overflow, 0, F * sizeof(int32_t));
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->h_count, c->d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     for (int s = 0; s < S; s++) c->bg_init[s] = 1;
     c->pending = n;
     c->ready = 0;
@@ -484,6 +551,27 @@ int fm_wait(fm_ctx* c) {
     if (e != hipSuccess) {
         c->pending = 0;
         return fail(c, FM_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    }
+    {
+        // Fused path: a tile with more runs than kTileMaxRuns cannot come from a
+        // dilated mask (<= 24 runs per 64-px row), but if it ever happens the
+        // frame is relabelled on the GPU by the pixel-level CCL.
+        const size_t F = (size_t)c->pending * c->p.n_streams;
+        bool redo = false;
+        for (size_t f = 0; f < F; f++) {
+            if (!c->h_overflow[f]) continue;
+            redo = true;
+            const size_t cap = c->p.max_contours;
+            HIP_TRY(c, hipMemsetAsync(c->d_count + f, 0, sizeof(int32_t), c->stream));
+            HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, c->stream));
+            CclArgs ca{c->d_mask + f * c->work_plane, c->d_label, c->d_outer, c->d_cid, c->d_count + f,
+                       c->d_rec_dev, 1, c->h, c->w, c->p.max_contours};
+            HIP_TRY(c, launch_ccl(c->stream, ca, nullptr));
+            HIP_TRY(c, hipMemcpyAsync(c->h_rec + f * cap * 5, c->d_rec_dev, cap * 5 * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(c->h_count + f, c->d_count + f, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        }
+        if (redo) HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     c->timer.collect();
     const int n = c->pending, S = c->p.n_streams, cap = c->p.max_contours;

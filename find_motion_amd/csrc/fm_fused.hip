@@ -1,0 +1,726 @@
+// fm_fused.hip — temporally blocked fused kernel + tile-summary CCL (gfx950).
+//
+// One workgroup (512 threads) owns a 64x64 output tile of one stream for ALL
+// frames of a batch:
+//
+//   per frame t:   raw BGR (tile + 2 + r halo) --16-B loads--> LDS      (prefetched one frame ahead)
+//                  gray (BGR2GRAY)                        LDS u8        fm.py:493
+//                  horizontal Gaussian taps               LDS u16       fm.py:494
+//                  vertical taps, keep-mask, convertScaleAbs + absdiff,
+//                  threshold, accumulateWeighted           registers    fm.py:619-662
+//                    -> threshold rows as bits via __ballot (lane = column)
+//                  dilate 5x5 on the bit rows (shift/or)   LDS u64/row  fm.py:266
+//                  mask bytes out                                        VideoFrame.thresh
+//                  run-length CCL of the tile (wave 0, lane = row)       fm.py:269-272
+//                    -> tile record (edge labels, root list) + node records
+//
+// The f64 background of the tile + 2-px dilation halo lives in registers for
+// the whole batch (the halo is updated redundantly, bit-identical to the
+// neighbour's own update), so background HBM traffic is 16 B/px per BATCH,
+// not per frame.  Reads come from bg_in and writes go to bg_out (ping-pong),
+// so a neighbour's halo read never sees this batch's update.
+//
+// Global CCL over tile records (k_tile_merge / k_tile_resolve1 / _2): nodes
+// are (tile, local component), unions only along tile edges.  The external
+// test is the oracle-checked rule of the v1 CCL: a foreground component has
+// an external contour iff the background component left of its raster-first
+// pixel contains the 1-px zero pad, i.e. touches the image border.
+#include "fm_internal.h"
+
+namespace fm {
+namespace fz {
+
+constexpr int TS = 64;                   // output tile edge
+constexpr int NT = 512;                  // threads per workgroup
+constexpr int NW = NT / 64;              // waves
+constexpr int EW = TS + 4;               // threshold region (tile + dilation halo)
+constexpr int NCJ = (EW + NW - 1) / NW;  // center rows per thread (9)
+constexpr int NHALO = EW * 4;            // 4 halo columns x 68 rows
+constexpr int MAXR = kTileMaxRuns;
+constexpr int NCH = 6;                   // max 16-B raw chunks per thread for the generic-k kernel
+constexpr int KMAX_FUSED = 49;
+constexpr uint32_t REF_OUTER = 0x80000000u;
+constexpr uint32_t REF_EDGE = 0x40000000u;
+
+__host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
+__host__ __device__ constexpr int gw_for(int r) { return TS + 4 + 2 * r; }
+__host__ __device__ constexpr int rs_for(int r) { return a16(3 * gw_for(r) + 32); }
+__host__ __device__ constexpr int nchunks_for(int r) { return gw_for(r) * (rs_for(r) / 16); }
+
+struct Layout {
+    int GW, RS, CPR, nchunks;
+    int o_G, o_H, o_E, o_EH, o_O, o_roff, o_cf, o_rowy, o_colx, bytes;
+    __host__ __device__ explicit Layout(int r) {
+        GW = gw_for(r);
+        RS = rs_for(r);
+        CPR = RS / 16;
+        nchunks = GW * CPR;
+        o_G = GW * RS;
+        o_H = o_G + a16(GW * GW);
+        o_E = o_H + a16(GW * EW * 2);
+        o_EH = o_E + EW * 8;
+        o_O = o_EH + a16(NHALO);
+        o_roff = o_O + TS * 8;
+        o_cf = o_roff + a16(GW * 4);
+        o_rowy = o_cf + 64 * 4;
+        o_colx = o_rowy + a16(GW * 4);
+        bytes = o_colx + a16(GW * 4);
+    }
+};
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = (p < 0) ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for
+// vmcnt(0), which would drain the next frame's raw prefetch at every barrier;
+// the stages below exchange data through LDS only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ int lload(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ int lfind(int* P, int x) {
+    for (;;) {
+        const int p = lload(&P[x]);
+        if (p == x) return x;
+        x = p;
+    }
+}
+__device__ __forceinline__ void lunion(int* P, int a, int b) {
+    for (;;) {
+        a = lfind(P, a);
+        b = lfind(P, b);
+        if (a == b) return;
+        if (a < b) {
+            const int old = atomicMin(&P[b], a);
+            if (old == b) return;
+            b = old;
+        } else {
+            const int old = atomicMin(&P[a], b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+// global union-find over NodeRec::parent (relaxed agent-scope loads bypass the
+// per-CU L1, so a find never follows a stale pointer written by another CU)
+__device__ __forceinline__ int gpar(NodeRec* N, int x) {
+    return __hip_atomic_load(&N[x].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int gfind(NodeRec* N, int x) {
+    for (;;) {
+        const int p = gpar(N, x);
+        if (p == x) return x;
+        x = p;
+    }
+}
+__device__ __forceinline__ void gunion(NodeRec* N, int a, int b) {
+    for (;;) {
+        a = gfind(N, a);
+        b = gfind(N, b);
+        if (a == b) return;
+        if (a < b) {
+            const int old = atomicMin(&N[b].parent, a);
+            if (old == b) return;
+            b = old;
+        } else {
+            const int old = atomicMin(&N[a].parent, b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t nib2bytes(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) * 255u; }
+
+// ---------------------------------------------------------------------------
+// raw BGR halo region: chunk c = 16 aligned bytes of row gy
+template <int N>
+struct RawLoad {
+    uint4 v[N];
+};
+
+template <int N>
+__device__ __forceinline__ void load_raw(RawLoad<N>& R, const uint8_t* fsrc, size_t fbytes, const int* rowy, int nchunks,
+                                         int cpr, int r, int x0, int w, int tid) {
+    const uintptr_t fb = (uintptr_t)fsrc, fe = fb + fbytes;
+    const int cx0 = max(x0 - 2 - r, 0), cx1 = min(x0 + TS + 2 + r, w);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const int c = tid + NT * i;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (c < nchunks) {
+            const int gy = c / cpr, k = c - gy * cpr;
+            const int y = rowy[gy];
+            const uintptr_t sb = fb + ((size_t)y * w + cx0) * 3, eb = fb + ((size_t)y * w + cx1) * 3;
+            const uintptr_t ca = (sb & ~(uintptr_t)15) + 16 * (uintptr_t)k;
+            if (ca < eb) {
+                if (ca >= fb && ca + 16 <= fe) {
+                    val = *reinterpret_cast<const uint4*>(ca);
+                } else {  // first/last bytes of the frame buffer: never read outside it
+                    uint32_t wds[4] = {0, 0, 0, 0};
+                    for (int b = 0; b < 16; b++)
+                        if (ca + b >= fb && ca + b < fe) wds[b >> 2] |= (uint32_t)(*(const uint8_t*)(ca + b)) << (8 * (b & 3));
+                    val = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+                }
+            }
+        }
+        R.v[i] = val;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_raw(const RawLoad<N>& R, uint8_t* smem, int* roff, const int* rowy,
+                                          const uint8_t* fsrc, int nchunks, int cpr, int rs, int r, int x0, int w,
+                                          int tid) {
+    const int cx0 = max(x0 - 2 - r, 0);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const int c = tid + NT * i;
+        if (c < nchunks) {
+            const int gy = c / cpr, k = c - gy * cpr;
+            *reinterpret_cast<uint4*>(smem + gy * rs + 16 * k) = R.v[i];
+            if (k == 0) roff[gy] = (int)(((uintptr_t)fsrc + ((size_t)rowy[gy] * w + cx0) * 3) & 15);
+        }
+    }
+}
+
+// vertical taps at one E pixel: exact fixed point, round half up
+template <int KC>
+__device__ __forceinline__ int vblur(const uint16_t* hv, const int* cf, int k) {
+    uint32_t acc = 0;
+    if (KC) {
+#pragma unroll
+        for (int t = 0; t < KC; t++) acc += (uint32_t)cf[t] * hv[t * EW];
+    } else {
+        for (int t = 0; t < k; t++) acc += (uint32_t)cf[t] * hv[t * EW];
+    }
+    return (int)((acc + 32768u) >> 16);
+}
+
+// convertScaleAbs + absdiff + threshold + accumulateWeighted for one pixel.
+__device__ __forceinline__ bool chain(int blur, long long li, double& bg, bool init, int thresh, double alpha,
+                                      double beta, long long vec_end, int cvt_simd, int& d_out) {
+    const double bv = init ? (double)blur : bg;
+    int q = cvt_simd ? __float2int_rn(fabsf(__double2float_rn(bv))) : __double2int_rn(fabs(bv));
+    q = min(max(q, 0), 255);
+    const int d = abs(blur - q);
+    const double bl = (double)blur;
+    bg = (li < vec_end) ? __fma_rn(bv, beta, __dmul_rn(bl, alpha)) : __dadd_rn(__dmul_rn(bl, alpha), __dmul_rn(bv, beta));
+    d_out = d;
+    return d > thresh;
+}
+
+template <int KC>
+__global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int k = KC ? KC : a.ksize;
+    const int r = k >> 1;
+    const Layout L(r);
+    uint8_t* G = smem + L.o_G;
+    uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + L.o_H);
+    uint64_t* Eb = reinterpret_cast<uint64_t*>(smem + L.o_E);
+    uint8_t* EH = smem + L.o_EH;
+    uint64_t* Ob = reinterpret_cast<uint64_t*>(smem + L.o_O);
+    int* roff = reinterpret_cast<int*>(smem + L.o_roff);
+    int* cfl = reinterpret_cast<int*>(smem + L.o_cf);
+    int* rowy = reinterpret_cast<int*>(smem + L.o_rowy);  // reflected source row of each halo-region row
+    int* colx = reinterpret_cast<int*>(smem + L.o_colx);  // 3 * (reflected column - first loaded column)
+
+    const int tid = threadIdx.x, ln = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ti = blockIdx.x, s = blockIdx.y;
+    const int h = a.h, w = a.w, S = a.S;
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const int x0 = tx * TS, y0 = ty * TS;
+    const size_t plane = (size_t)h * w;
+    const size_t fbytes = plane * 3;
+    const bool hk = a.has_keep[s] != 0;
+    const uint8_t* keep = a.keep + (size_t)s * plane;
+    const bool init0 = a.init != nullptr && a.init[s] != 0;
+    const int thresh = a.thresh, cvt_simd = a.cvt_simd;
+    const double alpha = a.alpha, beta = a.beta;
+    const long long vec_end = a.acc_vec_end;
+
+    int cfr[KC ? KC : 1];
+    if (KC) {
+#pragma unroll
+        for (int t = 0; t < (KC ? KC : 1); t++) cfr[t] = a.coef[t];
+    } else {
+        if (tid < 64) cfl[tid] = tid < k ? a.coef[tid] : 0;
+    }
+    const int* cf = KC ? cfr : cfl;
+    {
+        const int cx0 = max(x0 - 2 - r, 0), cx1 = min(x0 + TS + 2 + r, w);
+        for (int i = tid; i < L.GW; i += NT) {
+            rowy[i] = reflect101(y0 - 2 - r + i, h);
+            // out-of-range columns only feed pixels outside the image: clamp them
+            colx[i] = 3 * (min(max(reflect101(x0 - 2 - r + i, w), cx0), cx1 - 1) - cx0);
+        }
+    }
+    __syncthreads();
+
+    // ---- background of the owned E pixels -> registers
+    double bgc[NCJ];
+    double bgh = 0.0;
+    const double* bgi = a.bg_in + (size_t)s * plane;
+#pragma unroll
+    for (int j = 0; j < NCJ; j++) {
+        const int ey = wv + NW * j, y = y0 - 2 + ey, x = x0 + ln;
+        bgc[j] = (!init0 && ey < EW && y >= 0 && y < h && x < w) ? bgi[(size_t)y * w + x] : 0.0;
+    }
+    if (tid < NHALO && !init0) {
+        const int ey = tid >> 2, c = tid & 3, ex = c < 2 ? c : 64 + c;
+        const int y = y0 - 2 + ey, x = x0 - 2 + ex;
+        if (y >= 0 && y < h && x >= 0 && x < w) bgh = bgi[(size_t)y * w + x];
+    }
+
+    constexpr int NCHK = KC ? (nchunks_for(KC >> 1) + NT - 1) / NT : NCH;
+    RawLoad<NCHK> R;
+    load_raw(R, a.src + (size_t)s * fbytes, fbytes, rowy, L.nchunks, L.CPR, r, x0, w, tid);
+
+    const size_t F = (size_t)a.T * S;
+    for (int t = 0; t < a.T; t++) {
+        const size_t f = (size_t)t * S + s;
+        const uint8_t* fsrc = a.src + f * fbytes;
+        const bool init = init0 && t == 0;
+        // keep per-row scalar offsets from being hoisted out of the frame loop
+        // (LICM of 9 rows x 64-bit offsets spills SGPRs)
+        int y0v = y0, wvv = wv;
+        asm volatile("" : "+s"(y0v), "+s"(wvv));
+        store_raw(R, smem, roff, rowy, fsrc, L.nchunks, L.CPR, L.RS, r, x0, w, tid);
+        lds_barrier();
+        if (t + 1 < a.T) load_raw(R, a.src + (f + S) * fbytes, fbytes, rowy, L.nchunks, L.CPR, r, x0, w, tid);
+
+        // ---- gray over the G region
+        for (int i = tid; i < L.GW * L.GW; i += NT) {
+            const int gy = i / L.GW, gx = i - gy * L.GW;
+            const uint8_t* p = smem + gy * L.RS + roff[gy] + colx[gx];
+            G[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14);
+        }
+        lds_barrier();
+        // ---- horizontal taps (exact, 8 fraction bits)
+        for (int i = tid; i < L.GW * EW; i += NT) {
+            const int gy = i / EW, c = i - gy * EW;
+            const uint8_t* g = G + gy * L.GW + c;
+            uint32_t acc = 0;
+            if (KC) {
+#pragma unroll
+                for (int tt = 0; tt < (KC ? KC : 1); tt++) acc += (uint32_t)cf[tt] * g[tt];
+            } else {
+                for (int tt = 0; tt < k; tt++) acc += (uint32_t)cf[tt] * g[tt];
+            }
+            Hs[i] = (uint16_t)acc;
+        }
+        lds_barrier();
+
+        // ---- vertical taps + per-pixel chain; threshold row bits by ballot
+        uint8_t* planes = a.planes;
+#pragma unroll
+        for (int j = 0; j < NCJ; j++) {
+            const int ey = wvv + NW * j;
+            if (ey < EW) {  // wave-uniform
+                const int y = y0v - 2 + ey, x = x0 + ln;
+                bool th = false;
+                if (y >= 0 && y < h && x < w) {
+                    int blur = vblur<KC>(Hs + ey * EW + ln + 2, cf, k);
+                    const long long li = (long long)y * w + x;
+                    if (hk && keep[li] == 0) blur = 0;
+                    int d;
+                    th = chain(blur, li, bgc[j], init, thresh, alpha, beta, vec_end, cvt_simd, d);
+                    if (planes && ey >= 2 && ey < EW - 2) {
+                        const size_t o = f * plane + li;
+                        planes[o] = G[(ey + r) * L.GW + ln + 2 + r];
+                        planes[F * plane + o] = (uint8_t)blur;
+                        planes[2 * F * plane + o] = (uint8_t)d;
+                    }
+                }
+                const uint64_t bits = __ballot(th);
+                if (ln == 0) Eb[ey] = bits;
+            }
+        }
+        if (tid < NHALO) {
+            const int ey = tid >> 2, c = tid & 3, ex = c < 2 ? c : 64 + c;
+            const int y = y0 - 2 + ey, x = x0 - 2 + ex;
+            bool th = false;
+            if (y >= 0 && y < h && x >= 0 && x < w) {
+                int blur = vblur<KC>(Hs + ey * EW + ex, cf, k);
+                const long long li = (long long)y * w + x;
+                if (hk && keep[li] == 0) blur = 0;
+                int d;
+                th = chain(blur, li, bgh, init, thresh, alpha, beta, vec_end, cvt_simd, d);
+            }
+            EH[tid] = th ? 1 : 0;
+        }
+        lds_barrier();
+
+        // ---- dilate 5x5 on bit rows (wave 0, lane = output row)
+        if (wv == 0) {
+            uint64_t C = 0, hl = 0, hr = 0;
+#pragma unroll
+            for (int d = 0; d < 5; d++) {
+                const int ey = ln + d;
+                C |= Eb[ey];
+                hl |= (uint64_t)EH[ey * 4 + 0] | ((uint64_t)EH[ey * 4 + 1] << 1);
+                hr |= (uint64_t)EH[ey * 4 + 2] | ((uint64_t)EH[ey * 4 + 3] << 1);
+            }
+            // 68-bit row V (bit ex), out bit x = OR of V bits x..x+4
+            const uint64_t lo = hl | (C << 2), hi = (C >> 62) | (hr << 2);
+            uint64_t o = lo | ((lo >> 1) | (hi << 63)) | ((lo >> 2) | (hi << 62)) | ((lo >> 3) | (hi << 61)) |
+                         ((lo >> 4) | (hi << 60));
+            const int vc = w - x0;
+            if (vc < 64) o &= (1ull << vc) - 1;
+            if (y0 + ln >= h) o = 0;
+            Ob[ln] = o;
+            a.bits[(f * a.ntiles + ti) * 64 + ln] = o;
+        }
+        lds_barrier();
+
+        // ---- mask bytes out: 8 px per thread
+        {
+            const int row = tid >> 3, oc = tid & 7;
+            const int y = y0 + row, xs = x0 + 8 * oc;
+            if (y < h && xs < w) {
+                const uint32_t b = (uint32_t)(Ob[row] >> (8 * oc)) & 0xFFu;
+                uint8_t* dst = a.mask_out + f * plane + (size_t)y * w + xs;
+                const uint2 v = make_uint2(nib2bytes(b & 15), nib2bytes(b >> 4));
+                if (xs + 8 <= w && (((uintptr_t)dst) & 7) == 0) {
+                    *reinterpret_cast<uint2*>(dst) = v;
+                } else {
+                    for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = (uint8_t)((((i < 4 ? v.x : v.y) >> (8 * (i & 3))) & 0xFF));
+                }
+            }
+        }
+
+    }
+
+    // ---- interior background out: owned center pixels
+    double* bgo = a.bg_out + (size_t)s * plane;
+#pragma unroll
+    for (int j = 0; j < NCJ; j++) {
+        const int ey = wv + NW * j, y = y0 - 2 + ey, x = x0 + ln;
+        if (ey >= 2 && ey < EW - 2 && y < h && x < w) bgo[(size_t)y * w + x] = bgc[j];
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Run-length CCL of one dilated 64x64 tile (one wave, lane = tile row).
+// Runs are numbered in raster order; union-find over runs links the larger
+// root under the smaller, so a root is its component's raster-first run.
+// Foreground runs of adjacent rows connect 8-wise (x ranges within 1),
+// background runs 4-wise (x ranges overlap).  Out-of-image pixels are
+// background and, like pixels on the image border, mark their background
+// component "outer" (they play the role of findContours' 1-px zero pad).
+__global__ __launch_bounds__(64) void k_tile_ccl(FusedArgs a) {
+    __shared__ int par[MAXR];
+    __shared__ int amin[MAXR];   // fg root: min x0; bg root: outer flag
+    __shared__ int amax[MAXR];
+    __shared__ int ay[MAXR];
+    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
+    __shared__ int rb[66];
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    const int ti = blockIdx.x, ln = threadIdx.x;
+    const int h = a.h, w = a.w;
+    const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
+    TileRec* TR = a.tiles + f * a.ntiles + ti;
+    NodeRec* NR = a.nodes + f * (size_t)a.nnodes + (size_t)ti * MAXR;
+    const uint64_t m = a.bits[(f * a.ntiles + ti) * 64 + ln];
+
+    if (__ballot(m != 0) == 0) {  // empty tile: one background component (run 0)
+        TR->edges[ln] = 0;
+        TR->edges[64 + ln] = 0;
+        TR->edges[128 + ln] = 0;
+        TR->edges[192 + ln] = 0;
+        if (ln == 0) {
+            TR->nroots = 1;
+            TR->roots[0] = 0;
+            const bool outer = x0 == 0 || y0 == 0 || x0 + TS - 1 >= w - 1 || y0 + TS - 1 >= h - 1;
+            NodeRec nrec;
+            nrec.key = 0;
+            nrec.parent = ti * MAXR;
+            nrec.flags = outer ? 2u : 0u;
+            nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+            NR[0] = nrec;
+        }
+        return;
+    }
+
+    const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
+    const int nr = __popcll(starts);
+    int incl = nr;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (ln >= o) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    const int base = incl - nr;
+    if (total > MAXR) {  // impossible for a dilated mask (<= 24 runs per row); host relabels the frame
+        if (ln == 0) {
+            TR->nroots = 0;
+            atomicOr(&a.count[F + f], 1);
+        }
+        return;
+    }
+    rb[ln] = base;
+    if (ln == 63) rb[64] = total;
+    const int gy = y0 + ln;
+    {
+        uint64_t sb = starts;
+        int id = base;
+        while (sb) {
+            const int xs = __builtin_ctzll(sb);
+            sb &= sb - 1;
+            const int xe = sb ? __builtin_ctzll(sb) - 1 : 63;
+            const int fg = (int)((m >> xs) & 1);
+            const int outer = !fg && (x0 + xs == 0 || x0 + xe >= w - 1 || gy == 0 || gy >= h - 1);
+            rx0[id] = (uint8_t)xs;
+            rx1[id] = (uint8_t)xe;
+            rf[id] = (uint8_t)(fg | (outer << 1));
+            par[id] = id;
+            amin[id] = fg ? xs : outer;
+            amax[id] = xe;
+            ay[id] = ln;
+            id++;
+        }
+    }
+    lds_fence();
+    if (ln < 63) {  // union the runs of row ln with those of row ln+1
+        int j = rb[ln + 1];
+        const int jend = rb[ln + 2];
+        for (int i = base; i < base + nr; i++) {
+            const int fgi = rf[i] & 1;
+            const int lo = (int)rx0[i] - fgi, hi2 = (int)rx1[i] + fgi;
+            while (j < jend && (int)rx1[j] < lo) j++;
+            for (int kk = j; kk < jend && (int)rx0[kk] <= hi2; kk++)
+                if ((rf[kk] & 1) == fgi) lunion(par, i, kk);
+        }
+    }
+    lds_fence();
+    for (int i = base; i < base + nr; i++) {  // flatten + fold into roots
+        const int rt = lfind(par, i);
+        if (rt != i) {
+            par[i] = rt;
+            if (rf[i] & 1) {
+                atomicMin(&amin[rt], (int)rx0[i]);
+                atomicMax(&amax[rt], (int)rx1[i]);
+                atomicMax(&ay[rt], ln);
+            } else if (rf[i] & 2) {
+                atomicOr(&amin[rt], 1);
+            }
+        }
+    }
+    lds_fence();
+    int myr = 0;
+    for (int i = base; i < base + nr; i++) myr += (par[i] == i);
+    int rin = myr;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(rin, o, 64);
+        if (ln >= o) rin += v;
+    }
+    if (ln == 63) TR->nroots = rin;
+    int kk = rin - myr;
+    for (int i = base; i < base + nr; i++) {
+        if (par[i] != i) continue;
+        TR->roots[kk++] = (uint16_t)i;
+        const int fg = rf[i] & 1;
+        NodeRec nrec;
+        nrec.parent = ti * MAXR + i;
+        nrec.key = 0;
+        nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+        if (fg) {
+            const int xs = rx0[i];
+            uint32_t ref;
+            if (x0 + xs == 0) ref = REF_OUTER;
+            else if (xs == 0) ref = REF_EDGE | (uint32_t)ln;
+            else ref = (uint32_t)par[i - 1];  // the background run left of this run, flattened
+            nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
+            nrec.flags = 1u;
+            nrec.minx = x0 + amin[i];
+            nrec.maxx = x0 + amax[i];
+            nrec.maxy = y0 + ay[i];
+        } else {
+            nrec.flags = amin[i] ? 2u : 0u;
+        }
+        NR[i] = nrec;
+    }
+    const uint64_t mask_c = (2ull << ln) - 1;
+    const uint64_t s0 = __shfl(starts, 0, 64), s63 = __shfl(starts, 63, 64);
+    const uint64_t m0 = __shfl(m, 0, 64), m63 = __shfl(m, 63, 64);
+    const int id0 = rb[0] + __popcll(s0 & mask_c) - 1;
+    const int id63 = rb[63] + __popcll(s63 & mask_c) - 1;
+    TR->edges[ln] = (uint16_t)(par[base] | ((rf[base] & 1) << 15));
+    TR->edges[64 + ln] = (uint16_t)(par[base + nr - 1] | ((rf[base + nr - 1] & 1) << 15));
+    TR->edges[128 + ln] = (uint16_t)(par[id0] | (((m0 >> ln) & 1) << 15));
+    TR->edges[192 + ln] = (uint16_t)(par[id63] | (((m63 >> ln) & 1) << 15));
+}
+
+// ---------------------------------------------------------------------------
+// Global merge of tile records
+__device__ __forceinline__ int enode(int tile, uint16_t e) { return tile * MAXR + (e & 0x7FFF); }
+__device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
+
+__global__ __launch_bounds__(64) void k_tile_merge(FusedArgs a) {
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    const int ti = blockIdx.x, ln = threadIdx.x;
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    if (a.count[F + f]) return;
+    const TileRec* TR = a.tiles + f * a.ntiles;
+    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    if (tx + 1 < a.ntx) {  // vertical boundary with the right tile
+        const int tb = ti + 1;
+        const uint16_t A = TR[ti].edges[64 + ln], B = TR[tb].edges[ln];
+        const int Ap = __shfl_up((int)A, 1, 64), Bp = __shfl_up((int)B, 1, 64);
+        if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(ti, A), enode(tb, B));
+        if (efg(A)) {
+            if (ln > 0) {
+                const uint16_t Bu = TR[tb].edges[ln - 1];
+                if (efg(Bu) && Bu != B) gunion(N, enode(ti, A), enode(tb, Bu));
+            }
+            if (ln < 63) {
+                const uint16_t Bd = TR[tb].edges[ln + 1];
+                if (efg(Bd) && Bd != B) gunion(N, enode(ti, A), enode(tb, Bd));
+            }
+        }
+    }
+    if (ty + 1 < a.nty) {  // horizontal boundary with the tile below
+        const int tb = ti + a.ntx;
+        const uint16_t A = TR[ti].edges[192 + ln], B = TR[tb].edges[128 + ln];
+        const int Ap = __shfl_up((int)A, 1, 64), Bp = __shfl_up((int)B, 1, 64);
+        if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(ti, A), enode(tb, B));
+        if (efg(A)) {
+            if (ln > 0) {
+                const uint16_t Bl = TR[tb].edges[128 + ln - 1];
+                if (efg(Bl) && Bl != B) gunion(N, enode(ti, A), enode(tb, Bl));
+            }
+            if (ln < 63) {
+                const uint16_t Br = TR[tb].edges[128 + ln + 1];
+                if (efg(Br) && Br != B) gunion(N, enode(ti, A), enode(tb, Br));
+            }
+        }
+        if (ln == 0 && tx + 1 < a.ntx) {  // (63,63) <-> (0,0) of the down-right tile
+            const uint16_t P = TR[ti].edges[192 + 63], Q = TR[tb + 1].edges[128];
+            if (efg(P) && efg(Q)) gunion(N, enode(ti, P), enode(tb + 1, Q));
+        }
+        if (ln == 0 && tx > 0) {  // (0,63) <-> (63,0) of the down-left tile
+            const uint16_t P = TR[ti].edges[192], Q = TR[tb - 1].edges[128 + 63];
+            if (efg(P) && efg(Q)) gunion(N, enode(ti, P), enode(tb - 1, Q));
+        }
+    }
+}
+
+// fold every non-root node into its root: bbox / raster-first key (fg), outer flag (bg)
+__global__ __launch_bounds__(64) void k_tile_resolve1(FusedArgs a) {
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    const int ti = blockIdx.x;
+    if (a.count[F + f]) return;
+    const TileRec* TR = a.tiles + f * a.ntiles + ti;
+    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    const int nr = TR->nroots;
+    for (int kx = threadIdx.x; kx < nr; kx += 64) {
+        const int n = ti * MAXR + TR->roots[kx];
+        const int rt = gfind(N, n);
+        if (rt == n) continue;
+        N[n].parent = rt;
+        const uint32_t fl = N[n].flags;
+        if (fl & 1) {
+            atomicMin((unsigned long long*)&N[rt].key, (unsigned long long)N[n].key);
+            atomicMin(&N[rt].minx, N[n].minx);
+            atomicMax(&N[rt].maxx, N[n].maxx);
+            atomicMax(&N[rt].maxy, N[n].maxy);
+        } else if (fl & 2) {
+            atomicOr(&N[rt].flags, 2u);
+        }
+    }
+}
+
+// external test at every foreground root; emit contour records
+__global__ __launch_bounds__(64) void k_tile_resolve2(FusedArgs a) {
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    const int ti = blockIdx.x;
+    if (a.count[F + f]) return;
+    const TileRec* TRf = a.tiles + f * a.ntiles;
+    const TileRec* TR = TRf + ti;
+    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    const int nr = TR->nroots;
+    for (int kx = threadIdx.x; kx < nr; kx += 64) {
+        const int n = ti * MAXR + TR->roots[kx];
+        const NodeRec nd = N[n];
+        if (nd.parent != n || !(nd.flags & 1)) continue;
+        const uint32_t first = (uint32_t)(nd.key >> 32), ref = (uint32_t)nd.key;
+        const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
+        bool ext;
+        if (ref & REF_OUTER) {
+            ext = true;
+        } else {
+            const int tfirst = (fy / TS) * a.ntx + fx / TS;
+            const int bn = (ref & REF_EDGE) ? enode(tfirst - 1, TRf[tfirst - 1].edges[64 + (ref & 63)])
+                                            : tfirst * MAXR + (int)ref;
+            ext = (N[N[bn].parent].flags & 2) != 0;
+        }
+        if (!ext) continue;
+        const int id = atomicAdd(&a.count[f], 1);
+        if (id < a.cap) {
+            int32_t* rr = a.rec + (f * a.cap + id) * 5;
+            rr[0] = (int32_t)first;
+            rr[1] = nd.minx;
+            rr[2] = fy;
+            rr[3] = nd.maxx;
+            rr[4] = nd.maxy;
+        }
+    }
+}
+
+}  // namespace fz
+
+int fused_lds_bytes(int ksize) { return fz::Layout(ksize >> 1).bytes; }
+int fused_max_ksize() { return fz::KMAX_FUSED; }
+
+hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
+    const int bytes = fz::Layout(a.ksize >> 1).bytes;
+    if (a.ksize > fz::KMAX_FUSED || bytes > 160 * 1024) return hipErrorInvalidValue;
+    dim3 grid(a.ntiles, a.S);
+    int tok = tm ? tm->begin("fused") : -1;
+    if (a.ksize == 5) {
+        (void)hipFuncSetAttribute((const void*)fz::k_fused<5>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(fz::k_fused<5>, grid, dim3(fz::NT), bytes, st, a);
+    } else {
+        (void)hipFuncSetAttribute((const void*)fz::k_fused<0>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(fz::k_fused<0>, grid, dim3(fz::NT), bytes, st, a);
+    }
+    if (tm) tm->end(tok);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    dim3 gm(a.ntiles, a.T * a.S);
+    tok = tm ? tm->begin("tile_ccl") : -1;
+    hipLaunchKernelGGL(fz::k_tile_ccl, gm, dim3(64), 0, st, a);
+    if (tm) tm->end(tok);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tok = tm ? tm->begin("tile_merge") : -1;
+    hipLaunchKernelGGL(fz::k_tile_merge, gm, dim3(64), 0, st, a);
+    if (tm) tm->end(tok);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tok = tm ? tm->begin("tile_resolve1") : -1;
+    hipLaunchKernelGGL(fz::k_tile_resolve1, gm, dim3(64), 0, st, a);
+    if (tm) tm->end(tok);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tok = tm ? tm->begin("tile_resolve2") : -1;
+    hipLaunchKernelGGL(fz::k_tile_resolve2, gm, dim3(64), 0, st, a);
+    if (tm) tm->end(tok);
+    return hipGetLastError();
+}
+
+}  // namespace fm

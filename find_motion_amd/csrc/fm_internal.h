@@ -14,6 +14,7 @@ namespace fm {
 
 constexpr int kMaxK = 255;        // largest Gaussian size handled by the tiled kernel
 constexpr int kCclBlock = 32;     // CCL block edge (pixels)
+constexpr int kTileMaxRuns = 1600; // runs per 64x64 tile of a dilated mask (<= 24 per row => 1536)
 
 // Host-built INTER_AREA tables (computeResizeAreaTab restated in fm_capi.cpp).
 // Per destination index d: taps start at src index ofs[d], cnt[d] taps, weights
@@ -54,7 +55,42 @@ struct CclArgs {
     int F, h, w, cap;
 };
 
-// Kernel launchers (fm_kernels.hip).  All asynchronous on `st`.
+// Temporally blocked fused kernel + tile-summary CCL (fm_fused.hip).
+// Global CCL node = (tile, local component): index tile * kTileMaxRuns + local.
+struct NodeRec {
+    uint64_t key;     // foreground: (raster-first pixel << 32) | left-background reference
+    int32_t parent;   // global union-find
+    uint32_t flags;   // bit0 foreground, bit1 background touching the image border (outer)
+    int32_t minx, maxx, maxy, pad;
+};
+struct TileRec {
+    int32_t nroots, pad[3];
+    uint16_t edges[256];              // 0..63 left col, 64.. right col, 128.. top row, 192.. bottom row; bit15 = fg
+    uint16_t roots[kTileMaxRuns];     // local ids of the tile's components
+};
+
+struct FusedArgs {
+    const uint8_t* src;          // work-size BGR frames [T][S][h][w][3]
+    const double* bg_in;         // [S][h*w] background before the batch
+    double* bg_out;              // [S][h*w] background after the batch
+    const uint8_t* keep;         // [S][h*w]
+    const uint8_t* has_keep;     // [S]
+    const uint8_t* init;         // [S] or nullptr: 1 => bg := blur at the batch's first frame
+    uint8_t* mask_out;           // [T][S][h*w] dilated threshold
+    uint8_t* planes;             // optional [3][T][S][h*w] gray, blur, frame_delta
+    uint64_t* bits;              // [F][ntiles][64] dilated tile rows as bit masks (input of k_tile_ccl)
+    TileRec* tiles;              // [F][ntiles]
+    NodeRec* nodes;              // [F][nnodes]
+    int32_t* count;              // [F] external contours; count[F + f] = overflow flag
+    int32_t* rec;                // [F][cap][5]
+    int T, S, h, w, ksize, thresh;
+    int ntx, nty, ntiles, nnodes, cap, cvt_simd;
+    double alpha, beta;
+    long long acc_vec_end;
+    int32_t coef[kMaxK];
+};
+
+// Kernel launchers (fm_kernels.hip, fm_fused.hip).  All asynchronous on `st`.
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
                               int h, int w, const int32_t* xofs, const int32_t* xcnt, const float* xwt,
                               int xtaps, const int32_t* yofs, const int32_t* ycnt, const float* ywt,
@@ -64,6 +100,9 @@ hipError_t launch_resize_area_fast(hipStream_t st, const uint8_t* src, uint8_t* 
 hipError_t launch_pixel(hipStream_t st, const PixelArgs& a);
 struct KernelTimer;
 hipError_t launch_ccl(hipStream_t st, const CclArgs& a, KernelTimer* timer);
+hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* timer);
+int fused_lds_bytes(int ksize);
+int fused_max_ksize();
 
 // Optional per-kernel event timing (FM_FLAG_PROFILE): events are recorded on
 // the launch stream around each kernel and read back after the stream syncs.
