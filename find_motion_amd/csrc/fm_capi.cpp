@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -62,6 +63,7 @@ struct fm_ctx {
     bool use_fused = false;
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;
     TileRec* d_tiles = nullptr;
+    int32_t* d_heavy = nullptr;
     uint64_t* d_bits = nullptr;
     NodeRec* d_nodes = nullptr;
     int32_t* h_overflow = nullptr;  // pinned [T*S]
@@ -77,6 +79,7 @@ struct fm_ctx {
     int ready = 0;                // frames with readable results
     std::vector<std::vector<fm_contour>> contours;  // per (t*S+s), sorted
     std::string err;
+    int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of the fused kernel (results invalid)
 };
 
 namespace {
@@ -321,7 +324,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
         (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, px)) ||
-        (rc = dalloc(cp, &c->d_count, 2 * frames)))
+        (rc = dalloc(cp, &c->d_count, 2 * frames + 1)))
         return rc;
     // contour records: mapped pinned host memory written directly by the
     // kernels (only the records that exist cross PCIe; no D2H copy of the
@@ -334,7 +337,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
         c->nnodes = c->ntiles * kTileMaxRuns;
-        if ((rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64)) || (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
+        if ((rc = dalloc(cp, &c->d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64)) || (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
             return rc;
     }
     // pixel-level CCL buffers: the whole batch on the v1 path, one frame for the
@@ -364,6 +367,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     HIP_TRY(cp, hipHostMalloc((void**)&c->h_overflow, frames * sizeof(int32_t)));
     c->bg_init.assign(S, 0);
     c->has_keep.assign(S, 0);
+    if (const char* e = std::getenv("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
     *out = c.release();
     return FM_OK;
 }
@@ -376,7 +380,7 @@ void fm_destroy(fm_ctx* c) {
     dfree(c->d_in); dfree(c->d_work); dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep);
     dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask); dfree(c->d_planes); dfree(c->d_label);
     dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec_dev); c->d_rec = nullptr;
-    dfree(c->d_tiles); dfree(c->d_bits); dfree(c->d_nodes);
+    dfree(c->d_tiles); dfree(c->d_heavy); dfree(c->d_bits); dfree(c->d_nodes);
     if (c->h_overflow) (void)hipHostFree(c->h_overflow);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     if (c->h_init) (void)hipHostFree(c->h_init);
@@ -464,7 +468,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, c->h_init, S, hipMemcpyHostToDevice, c->stream));
 
     const long long npx = (long long)c->work_plane;
-    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, 2 * F * sizeof(int32_t), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, (2 * F + 1) * sizeof(int32_t), c->stream));
     if (c->use_fused) {
         FusedArgs fa{};
         fa.src = work;
@@ -479,6 +483,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.tiles = c->d_tiles;
         fa.nodes = c->d_nodes;
         fa.count = c->d_count;
+        fa.heavy = c->d_heavy;
         fa.rec = c->d_rec;
         fa.T = n;
         fa.S = S;
@@ -495,6 +500,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.alpha = c->p.avg;
         fa.beta = 1.0 - c->p.avg;
         fa.acc_vec_end = npx - npx % 16;
+        fa.dbg_skip = c->dbg_skip;
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
         HIP_TRY(c, launch_fused(c->stream, fa, &c->timer));
         c->bg_cur ^= 1;

@@ -114,11 +114,16 @@ __device__ __forceinline__ void lunion(int* P, int a, int b) {
 __device__ __forceinline__ int gpar(NodeRec* N, int x) {
     return __hip_atomic_load(&N[x].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// find with path halving done by atomicMin: a pointer only ever moves to a
+// smaller member of the same set, so it cannot undo a concurrent link
 __device__ __forceinline__ int gfind(NodeRec* N, int x) {
     for (;;) {
         const int p = gpar(N, x);
         if (p == x) return x;
-        x = p;
+        const int gp = gpar(N, p);
+        if (gp == p) return p;
+        atomicMin(&N[x].parent, gp);
+        x = gp;
     }
 }
 __device__ __forceinline__ void gunion(NodeRec* N, int a, int b) {
@@ -147,10 +152,22 @@ struct RawLoad {
     uint4 v[N];
 };
 
+// Bytes of a chunk that straddles the frame buffer's first/last byte (only
+// possible when a frame does not start 16-B aligned): never read outside it.
+__device__ __attribute__((noinline)) uint4 load_partial(const uint8_t* ca, const uint8_t* fb, const uint8_t* fe) {
+    uint32_t wds[4] = {0, 0, 0, 0};
+    for (int b = 0; b < 16; b++)
+        if (ca + b >= fb && ca + b < fe) wds[b >> 2] |= (uint32_t)ca[b] << (8 * (b & 3));
+    return make_uint4(wds[0], wds[1], wds[2], wds[3]);
+}
+
+// Pointer arithmetic stays on the kernel-argument pointer so the compiler
+// emits global_load (a flat load would also count in lgkmcnt and every LDS
+// wait would drain the next frame's prefetch).
 template <int N>
 __device__ __forceinline__ void load_raw(RawLoad<N>& R, const uint8_t* fsrc, size_t fbytes, const int* rowy, int nchunks,
                                          int cpr, int r, int x0, int w, int tid) {
-    const uintptr_t fb = (uintptr_t)fsrc, fe = fb + fbytes;
+    const uint8_t* fe = fsrc + fbytes;
     const int cx0 = max(x0 - 2 - r, 0), cx1 = min(x0 + TS + 2 + r, w);
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -158,18 +175,13 @@ __device__ __forceinline__ void load_raw(RawLoad<N>& R, const uint8_t* fsrc, siz
         uint4 val = make_uint4(0, 0, 0, 0);
         if (c < nchunks) {
             const int gy = c / cpr, k = c - gy * cpr;
-            const int y = rowy[gy];
-            const uintptr_t sb = fb + ((size_t)y * w + cx0) * 3, eb = fb + ((size_t)y * w + cx1) * 3;
-            const uintptr_t ca = (sb & ~(uintptr_t)15) + 16 * (uintptr_t)k;
+            const size_t rowoff = (size_t)rowy[gy] * w;
+            const uint8_t* sb = fsrc + (rowoff + cx0) * 3;
+            const uint8_t* eb = fsrc + (rowoff + cx1) * 3;
+            const uint8_t* ca = sb - ((uintptr_t)sb & 15) + 16 * k;
             if (ca < eb) {
-                if (ca >= fb && ca + 16 <= fe) {
-                    val = *reinterpret_cast<const uint4*>(ca);
-                } else {  // first/last bytes of the frame buffer: never read outside it
-                    uint32_t wds[4] = {0, 0, 0, 0};
-                    for (int b = 0; b < 16; b++)
-                        if (ca + b >= fb && ca + b < fe) wds[b >> 2] |= (uint32_t)(*(const uint8_t*)(ca + b)) << (8 * (b & 3));
-                    val = make_uint4(wds[0], wds[1], wds[2], wds[3]);
-                }
+                if (__builtin_expect(ca >= fsrc && ca + 16 <= fe, 1)) val = *reinterpret_cast<const uint4*>(ca);
+                else val = load_partial(ca, fsrc, fe);
             }
         }
         R.v[i] = val;
@@ -195,25 +207,45 @@ __device__ __forceinline__ void store_raw(const RawLoad<N>& R, uint8_t* smem, in
 // vertical taps at one E pixel: exact fixed point, round half up
 template <int KC>
 __device__ __forceinline__ int vblur(const uint16_t* hv, const int* cf, int k) {
-    uint32_t acc = 0;
+    uint32_t acc = 0;  // taps < 256, horizontal sums <= 65280: 24-bit multiplies are exact
     if (KC) {
 #pragma unroll
-        for (int t = 0; t < KC; t++) acc += (uint32_t)cf[t] * hv[t * EW];
+        for (int t = 0; t < KC; t++) acc += __umul24((uint32_t)cf[t], hv[t * EW]);
     } else {
-        for (int t = 0; t < k; t++) acc += (uint32_t)cf[t] * hv[t * EW];
+        for (int t = 0; t < k; t++) acc += __umul24((uint32_t)cf[t], hv[t * EW]);
     }
     return (int)((acc + 32768u) >> 16);
 }
 
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+// BGR2GRAY of 4 consecutive pixels packed in 3 dwords (B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3):
+// (B*1868 + G*9617 + R*4899 + 8192) >> 14 via v_perm (B,G as u16x2) + v_dot2_u32_u16.
+__device__ __forceinline__ uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
+    const u16x2_t cbg = __builtin_bit_cast(u16x2_t, 1868u | (9617u << 16));
+    const uint32_t p0 = __builtin_amdgcn_perm(d0, d0, 0x0C010C00u);
+    const uint32_t p1 = __builtin_amdgcn_perm(d1, d0, 0x0C040C03u);
+    const uint32_t p2 = __builtin_amdgcn_perm(d1, d1, 0x0C030C02u);
+    const uint32_t p3 = __builtin_amdgcn_perm(d2, d2, 0x0C020C01u);
+    const uint32_t g0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p0), cbg, __umul24((d0 >> 16) & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p1), cbg, __umul24((d1 >> 8) & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g2 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p2), cbg, __umul24(d2 & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g3 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p3), cbg, __umul24(d2 >> 24, 4899u) + 8192u, false) >> 14;
+    return g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);
+}
+
 // convertScaleAbs + absdiff + threshold + accumulateWeighted for one pixel.
+// row_vec: the whole row lies in OpenCV's vector body (the usual case), so the
+// per-pixel tail test is skipped.
 __device__ __forceinline__ bool chain(int blur, long long li, double& bg, bool init, int thresh, double alpha,
-                                      double beta, long long vec_end, int cvt_simd, int& d_out) {
+                                      double beta, long long vec_end, int cvt_simd, int& d_out, bool row_vec = false) {
     const double bv = init ? (double)blur : bg;
     int q = cvt_simd ? __float2int_rn(fabsf(__double2float_rn(bv))) : __double2int_rn(fabs(bv));
     q = min(max(q, 0), 255);
     const int d = abs(blur - q);
     const double bl = (double)blur;
-    bg = (li < vec_end) ? __fma_rn(bv, beta, __dmul_rn(bl, alpha)) : __dadd_rn(__dmul_rn(bl, alpha), __dmul_rn(bv, beta));
+    if (row_vec || li < vec_end) bg = __fma_rn(bv, beta, __dmul_rn(bl, alpha));
+    else bg = __dadd_rn(__dmul_rn(bl, alpha), __dmul_rn(bv, beta));
     d_out = d;
     return d > thresh;
 }
@@ -266,20 +298,49 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
         }
     }
     __syncthreads();
+    const int cxa = colx[ln];  // this lane's column offset in the raw rows (column ln of the G region)
 
-    // ---- background of the owned E pixels -> registers
+    // ---- background of the owned E pixels -> registers.  Wave w owns the
+    //      contiguous E rows [rs, rs + cnt) (9 rows for waves 0-3, 8 for 4-7).
+    const int rs = min(9 * wv, 8 * wv + 4), cnt = wv < 4 ? 9 : 8;
     double bgc[NCJ];
     double bgh = 0.0;
     const double* bgi = a.bg_in + (size_t)s * plane;
 #pragma unroll
     for (int j = 0; j < NCJ; j++) {
-        const int ey = wv + NW * j, y = y0 - 2 + ey, x = x0 + ln;
-        bgc[j] = (!init0 && ey < EW && y >= 0 && y < h && x < w) ? bgi[(size_t)y * w + x] : 0.0;
+        const int ey = rs + j, y = y0 - 2 + ey, x = x0 + ln;
+        bgc[j] = (!init0 && j < cnt && y >= 0 && y < h && x < w) ? bgi[(size_t)y * w + x] : 0.0;
     }
     if (tid < NHALO && !init0) {
         const int ey = tid >> 2, c = tid & 3, ex = c < 2 ? c : 64 + c;
         const int y = y0 - 2 + ey, x = x0 - 2 + ex;
         if (y >= 0 && y < h && x >= 0 && x < w) bgh = bgi[(size_t)y * w + x];
+    }
+
+    // fast gray + horizontal path (k = 5, 13, 21, ...: (2 + r) % 4 == 0 keeps pixel
+    // quads dword-aligned in the raw rows); lane -> (row group rg, pixel quad q)
+    constexpr bool FAST = KC > 1 && ((2 + (KC >> 1)) % 4) == 0;
+    constexpr int GWc = gw_for(KC >> 1);
+    constexpr int NQG = GWc / 4;                     // gray quads per row
+    constexpr int RPW = FAST ? 64 / NQG : 1;         // rows per wave instruction
+    constexpr int NIT = FAST ? (GWc + RPW * NW - 1) / (RPW * NW) : 1;
+    constexpr int NQN = (KC + 6) / 4;                // gray quads feeding one horizontal quad
+    constexpr int NGRP = KC / 4;                     // 4-tap dot groups
+    const int rg = ln / NQG, q = ln - rg * NQG;
+    int colq[4] = {0, 0, 0, 0};
+    bool qfast = false;
+    uint32_t cpk[NGRP > 0 ? NGRP : 1];
+    if (FAST) {
+        if (rg < RPW) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) colq[i] = colx[4 * q + i];
+            qfast = colq[1] == colq[0] + 3 && colq[2] == colq[0] + 6 && colq[3] == colq[0] + 9 && (colq[0] & 3) == 0;
+        }
+#pragma unroll
+        for (int g = 0; g < (NGRP > 0 ? NGRP : 1); g++)
+            cpk[g] = NGRP > 0 ? ((uint32_t)cf[4 * g] | ((uint32_t)cf[4 * g + 1] << 8) | ((uint32_t)cf[4 * g + 2] << 16) |
+                                 ((uint32_t)cf[4 * g + 3] << 24))
+                              : 0u;
     }
 
     constexpr int NCHK = KC ? (nchunks_for(KC >> 1) + NT - 1) / NT : NCH;
@@ -295,55 +356,129 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
         // (LICM of 9 rows x 64-bit offsets spills SGPRs)
         int y0v = y0, wvv = wv;
         asm volatile("" : "+s"(y0v), "+s"(wvv));
-        store_raw(R, smem, roff, rowy, fsrc, L.nchunks, L.CPR, L.RS, r, x0, w, tid);
-        lds_barrier();
-        if (t + 1 < a.T) load_raw(R, a.src + (f + S) * fbytes, fbytes, rowy, L.nchunks, L.CPR, r, x0, w, tid);
-
-        // ---- gray over the G region
-        for (int i = tid; i < L.GW * L.GW; i += NT) {
-            const int gy = i / L.GW, gx = i - gy * L.GW;
-            const uint8_t* p = smem + gy * L.RS + roff[gy] + colx[gx];
-            G[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14);
-        }
-        lds_barrier();
-        // ---- horizontal taps (exact, 8 fraction bits)
-        for (int i = tid; i < L.GW * EW; i += NT) {
-            const int gy = i / EW, c = i - gy * EW;
-            const uint8_t* g = G + gy * L.GW + c;
-            uint32_t acc = 0;
-            if (KC) {
-#pragma unroll
-                for (int tt = 0; tt < (KC ? KC : 1); tt++) acc += (uint32_t)cf[tt] * g[tt];
-            } else {
-                for (int tt = 0; tt < k; tt++) acc += (uint32_t)cf[tt] * g[tt];
-            }
-            Hs[i] = (uint16_t)acc;
-        }
-        lds_barrier();
-
-        // ---- vertical taps + per-pixel chain; threshold row bits by ballot
+        const int dbg = a.dbg_skip;
         uint8_t* planes = a.planes;
+        if (!(dbg & 16)) store_raw(R, smem, roff, rowy, fsrc, L.nchunks, L.CPR, L.RS, r, x0, w, tid);
+        lds_barrier();
+        if (t + 1 < a.T && !(dbg & 16)) load_raw(R, a.src + (f + S) * fbytes, fbytes, rowy, L.nchunks, L.CPR, r, x0, w, tid);
+
+        if (FAST) {
+            // ---- gray (4 px per lane) + horizontal taps in registers: no G in LDS
+            if (!(dbg & 3)) {
 #pragma unroll
-        for (int j = 0; j < NCJ; j++) {
-            const int ey = wvv + NW * j;
-            if (ey < EW) {  // wave-uniform
-                const int y = y0v - 2 + ey, x = x0 + ln;
-                bool th = false;
-                if (y >= 0 && y < h && x < w) {
-                    int blur = vblur<KC>(Hs + ey * EW + ln + 2, cf, k);
-                    const long long li = (long long)y * w + x;
-                    if (hk && keep[li] == 0) blur = 0;
-                    int d;
-                    th = chain(blur, li, bgc[j], init, thresh, alpha, beta, vec_end, cvt_simd, d);
-                    if (planes && ey >= 2 && ey < EW - 2) {
-                        const size_t o = f * plane + li;
-                        planes[o] = G[(ey + r) * L.GW + ln + 2 + r];
-                        planes[F * plane + o] = (uint8_t)blur;
-                        planes[2 * F * plane + o] = (uint8_t)d;
+                for (int it = 0; it < NIT; it++) {
+                    const int gy = (it * NW + wvv) * RPW + rg;
+                    const bool act = rg < RPW && gy < GWc;
+                    uint32_t g4 = 0;
+                    if (act) {
+                        const int ro = roff[gy];
+                        const uint8_t* rowp = smem + gy * L.RS + ro;
+                        uint32_t d0, d1, d2;
+                        if (qfast && (ro & 3) == 0) {
+                            const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rowp + colq[0]);
+                            d0 = p32[0];
+                            d1 = p32[1];
+                            d2 = p32[2];
+                        } else {  // reflected / unaligned columns (border tiles)
+                            const uint8_t *p0 = rowp + colq[0], *p1 = rowp + colq[1], *p2 = rowp + colq[2], *p3 = rowp + colq[3];
+                            d0 = p0[0] | (p0[1] << 8) | (p0[2] << 16) | ((uint32_t)p1[0] << 24);
+                            d1 = p1[1] | (p1[2] << 8) | (p2[0] << 16) | ((uint32_t)p2[1] << 24);
+                            d2 = p2[2] | (p3[0] << 8) | (p3[1] << 16) | ((uint32_t)p3[2] << 24);
+                        }
+                        g4 = gray4(d0, d1, d2);
+                        if (planes) *reinterpret_cast<uint32_t*>(G + gy * GWc + 4 * q) = g4;
+                    }
+                    uint32_t qv[NQN];
+                    qv[0] = g4;
+#pragma unroll
+                    for (int d = 1; d < NQN; d++) qv[d] = (uint32_t)__shfl_down((int)g4, d, 64);
+                    if (act && q < EW / 4) {
+                        uint32_t hq[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            uint32_t acc = 0;
+#pragma unroll
+                            for (int g = 0; g < NGRP; g++)
+                                acc = __builtin_amdgcn_udot4(j ? __builtin_amdgcn_alignbyte(qv[g + 1], qv[g], j) : qv[g],
+                                                             cpk[g], acc, false);
+#pragma unroll
+                            for (int tt = 4 * NGRP; tt < KC; tt++)
+                                acc += __umul24((uint32_t)cf[tt], (qv[(j + tt) >> 2] >> (8 * ((j + tt) & 3))) & 0xFFu);
+                            hq[j] = acc;
+                        }
+                        *reinterpret_cast<uint2*>(Hs + gy * EW + 4 * q) = make_uint2(hq[0] | (hq[1] << 16), hq[2] | (hq[3] << 16));
                     }
                 }
-                const uint64_t bits = __ballot(th);
-                if (ln == 0) Eb[ey] = bits;
+            }
+            lds_barrier();
+        } else {
+            // ---- gray over the G region (generic k)
+            if (!(dbg & 1)) {
+                for (int i = tid; i < L.GW * L.GW; i += NT) {
+                    const int gy = i / L.GW, gx = i - gy * L.GW;
+                    const uint8_t* p = smem + gy * L.RS + roff[gy] + colx[gx];
+                    G[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14);
+                }
+            }
+            lds_barrier();
+            // ---- horizontal taps (exact, 8 fraction bits)
+            if (!(dbg & 2)) {
+                for (int i = tid; i < L.GW * EW; i += NT) {
+                    const int gy = i / EW, c = i - gy * EW;
+                    const uint8_t* g = G + gy * L.GW + c;
+                    uint32_t acc = 0;
+                    for (int tt = 0; tt < k; tt++) acc += __umul24((uint32_t)cf[tt], g[tt]);
+                    Hs[i] = (uint16_t)acc;
+                }
+            }
+            lds_barrier();
+        }
+
+        // ---- vertical taps (sliding window over the wave's rows) + per-pixel
+        //      chain; threshold row bits by ballot
+        {
+            const int rsv = min(9 * wvv, 8 * wvv + 4), cntv = wvv < 4 ? 9 : 8;
+            uint32_t win[KC ? KC : 1];
+            if (KC) {
+#pragma unroll
+                for (int tt = 0; tt + 1 < (KC ? KC : 1); tt++) win[tt] = Hs[(rsv + tt) * EW + ln + 2];
+            }
+#pragma unroll
+            for (int j = 0; j < NCJ; j++) {
+                const int ey = rsv + j;
+                if (j < cntv && !(dbg & 4)) {  // wave-uniform
+                    if (KC) win[(KC ? KC : 1) - 1] = Hs[(ey + (KC ? KC : 1) - 1) * EW + ln + 2];
+                    const int y = y0v - 2 + ey, x = x0 + ln;
+                    bool th = false;
+                    if (y >= 0 && y < h && x < w) {
+                        int blur;
+                        if (KC) {
+                            uint32_t acc = 0;
+#pragma unroll
+                            for (int tt = 0; tt < (KC ? KC : 1); tt++) acc += __umul24((uint32_t)cf[tt], win[tt]);
+                            blur = (int)((acc + 32768u) >> 16);
+                        } else {
+                            blur = vblur<0>(Hs + ey * EW + ln + 2, cf, k);
+                        }
+                        const long long li = (long long)y * w + x;
+                        if (hk && keep[li] == 0) blur = 0;
+                        int d;
+                        const bool row_vec = (long long)y * w + x0 + 63 < vec_end;  // wave-uniform
+                        th = chain(blur, li, bgc[j], init, thresh, alpha, beta, vec_end, cvt_simd, d, row_vec);
+                        if (planes && ey >= 2 && ey < EW - 2) {
+                            const size_t o = f * plane + li;
+                            planes[o] = G[(ey + r) * L.GW + ln + 2 + r];
+                            planes[F * plane + o] = (uint8_t)blur;
+                            planes[2 * F * plane + o] = (uint8_t)d;
+                        }
+                    }
+                    const uint64_t bits = __ballot(th);
+                    if (ln == 0) Eb[ey] = bits;
+                    if (KC) {
+#pragma unroll
+                        for (int tt = 0; tt + 1 < (KC ? KC : 1); tt++) win[tt] = win[tt + 1];
+                    }
+                }
             }
         }
         if (tid < NHALO) {
@@ -362,7 +497,7 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
         lds_barrier();
 
         // ---- dilate 5x5 on bit rows (wave 0, lane = output row)
-        if (wv == 0) {
+        if (wv == 0 && !(dbg & 8)) {
             uint64_t C = 0, hl = 0, hr = 0;
 #pragma unroll
             for (int d = 0; d < 5; d++) {
@@ -384,7 +519,7 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
         lds_barrier();
 
         // ---- mask bytes out: 8 px per thread
-        {
+        if (!(dbg & 8)) {
             const int row = tid >> 3, oc = tid & 7;
             const int y = y0 + row, xs = x0 + 8 * oc;
             if (y < h && xs < w) {
@@ -405,8 +540,8 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
     double* bgo = a.bg_out + (size_t)s * plane;
 #pragma unroll
     for (int j = 0; j < NCJ; j++) {
-        const int ey = wv + NW * j, y = y0 - 2 + ey, x = x0 + ln;
-        if (ey >= 2 && ey < EW - 2 && y < h && x < w) bgo[(size_t)y * w + x] = bgc[j];
+        const int ey = rs + j, y = y0 - 2 + ey, x = x0 + ln;
+        if (j < cnt && ey >= 2 && ey < EW - 2 && y < h && x < w) bgo[(size_t)y * w + x] = bgc[j];
     }
 }
 
@@ -419,16 +554,27 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
 // background runs 4-wise (x ranges overlap).  Out-of-image pixels are
 // background and, like pixels on the image border, mark their background
 // component "outer" (they play the role of findContours' 1-px zero pad).
-__global__ __launch_bounds__(64) void k_tile_ccl(FusedArgs a) {
-    __shared__ int par[MAXR];
-    __shared__ int amin[MAXR];   // fg root: min x0; bg root: outer flag
-    __shared__ int amax[MAXR];
-    __shared__ int ay[MAXR];
-    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
-    __shared__ int rb[66];
-    const size_t f = blockIdx.y;
+struct CclScratch {
+    int* par;
+    int* amin;  // fg root: min x0; bg root: outer flag
+    int* amax;
+    int* ay;
+    uint8_t *rx0, *rx1, *rf;
+    int* rb;
+};
+
+// returns false (nothing written) if the tile has more than CAP runs
+template <int CAP>
+__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, const CclScratch& sc) {
+    int* par = sc.par;
+    int* amin = sc.amin;
+    int* amax = sc.amax;
+    int* ay = sc.ay;
+    uint8_t* rx0 = sc.rx0;
+    uint8_t* rx1 = sc.rx1;
+    uint8_t* rf = sc.rf;
+    int* rb = sc.rb;
     const size_t F = (size_t)a.T * a.S;
-    const int ti = blockIdx.x, ln = threadIdx.x;
     const int h = a.h, w = a.w;
     const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
     TileRec* TR = a.tiles + f * a.ntiles + ti;
@@ -451,7 +597,7 @@ __global__ __launch_bounds__(64) void k_tile_ccl(FusedArgs a) {
             nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
             NR[0] = nrec;
         }
-        return;
+        return true;
     }
 
     const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
@@ -464,12 +610,12 @@ __global__ __launch_bounds__(64) void k_tile_ccl(FusedArgs a) {
     }
     const int total = __shfl(incl, 63, 64);
     const int base = incl - nr;
-    if (total > MAXR) {  // impossible for a dilated mask (<= 24 runs per row); host relabels the frame
-        if (ln == 0) {
+    if (total > CAP) {
+        if (CAP >= MAXR && ln == 0) {  // impossible for a dilated mask (<= 24 runs per row); host relabels the frame
             TR->nroots = 0;
             atomicOr(&a.count[F + f], 1);
         }
-        return;
+        return CAP >= MAXR;
     }
     rb[ln] = base;
     if (ln == 63) rb[64] = total;
@@ -563,6 +709,46 @@ __global__ __launch_bounds__(64) void k_tile_ccl(FusedArgs a) {
     TR->edges[64 + ln] = (uint16_t)(par[base + nr - 1] | ((rf[base + nr - 1] & 1) << 15));
     TR->edges[128 + ln] = (uint16_t)(par[id0] | (((m0 >> ln) & 1) << 15));
     TR->edges[192 + ln] = (uint16_t)(par[id63] | (((m63 >> ln) & 1) << 15));
+    return true;
+}
+
+constexpr int LIGHT_RUNS = 256;   // most tiles: empty or a few blobs
+constexpr int CCL_WAVES = 4;
+
+// light pass: one wave per tile, 4 tiles per workgroup, small LDS; tiles with
+// more runs are appended to a work list for the heavy pass
+__global__ __launch_bounds__(64 * CCL_WAVES) void k_tile_ccl(FusedArgs a) {
+    __shared__ int par[CCL_WAVES][LIGHT_RUNS], amin[CCL_WAVES][LIGHT_RUNS], amax[CCL_WAVES][LIGHT_RUNS],
+        ay[CCL_WAVES][LIGHT_RUNS];
+    __shared__ uint8_t rx0[CCL_WAVES][LIGHT_RUNS], rx1[CCL_WAVES][LIGHT_RUNS], rf[CCL_WAVES][LIGHT_RUNS];
+    __shared__ int rb[CCL_WAVES][66];
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const long long item = (long long)blockIdx.x * CCL_WAVES + wv;
+    const long long nitems = (long long)a.T * a.S * a.ntiles;
+    if (item >= nitems) return;
+    const size_t f = item / a.ntiles;
+    const int ti = (int)(item - (long long)f * a.ntiles);
+    CclScratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv]};
+    if (!tile_ccl<LIGHT_RUNS>(a, f, ti, ln, sc) && ln == 0) {
+        const size_t F = (size_t)a.T * a.S;
+        const int slot = atomicAdd(&a.count[2 * F], 1);
+        a.heavy[slot] = (int)item;
+    }
+}
+
+// heavy pass: persistent workgroups drain the work list with full-size LDS
+__global__ __launch_bounds__(64) void k_tile_ccl_heavy(FusedArgs a) {
+    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
+    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
+    __shared__ int rb[66];
+    const size_t F = (size_t)a.T * a.S;
+    const int n = a.count[2 * F];
+    CclScratch sc{par, amin, amax, ay, rx0, rx1, rf, rb};
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int item = a.heavy[i];
+        const size_t f = item / a.ntiles;
+        tile_ccl<MAXR>(a, f, (int)(item - (long long)f * a.ntiles), threadIdx.x, sc);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -706,7 +892,10 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
     if (e != hipSuccess) return e;
     dim3 gm(a.ntiles, a.T * a.S);
     tok = tm ? tm->begin("tile_ccl") : -1;
-    hipLaunchKernelGGL(fz::k_tile_ccl, gm, dim3(64), 0, st, a);
+    const long long items = (long long)a.T * a.S * a.ntiles;
+    hipLaunchKernelGGL(fz::k_tile_ccl, dim3((unsigned)((items + fz::CCL_WAVES - 1) / fz::CCL_WAVES)),
+                       dim3(64 * fz::CCL_WAVES), 0, st, a);
+    hipLaunchKernelGGL(fz::k_tile_ccl_heavy, dim3(512), dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     tok = tm ? tm->begin("tile_merge") : -1;

@@ -81,10 +81,12 @@ struct FusedArgs {
     uint64_t* bits;              // [F][ntiles][64] dilated tile rows as bit masks (input of k_tile_ccl)
     TileRec* tiles;              // [F][ntiles]
     NodeRec* nodes;              // [F][nnodes]
-    int32_t* count;              // [F] external contours; count[F + f] = overflow flag
+    int32_t* count;              // [2F+1]: [f] external contours, [F+f] overflow flag, [2F] heavy-tile count
+    int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
     int32_t* rec;                // [F][cap][5]
     int T, S, h, w, ksize, thresh;
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
+    int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     double alpha, beta;
     long long acc_vec_end;
     int32_t coef[kMaxK];

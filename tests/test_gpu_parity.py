@@ -111,3 +111,31 @@ def test_random_masks_contours():
             f[t, 0] = img[..., None]
         fr.append(f)
     run_pair(W, H, W, ksize=1, T=2, n_batches=3, thresh=20, alpha=0.5, frames=fr)
+
+
+def _pattern_frames(patterns):
+    """Frames whose dilated threshold mask is dilate(pattern): frame 0 is black
+    (background init), every later frame is the pattern (ksize 1: no blur)."""
+    H, W = patterns[0].shape
+    fr = np.zeros((len(patterns) + 1, 1, H, W, 3), np.uint8)
+    for i, p in enumerate(patterns):
+        fr[i + 1, 0] = (p.astype(np.uint8) * 255)[..., None]
+    return fr
+
+
+def test_heavy_tiles_stripes_and_rings():
+    """Tiles with > 256 runs (heavy CCL pass) and nested rings (external test)."""
+    H, W = 150, 200
+    stripes = np.zeros((H, W), bool)
+    stripes[:, ::6] = True                      # dilates to 5-px bars with 1-px gaps: ~22 runs per row
+    rings = np.zeros((H, W), bool)
+    for k, (cy, cx) in enumerate([(40, 40), (75, 130), (120, 60)]):
+        for rad in (30, 18, 8):
+            yy, xx = np.ogrid[:H, :W]
+            d = np.abs(np.hypot(yy - cy, xx - cx) - rad)
+            rings |= d < 0.6
+        rings[cy, cx] = True                    # a dot inside the innermost ring
+    checker = np.zeros((H, W), bool)
+    checker[::7, ::7] = True
+    frames = _pattern_frames([stripes, rings, checker])
+    run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])

@@ -1,0 +1,24 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (tools/profile.sh output) per kernel: mean per dispatch."""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row["Kernel_Name"].split("(")[0]
+                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    for k, cs in acc.items():
+        print(k)
+        for c, v in sorted(cs.items()):
+            print(f"   {c:28s} mean/dispatch {sum(v)/len(v):16.1f}   (n={len(v)})")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_run")

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Profile the bench workload on the GPU box: kernel-trace stats + PMC passes.
+# Usage: tools/profile.sh <tag> [bench args...]   (outputs under gpurun_out/prof_<tag>/)
+set -o pipefail
+TAG=${1:-run}; shift
+OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
+[ -z "$GRAFT_REPO_ROOT" ] && OUT=$PWD/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1 || exit 1
+i=0
+for PMC in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+           "SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $PMC -d "$OUT/pmc$i" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+done
+echo "profile $TAG done"
