@@ -1,0 +1,38 @@
+"""Loader for the committed golden fixtures (tests/golden/, made by tests/golden/make_golden.py)."""
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def chain_files():
+    return sorted(glob.glob(os.path.join(GOLDEN, "chain_*.npz")))
+
+
+def load_chain(path):
+    d = np.load(path, allow_pickle=False)
+    W, H, box, k, T, thresh = (int(v) for v in d["params"])
+    case = {k_: d[k_] for k_ in d.files}
+    case.update(W=W, H=H, box=box, ksize=k, T=T, thresh=thresh, alpha=float(d["alpha"]),
+                has_keep=bool(int(d["has_keep"])), name=os.path.basename(path)[6:-4])
+    return case
+
+
+def boxes_of(case, t):
+    b = case["boxes"]
+    return [tuple(int(v) for v in r[1:]) for r in b[b[:, 0] == t]] if len(b) else []
+
+
+def origins_of(case, t):
+    o = case["origins"]
+    return [tuple(int(v) for v in r[1:]) for r in o[o[:, 0] == t]] if len(o) else []
+
+
+def contour_cases():
+    d = np.load(os.path.join(GOLDEN, "contours_external.npz"), allow_pickle=False)
+    names = sorted({k.split("__")[0] for k in d.files})
+    return {n: {"mask": d[n + "__mask"], "boxes": [tuple(int(v) for v in r) for r in d[n + "__boxes"]],
+                "origins": [tuple(int(v) for v in r) for r in d[n + "__origins"]], "areas": d[n + "__areas"]}
+            for n in names}

@@ -1,0 +1,402 @@
+"""Known-answer tests pinning the CPU oracle (oracle/fm_oracle.c).
+
+The reference has no tests and OpenCV is not installed here (SURVEY.md §4,
+§8c), so the oracle is pinned three ways:
+
+1. analytic known answers for each restated OpenCV op (Appendix A of
+   SURVEY.md), e.g. the 5x5 Gaussian impulse response, `.5` ties of
+   convertScaleAbs, RETR_EXTERNAL on nested rings;
+2. the independent numpy/scipy restatement in oracle/oracle_np.py, compared
+   bit-for-bit on seeded random inputs;
+3. real OpenCV when it happens to be importable (pytest.importorskip("cv2")).
+
+Each test names the reference call site (fm.py = find_motion/find_motion.py).
+CPU only.
+"""
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import oracle_np as onp
+
+# ---------------------------------------------------------------------------
+# geometry rules: _make_gaussian (fm.py:478-484), imutils.resize height (fm.py:492)
+
+
+@pytest.mark.parametrize("box,scale,k", [(100, 20, 5), (1920, 384, 5), (3840, 183, 21), (1920, 20, 97),
+                                         (3840, 20, 193), (640, 20, 33), (100, 50, 3), (100, 100, 1)])
+def test_make_gaussian(box, scale, k):
+    assert oracle.make_gaussian(box, scale) == k
+
+
+@pytest.mark.parametrize("H,W,box,h", [(1080, 1920, 100, 56), (480, 640, 100, 75), (2160, 3840, 3840, 2160),
+                                       (1080, 1920, 1920, 1080), (2160, 3840, 100, 56), (130, 230, 100, 56)])
+def test_work_height(H, W, box, h):
+    assert oracle.work_height(H, W, box) == h
+    assert oracle.lib().fmo_work_height(H, W, box) == h
+
+
+# ---------------------------------------------------------------------------
+# GaussianBlur fixed-point taps (fm.py:494)
+
+KNOWN_TAPS = {
+    1: [256],
+    3: [64, 128, 64],
+    5: [16, 64, 96, 64, 16],
+    7: [8, 28, 56, 72, 56, 28, 8],
+    21: [0, 2, 2, 4, 6, 11, 15, 20, 25, 28, 30, 28, 25, 20, 15, 11, 6, 4, 2, 2, 0],
+    33: [0, 1, 0, 1, 2, 2, 3, 5, 6, 8, 10, 12, 15, 16, 18, 19, 20, 19, 18, 16, 15, 12, 10, 8, 6, 5, 3, 2, 2, 1, 0, 1, 0],
+}
+
+
+@pytest.mark.parametrize("k", sorted(KNOWN_TAPS))
+def test_gauss_taps_known(k):
+    assert oracle.gauss_coeffs(k).tolist() == KNOWN_TAPS[k]
+
+
+def test_gauss_taps_all_odd_sizes_sum_256_symmetric_and_match_numpy():
+    for k in range(1, 256, 2):
+        c = oracle.gauss_coeffs(k)
+        assert c.sum() == 256, k
+        assert (c == c[::-1]).all(), k
+        assert (c >= 0).all(), k
+        assert c.tolist() == onp.gauss_coeffs(k).tolist(), k
+
+
+def test_gauss_even_size_rejected():
+    with pytest.raises(ValueError):
+        oracle.gauss_coeffs(4)
+
+
+def test_blur_impulse_response_k5():
+    img = np.zeros((11, 11), np.uint8)
+    img[5, 5] = 255
+    out = oracle.gauss_blur(img, 5)
+    b = np.array([16, 64, 96, 64, 16], np.int64)
+    want = np.zeros((11, 11), np.int64)
+    want[3:8, 3:8] = (np.outer(b, b) * 255 + 32768) >> 16
+    assert out[5, 5] == 36  # (255*36*256 + 2^15) >> 16
+    np.testing.assert_array_equal(out, want.astype(np.uint8))
+
+
+@pytest.mark.parametrize("k", [1, 3, 5, 7, 9, 21, 33, 97])
+def test_blur_constant_image_is_identity(k):
+    for v in (0, 1, 127, 200, 255):
+        img = np.full((23, 31), v, np.uint8)
+        np.testing.assert_array_equal(oracle.gauss_blur(img, k), img)
+
+
+@pytest.mark.parametrize("k", [3, 5, 7, 9, 11, 21, 33])
+@pytest.mark.parametrize("shape", [(1, 17), (17, 1), (2, 3), (13, 29), (40, 64)])
+def test_blur_c_vs_numpy(k, shape):
+    rng = np.random.default_rng(k * 100 + shape[0])
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.gauss_blur(img, k), onp.gauss_blur(img, k))
+
+
+def test_reflect101():
+    L = oracle.lib()
+    # BORDER_REFLECT_101: gfedcb|abcdefgh|gfedcba
+    assert [L.fmo_reflect101(p, 8) for p in range(-3, 11)] == [3, 2, 1, 0, 1, 2, 3, 4, 5, 6, 7, 6, 5, 4]
+    assert [L.fmo_reflect101(p, 1) for p in (-2, 0, 3)] == [0, 0, 0]
+    assert [L.fmo_reflect101(p, 3) for p in range(-6, 9)] == onp.reflect101_index(3, -6, 9).tolist()
+
+
+# ---------------------------------------------------------------------------
+# cvtColor(BGR2GRAY) (fm.py:493; A3)
+
+def test_bgr2gray_known():
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [0, 0, 0], [10, 20, 30]]], np.uint8)
+    want = [(255 * 1868 + 8192) >> 14, (255 * 9617 + 8192) >> 14, (255 * 4899 + 8192) >> 14, 255, 0,
+            (10 * 1868 + 20 * 9617 + 30 * 4899 + 8192) >> 14]
+    assert want[:3] == [29, 150, 76]
+    assert oracle.bgr2gray(px)[0].tolist() == want
+
+
+def test_bgr2gray_exhaustive_grey_axis_and_random():
+    g = np.arange(256, dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.bgr2gray(np.stack([g, g, g], -1)[None])[0], g)
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (64, 64, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.bgr2gray(img), onp.bgr2gray(img))
+
+
+# ---------------------------------------------------------------------------
+# resize(INTER_AREA) via imutils.resize(width=box) (fm.py:492; A1-A2)
+
+@pytest.mark.parametrize("s,d,lo,hi", [(1920, 100, 20, 20), (1080, 56, 20, 21), (3840, 100, 39, 40),
+                                       (640, 100, 7, 8), (480, 75, 7, 8)])
+def test_area_tab_taps(s, d, lo, hi):
+    tab = onp.area_tab(s, d)
+    taps = [len(e) for e in tab]
+    assert min(taps) >= lo - 1 and max(taps) <= hi + 1
+    assert oracle.lib().fmo_area_tab_size(s, d) == sum(taps)
+    # each destination's weights sum to 1 (within float32 rounding)
+    for e in tab:
+        assert abs(sum(float(a) for _, a in e) - 1.0) < 1e-5
+
+
+def test_area_tab_1920_to_100_is_exactly_20_taps():
+    assert oracle.lib().fmo_area_tab_size(1920, 100) == 2000
+
+
+@pytest.mark.parametrize("H,W,box", [(1080, 1920, 100), (480, 640, 100), (130, 230, 100), (96, 128, 64),
+                                     (90, 120, 40), (45, 77, 31), (61, 100, 99)])
+def test_resize_area_c_vs_numpy(H, W, box):
+    rng = np.random.default_rng(H + W + box)
+    src = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.resize_area_bgr(src, box), onp.resize_area_bgr(src, box))
+
+
+def test_resize_area_constant_and_identity():
+    src = np.full((108, 192, 3), 77, np.uint8)
+    assert (oracle.resize_area_bgr(src, 10) == 77).all()
+    rng = np.random.default_rng(2)
+    src = rng.integers(0, 256, (30, 40, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(oracle.resize_area_bgr(src, 40), src)  # dsize == ssize: plain copy
+
+
+def test_resize_area_fast_2x_rounds_half_up():
+    src = np.zeros((2, 2, 3), np.uint8)
+    src[0, 0] = 1
+    src[0, 1] = 1  # sum 2 -> (2 + 2) >> 2 = 1
+    assert oracle.resize_area_bgr(np.tile(src, (4, 4, 1)), 4)[0, 0, 0] == 1
+
+
+def test_resize_upscale_rejected():
+    with pytest.raises(ValueError):
+        oracle.resize_area_bgr(np.zeros((10, 10, 3), np.uint8), 20)
+
+
+# ---------------------------------------------------------------------------
+# convertScaleAbs + absdiff + threshold (fm.py:246-257; A5, A10)
+
+def test_convert_scale_abs_ties_round_half_even():
+    bg = np.array([0.5, 1.5, 2.5, 3.5, 254.5, 255.5, 300.0, -2.5, 7.0, 7.49, 7.51, 0.0, 1.0, 2.0, 3.0, 4.0])
+    blur = np.zeros(16, np.uint8)
+    delta, _ = oracle.diff_thresh(blur, bg, 255)
+    assert delta.tolist() == [0, 2, 2, 4, 254, 255, 255, 2, 7, 7, 8, 0, 1, 2, 3, 4]
+
+
+def test_convert_scale_abs_goes_through_float32_for_16_plus_elements():
+    # 2.5000000001 -> float32 2.5 -> even 2 on the SIMD path (>= 16 elements) ...
+    bg = np.full(16, 2.5000000001)
+    d16, _ = oracle.diff_thresh(np.zeros(16, np.uint8), bg, 255)
+    assert (d16 == 2).all()
+    # ... but the scalar path (< 16 elements) rounds the double: 3
+    d15, _ = oracle.diff_thresh(np.zeros(15, np.uint8), bg[:15].copy(), 255)
+    assert (d15 == 3).all()
+
+
+def test_threshold_is_strictly_greater():
+    blur = np.arange(0, 32, dtype=np.uint8)
+    bg = np.zeros(32)
+    delta, th = oracle.diff_thresh(blur, bg, 12)
+    assert th.tolist() == [255 if v > 12 else 0 for v in range(32)]
+    _, th = oracle.diff_thresh(blur, bg, -1)
+    assert (th == 255).all()
+    _, th = oracle.diff_thresh(blur, bg, 255)
+    assert (th == 0).all()
+
+
+def test_diff_thresh_c_vs_numpy():
+    rng = np.random.default_rng(3)
+    for n in (5, 15, 16, 17, 1000):
+        blur = rng.integers(0, 256, n, dtype=np.uint8)
+        bg = rng.random(n) * 300 - 20
+        bg[::7] = np.round(bg[::7]) + 0.5  # exact ties
+        for t in (0, 7, 12, 40):
+            a = oracle.diff_thresh(blur, bg, t)
+            b = onp.diff_thresh(blur, bg, t)
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_array_equal(a[1], b[1])
+
+
+# ---------------------------------------------------------------------------
+# accumulateWeighted (fm.py:659; A6)
+
+def _fma_exact(a: float, b: float, c: float) -> float:
+    return float(Fraction(a) * Fraction(b) + Fraction(c))  # correctly rounded, half-even
+
+
+def test_accumulate_fma_body_and_scalar_tail():
+    rng = np.random.default_rng(4)
+    n = 37  # 32 in the vector body, 5 in the scalar tail
+    src = rng.integers(0, 256, n, dtype=np.uint8)
+    bg0 = rng.random(n) * 255
+    for alpha in (0.1, 0.02, 0.5, 1.0 / 3.0):
+        bg = bg0.copy()
+        oracle.accumulate(src, bg, alpha)
+        beta = 1.0 - alpha
+        for i in range(n):
+            if i < 32:
+                want = _fma_exact(bg0[i], beta, float(src[i]) * alpha)
+            else:
+                want = float(src[i]) * alpha + bg0[i] * beta
+            assert bg[i] == want, (alpha, i)
+        np.testing.assert_allclose(bg, onp.accumulate_nofma(src, bg0, alpha), rtol=0, atol=1e-12)
+
+
+def test_accumulate_alpha_one_and_zero():
+    src = np.arange(20, dtype=np.uint8)
+    bg = np.full(20, 99.0)
+    oracle.accumulate(src, bg, 1.0)
+    np.testing.assert_array_equal(bg, src.astype(np.float64))
+    bg = np.full(20, 99.0)
+    oracle.accumulate(src, bg, 0.0)
+    assert (bg == 99.0).all()
+
+
+# ---------------------------------------------------------------------------
+# dilate(None, iterations=2) (fm.py:266; A7)
+
+def test_dilate_single_pixel_is_5x5_square():
+    m = np.zeros((9, 9), np.uint8)
+    m[4, 4] = 255
+    d = oracle.dilate5(m)
+    assert (d[2:7, 2:7] == 255).all() and d.sum() == 25 * 255
+    m = np.zeros((4, 4), np.uint8)
+    m[0, 0] = 255  # out-of-image pixels ignored (zero border)
+    assert oracle.dilate5(m)[:3, :3].all() and oracle.dilate5(m)[3].sum() == 0
+
+
+def test_dilate_c_vs_scipy():
+    rng = np.random.default_rng(5)
+    for shape in ((1, 1), (3, 70), (64, 64), (67, 131)):
+        m = ((rng.random(shape) < 0.05) * 255).astype(np.uint8)
+        np.testing.assert_array_equal(oracle.dilate5(m), onp.dilate5(m))
+
+
+# ---------------------------------------------------------------------------
+# findContours(RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) (fm.py:269-276; A8)
+
+def _count(m):
+    return len(oracle.find_contours_ext(np.ascontiguousarray(m)))
+
+
+def test_contours_nested_and_diagonal_known_answers():
+    m = np.zeros((20, 20), np.uint8)
+    m[2:18, 2:18] = 255
+    m[4:16, 4:16] = 0
+    m[8:12, 8:12] = 255
+    assert _count(m) == 1  # blob inside the ring's hole is not external
+    m = np.zeros((6, 6), np.uint8)
+    m[1, 1] = m[2, 2] = 255
+    assert _count(m) == 1  # 8-connected foreground
+    m = np.zeros((6, 6), np.uint8)
+    m[1, 1] = m[1, 3] = 255
+    assert _count(m) == 2
+    assert _count(np.zeros((5, 5), np.uint8)) == 0
+    assert _count(np.full((5, 5), 255, np.uint8)) == 1
+    # a hole closed only diagonally: background is 4-connected, so the inner dot is still nested
+    m = np.zeros((9, 9), np.uint8)
+    m[1:8, 1:8] = 255
+    m[2:7, 2:7] = 0
+    m[1, 4] = 0  # gap in the ring: hole now open to the outside
+    m[4, 4] = 255
+    assert _count(m) == 2
+    m[1, 4] = 255
+    m[1, 3] = 0
+    m[2, 3] = 0  # gap closed again (the ring reconnects diagonally around (1,3))
+    assert _count(m) in (1, 2)  # decided by the numpy topology check below
+    assert _count(m) == len(onp.external_components(m))
+
+
+def test_contours_bbox_and_origin():
+    m = np.zeros((10, 12), np.uint8)
+    m[2:5, 3:9] = 255
+    m[7, 0:12] = 255
+    cs = oracle.find_contours_ext(m)
+    assert [c["bbox"] for c in cs] == [(3, 2, 6, 3), (0, 7, 12, 1)]
+    assert [c["origin"] for c in cs] == [(3, 2), (0, 7)]
+    assert cs[0]["area"] == (6 - 1) * (3 - 1)  # contourArea of the traced border polygon
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_contours_c_vs_topological_numpy(seed):
+    rng = np.random.default_rng(100 + seed)
+    h, w = rng.integers(1, 60, 2)
+    p = [0.02, 0.2, 0.35, 0.5, 0.65, 0.9][seed % 6]
+    m = ((rng.random((h, w)) < p) * 255).astype(np.uint8)
+    if seed % 2:
+        m = oracle.dilate5(m)
+    got = [(c["origin"], c["bbox"]) for c in oracle.find_contours_ext(m)]
+    assert got == onp.external_components(m)
+
+
+# ---------------------------------------------------------------------------
+# the find_diff ordering (fm.py:638-662): first frame initialises bg, diff uses
+# the background BEFORE this frame's accumulate
+
+def test_oracle_stream_matches_composed_numpy_chain():
+    from find_motion_amd.synthetic import SyntheticVideo
+
+    W, H, box, k = 230, 130, 100, 5
+    cfg = oracle.OracleConfig(H=H, W=W, box=box, ksize=k, thresh=12, alpha=0.1)
+    st = oracle.OracleStream(cfg)
+    vid = SyntheticVideo(W, H, stream=1)
+    bg = None
+    for t in range(5):
+        fr = vid.frame(92 + t)
+        r = st.step(fr)
+        small = onp.resize_area_bgr(fr, box)
+        gray = onp.bgr2gray(small)
+        blur = onp.gauss_blur(gray, k)
+        if bg is None:
+            bg = blur.astype(np.float64)
+            assert r["count"] == 0
+        delta, th = onp.diff_thresh(blur, bg, 12)
+        bg = onp.accumulate_nofma(blur, bg, 0.1)
+        mask = onp.dilate5(th)
+        np.testing.assert_array_equal(r["gray"], gray)
+        np.testing.assert_array_equal(r["blur"], blur)
+        np.testing.assert_array_equal(r["delta"], delta)
+        np.testing.assert_array_equal(r["mask"], mask)
+        ext = onp.external_components(mask)
+        assert r["count"] == len(ext)
+        assert r["boxes"] == [b for _, b in ext]
+        np.testing.assert_allclose(st.bg, bg, rtol=0, atol=1e-9)
+
+
+def test_keep_mask_zeroes_blur_and_decays_background():
+    """Masks are applied to blur, so the stored background decays to 0 under a mask (Appendix B-10)."""
+    W = H = 32
+    cfg = oracle.OracleConfig(H=H, W=W, box=W, ksize=3, thresh=12, alpha=0.5)
+    keep = np.ones((H, W), np.uint8)
+    keep[:8, :8] = 0
+    st = oracle.OracleStream(cfg, keep)
+    fr = np.full((H, W, 3), 200, np.uint8)
+    for _ in range(3):
+        r = st.step(fr)
+    assert (r["blur"][:8, :8] == 0).all() and (st.bg[:8, :8] == 0).all()
+    assert (st.bg[8:, 8:] == 200).all()
+
+
+# ---------------------------------------------------------------------------
+# real OpenCV, wherever it exists (never required)
+
+def test_cross_check_against_real_opencv():
+    cv2 = pytest.importorskip("cv2")
+    rng = np.random.default_rng(9)
+    src = rng.integers(0, 256, (108, 192, 3), dtype=np.uint8)
+    small = cv2.resize(src, (100, 56), interpolation=cv2.INTER_AREA)
+    np.testing.assert_array_equal(oracle.resize_area_bgr(src, 100), small)
+    gray = cv2.cvtColor(small, cv2.COLOR_BGR2GRAY)
+    np.testing.assert_array_equal(oracle.bgr2gray(small), gray)
+    for k in (3, 5, 21):
+        np.testing.assert_array_equal(oracle.gauss_blur(gray, k), cv2.GaussianBlur(gray, (k, k), 0))
+    bg = rng.random(gray.shape) * 255
+    np.testing.assert_array_equal(oracle.diff_thresh(gray, bg, 12)[0], cv2.absdiff(gray, cv2.convertScaleAbs(bg)))
+    bg2 = bg.copy()
+    cv2.accumulateWeighted(gray, bg2, 0.1)
+    bg3 = bg.copy()
+    oracle.accumulate(gray, bg3, 0.1)
+    np.testing.assert_allclose(bg3, bg2, rtol=0, atol=1e-12)
+    th = ((rng.random((64, 80)) < 0.05) * 255).astype(np.uint8)
+    d = cv2.dilate(th, None, iterations=2)
+    np.testing.assert_array_equal(oracle.dilate5(th), d)
+    cnts = cv2.findContours(d, cv2.RETR_EXTERNAL, cv2.CHAIN_APPROX_SIMPLE)[-2]
+    assert len(cnts) == len(oracle.find_contours_ext(d))
+    assert sorted(cv2.boundingRect(c) for c in cnts) == sorted(c["bbox"] for c in oracle.find_contours_ext(d))
