@@ -95,18 +95,15 @@ def main() -> None:
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from find_motion_amd import dist
+
+    pl = dist.placement_from_env()
+    rank, world, local = pl.rank, pl.world, pl.local_rank
 
     import torch
 
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    active = dist.init(pl, "nccl", torch.device("cuda", local))
 
     from find_motion_amd import MotionEngine, make_gaussian, work_height
     from find_motion_amd.synthetic import SyntheticVideo
@@ -123,8 +120,8 @@ def main() -> None:
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
            "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
 
-    # synthetic ring [R][S][H][W][3], distinct streams per rank
-    vids = [SyntheticVideo(W, H, stream=rank * S + s) for s in range(S)]
+    # synthetic ring [R][S][H][W][3], distinct streams per rank (stream s -> rank s // S)
+    vids = [SyntheticVideo(W, H, stream=g) for g in dist.rank_streams(pl, S)]
     host = np.empty((R, S, H, W, 3), np.uint8)
     for t in range(R):
         for s in range(S):
@@ -145,22 +142,14 @@ def main() -> None:
         step(i)
     eng.reset_kernel_times()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
+    dist.barrier(active)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    dist.barrier(active)
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, active, device=f"cuda:{local}")
 
     ktimes = eng.kernel_times()
     total_frames = world * S * T * args.steps
@@ -223,8 +212,7 @@ def main() -> None:
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels}
         print(json.dumps(out), flush=True)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    dist.finalize(active)
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@ from ._native import (  # noqa: F401
     NativeLibraryMissing,
     rasterize_masks,
 )
+from .motion import StreamGroup, VideoError, VideoFrame, VideoMotion, run_vid  # noqa: F401,E402
 
 
 def make_gaussian(box_size: int, blur_scale: int) -> int:

@@ -149,6 +149,9 @@ class MotionEngine:
         self.max_batch = max_batch
         self.max_contours = max_contours
         self.last_batch = 0
+        self.keep_planes = bool(keep_planes)
+        self.generation = 0    # bumped at every wait(): results of older batches are gone
+        self._init = [False] * n_streams
         self._inflight = None  # keeps host frames alive until wait()
 
     # -- plumbing ------------------------------------------------------------
@@ -186,6 +189,11 @@ class MotionEngine:
 
     def reset(self, stream: int) -> None:
         self._check(self._L.fm_reset_stream(self._h, stream))
+        self._init[stream] = False
+
+    def initialized(self, stream: int) -> bool:
+        """True once the stream's background exists (after its first frame, fm.py:651-652)."""
+        return self._init[stream]
 
     def background(self, stream: int) -> np.ndarray:
         out = np.empty(self.work_shape, np.float64)
@@ -197,6 +205,7 @@ class MotionEngine:
         if bg.shape != self.work_shape:
             raise ValueError(f"background shape {bg.shape} != work shape {self.work_shape}")
         self._check(self._L.fm_write_background(self._h, stream, _ptr(bg)))
+        self._init[stream] = True
 
     def set_hip_stream(self, stream_handle: int | None) -> None:
         self._check(self._L.fm_set_hip_stream(self._h, stream_handle))
@@ -223,6 +232,8 @@ class MotionEngine:
         self._check(self._L.fm_wait(self._h))
         self._inflight = None
         self.last_batch = getattr(self, "_pending_n", 0)
+        self.generation += 1
+        self._init = [True] * self.n_streams
 
     def counts(self) -> np.ndarray:
         out = np.zeros((self.last_batch, self.n_streams), np.int32)

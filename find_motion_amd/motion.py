@@ -1,0 +1,674 @@
+"""Drop-in VideoMotion / VideoFrame whose per-frame cv2 chain runs on MI355X.
+
+Mirrors the reference's classes (find_motion/find_motion.py, "fm.py"):
+
+* VideoFrame  (fm.py:230-291) -- same attributes: raw, frame, in_cache,
+  contours, frame_delta, gray, thresh, blur, resized;
+* VideoMotion (fm.py:294-926) -- same constructor arguments and methods,
+  the same frame loop (find_motion, fm.py:852-904), the same movement /
+  output state machine (find_movement fm.py:665-700, decide_output
+  fm.py:549-589, cleanup_cache fm.py:592-601) and writer behaviour.
+
+What changes is the hot path.  blur_frame / mask_off_areas / find_diff
+(fm.py:487-494, 619-636, 638-662) no longer call cv2: the frames go through
+the C ABI (include/find_motion_amd.h) into one fused HIP kernel plus a GPU
+connected-components pass, and the results are bound back onto the
+VideoFrame:
+
+* frame.contours -- one Contour per external contour (len = the count
+  find_movement adds up, fm.py:694); Contour.bbox is cv2.boundingRect;
+* frame.thresh   -- the dilated threshold mask (fm.py:266), fetched from the
+  device on first access;
+* frame.gray / frame.blur / frame.frame_delta -- fetched on access when the
+  engine keeps planes (show or debug), else None;
+* VideoMotion.ref_frame -- the float64 background, read from the device on
+  access.  The mask polygons are rasterised once per video (they are static)
+  and applied inside the kernel, so mask_off_areas() has nothing left to do.
+
+Extra keyword arguments (not in the reference): device (HIP ordinal),
+batch (frames decoded ahead and processed per kernel launch; the per-frame
+results and the decisions are identical for any batch -- only ref_frame is
+then observed at batch boundaries), capture (a ready capture object).
+
+There is no CPU fallback: without the HIP library this module raises
+NativeLibraryMissing at VideoMotion construction.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import math
+import os
+import typing
+from collections import deque
+
+import numpy as np
+
+from . import videoio
+from ._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, MotionEngine, rasterize_masks
+
+log = logging.getLogger("find_motion_amd")
+
+BLACK = (0, 0, 0)
+RED = (0, 0, 255)
+GREEN = (0, 255, 0)
+
+# fm.py:104-122
+CASCADE_LOOKUP = {
+    "frontalcatface": "Cat 1",
+    "frontalcatface_extended": "Cat 2",
+    "frontalface_alt": "Face 1",
+    "frontalface_alt2": "Face 2",
+    "frontalface_alt_tree": "Face 3",
+    "frontalface_default": "Face 4",
+    "fullbody": "Person",
+    "lowerbody": "Legs",
+    "profileface": "Face 5",
+}
+
+
+class VideoError(Exception):
+    """fm.py:173-178"""
+
+
+def make_gaussian_size(box_size: int, blur_scale: int) -> int:
+    """VideoMotion._make_gaussian (fm.py:478-484)."""
+    k = int(box_size / blur_scale)
+    return k + 1 if k % 2 == 0 else k
+
+
+class _Bound:
+    """Where a frame's results live: (engine, batch generation, frame index in the batch, stream)."""
+
+    __slots__ = ("engine", "gen", "t", "s")
+
+    def __init__(self, engine, gen, t, s):
+        self.engine, self.gen, self.t, self.s = engine, gen, t, s
+
+    def fetch(self, what):
+        eng = self.engine
+        if eng.generation != self.gen:
+            raise RuntimeError("frame results were overwritten by a later batch; read them before the next batch")
+        if what == "thresh":
+            return eng.mask(self.t, self.s)
+        if not eng.keep_planes:
+            return None
+        return eng.plane({"gray": PLANE_GRAY, "blur": PLANE_BLUR, "frame_delta": PLANE_DELTA}[what], self.t, self.s)
+
+
+class VideoFrame:
+    """fm.py:230-291.  Holds one decoded frame and the hot path's results for it."""
+
+    _LAZY = ("gray", "blur", "frame_delta", "thresh")
+
+    def __init__(self, frame, show: bool = False) -> None:
+        self.raw = frame
+        # fm.py:236 always copies raw; the copy is only drawn on (show), so it is made only then
+        self.frame = frame.copy() if show else frame
+        self.in_cache = False
+        self.contours: list = []
+        self.resized = None
+        self._bound: typing.Optional[_Bound] = None
+        self._vals: dict = {}
+        self.processed = False
+        self.index = -1  # position in the source (set when the engine processes the frame)
+
+    def _get(self, name):
+        if name in self._vals:
+            return self._vals[name]
+        b = self._bound
+        if b is None:
+            return None
+        v = b.fetch(name)
+        self._vals[name] = v
+        return v
+
+    gray = property(lambda s: s._get("gray"), lambda s, v: s._vals.__setitem__("gray", v))
+    blur = property(lambda s: s._get("blur"), lambda s, v: s._vals.__setitem__("blur", v))
+    frame_delta = property(lambda s: s._get("frame_delta"), lambda s, v: s._vals.__setitem__("frame_delta", v))
+    thresh = property(lambda s: s._get("thresh"), lambda s, v: s._vals.__setitem__("thresh", v))
+
+    # fm.py:246-276 compute on the device (VideoMotion.find_diff); on a frame the
+    # engine has already processed these are no-ops that keep the reference's surface
+    def diff(self, ref_frame) -> None:
+        self._require()
+
+    def threshold(self, thresh) -> None:
+        self._require()
+
+    def find_contours(self) -> None:
+        self._require()
+
+    def _require(self):
+        if not self.processed:
+            raise RuntimeError("VideoFrame ops run on the GPU: pass the frame through VideoMotion.blur_frame/find_diff")
+
+    def cleanup(self) -> None:
+        """fm.py:279-291"""
+        for attr in ("frame", "contours"):
+            if attr in self.__dict__:
+                delattr(self, attr)
+        self._vals.clear()
+        self._bound = None
+        if self.in_cache:
+            return
+        if "raw" in self.__dict__:
+            del self.raw
+
+
+class VideoMotion:
+    """fm.py:294-926 with the per-frame chain on the GPU (see the module docstring)."""
+
+    # pylint: disable=too-many-instance-attributes,too-many-arguments
+    def __init__(self, filename: typing.Union[str, int, None] = None, outdir: str = "", fps: int = 30,
+                 box_size: int = 100, min_box_scale: int = 50, cache_time: float = 2.0, min_time: float = 0.5,
+                 threshold: int = 7, avg: float = 0.1, blur_scale: int = 20,
+                 mask_areas: list = None, show: bool = False,
+                 codec: str = "MJPG", log_level: int = logging.INFO,
+                 mem: bool = False, cleanup: bool = False,
+                 multiprocess: bool = False,
+                 cascades: typing.List[str] = None,
+                 yolo_tiny: bool = False, *,
+                 device: int = 0, batch: int = 1, capture=None, engine: MotionEngine = None,
+                 stream: int = 0, keep_planes: bool = None) -> None:
+        self.filename = filename
+        if self.filename is None and capture is None:
+            raise Exception("Filename required")
+        self.log = logging.getLogger("find_motion_amd.VideoMotion")
+        self.log.setLevel(log_level)
+        self.multiprocess = multiprocess
+        self.outfile = None
+        self.outfiles = 0
+        self.outfile_name = ""
+        self.outdir = os.path.normpath(outdir)
+        self.fps = fps
+        self.box_size = box_size
+        self.min_box_scale = min_box_scale
+        self.min_area = -1
+        self.max_area = -1
+        self.gaussian_scale = blur_scale
+        self.cache_frames = int(cache_time * fps)
+        self.min_movement_frames = int(min_time * fps)
+        self.delta_thresh = threshold
+        self.avg = avg
+        self.mask_areas = mask_areas if mask_areas is not None else []
+        self.show = show
+        self.cascade_names = cascades
+        self.codec = codec
+        self.debug = log_level == logging.DEBUG
+        self.mem = mem
+        self.cleanup_flag = cleanup
+        self.cascades = None
+        self._load_cascades()
+        self.tiny = yolo_tiny
+        self.amount_of_frames = -1
+        self.frame_width = -1
+        self.frame_height = -1
+        self.scale = -1.0
+        self.current_frame: typing.Optional[VideoFrame] = None
+        self.frame_cache: typing.Deque[VideoFrame] = deque()
+        self.wrote_frames: typing.Optional[bool] = False
+        self.err_msg = ""
+        self.movement = False
+        self.movement_decay = 0
+        self.movement_counter = 0
+        self.object_counter = 0
+        self.last_objects: typing.Dict[str, typing.List] = {}
+        self.seen_objects: typing.Set[str] = set()
+        # MI355X engine
+        self.device = int(device)
+        self.batch = max(1, int(batch))
+        self.keep_planes = (show or self.debug) if keep_planes is None else bool(keep_planes)
+        self._engine = engine
+        self._own_engine = engine is None
+        self._stream = int(stream)
+        self._capture = capture
+        self._ahead: typing.Deque[VideoFrame] = deque()
+        self.frames_read = 0
+        self.written_indices: typing.List[int] = []  # source frame indices written, in write order
+        self._calc_min_area()
+        self._make_gaussian()
+        self.loaded = self._load_video()
+
+    # -- init (fm.py:383-484) ------------------------------------------------
+    def _load_cascades(self) -> None:
+        """fm.py:383-399 (needs OpenCV's CascadeClassifier; without cv2 no cascade is loaded)."""
+        self.cascades = dict()
+        if self.cascade_names is None:
+            return
+        names = copy.copy(CASCADE_LOOKUP) if "ALL" in self.cascade_names else {
+            c: CASCADE_LOOKUP[c] for c in self.cascade_names if c in CASCADE_LOOKUP}
+        cv2 = videoio.cv2
+        if cv2 is None:
+            if names:
+                self.log.warning("Haar cascades %s need OpenCV, which is not installed: object detection off",
+                                 list(names))
+            return
+        base = os.path.join(cv2.data.haarcascades) if hasattr(cv2, "data") else ""
+        self.cascades = {title: cv2.CascadeClassifier(os.path.join(base, f"haarcascade_{c}.xml"))
+                         for c, title in names.items()}
+
+    def _calc_min_area(self) -> None:
+        """fm.py:402-406"""
+        self.min_area = int(math.pow(self.box_size / self.min_box_scale, 2))
+
+    def _make_gaussian(self) -> None:
+        """fm.py:478-484"""
+        g = make_gaussian_size(self.box_size, self.gaussian_scale)
+        self.gaussian = (g, g)
+
+    def _load_video(self) -> bool:
+        """fm.py:409-424, plus engine creation and the one-time mask rasterisation."""
+        self.cap = videoio.open_capture(self._capture if self._capture is not None else self.filename)
+        self.frame_cache = deque(maxlen=self.cache_frames)
+        try:
+            self._get_video_info()
+        except VideoError as e:
+            self.log.error(str(e))
+            return False
+        self.scale = self.box_size / self.frame_width
+        self.max_area = int((self.frame_width * self.frame_height) / 2 * self.scale)
+        if self.max_area < self.min_area:
+            # the contourArea filter of fm.py:684 is live only in this corner; it needs
+            # traced contour areas, which the GPU path does not produce
+            raise VideoError(f"max_area {self.max_area} < min_area {self.min_area}: the contour-area filter "
+                             f"(fm.py:684) is not supported by the GPU path")
+        if self._engine is None:
+            self._engine = MotionEngine(n_streams=1, src_w=self.frame_width, src_h=self.frame_height,
+                                        box_size=self.box_size, ksize=self.gaussian[0], threshold=self.delta_thresh,
+                                        avg=self.avg, max_batch=self.batch, keep_planes=self.keep_planes,
+                                        device=self.device)
+        if self.mask_areas:
+            h, w = self._engine.work_shape
+            self._engine.set_mask(self._stream, rasterize_masks(h, w, self.scale, self.mask_areas))
+        return True
+
+    def _get_video_info(self) -> None:
+        """fm.py:427-444"""
+        self.amount_of_frames = int(self.cap.get(videoio.CAP_PROP_FRAME_COUNT))
+        self.frame_width = int(self.cap.get(videoio.CAP_PROP_FRAME_WIDTH))
+        self.frame_height = int(self.cap.get(videoio.CAP_PROP_FRAME_HEIGHT))
+        if self.frame_width == 0 or self.frame_height == 0:
+            broken = "width" if self.frame_width == 0 else "height"
+            raise VideoError("Video info malformed - {} is 0: {}".format(broken, self.filename))
+        if self.amount_of_frames == 0:
+            log.warning("Video info malformed - frames reported as 0")
+
+    @property
+    def engine(self) -> MotionEngine:
+        return self._engine
+
+    # -- background state (VideoMotion.ref_frame, fm.py:363, 414, 651-659) ----
+    @property
+    def ref_frame(self):
+        """float64 background after the most recent batch (None before the first frame)."""
+        eng = self._engine
+        if eng is None or not eng.initialized(self._stream):
+            return None
+        return eng.background(self._stream)
+
+    @ref_frame.setter
+    def ref_frame(self, value):
+        eng = self._engine
+        if eng is None:
+            return
+        if value is None:
+            eng.reset(self._stream)
+        else:
+            eng.set_background(self._stream, np.asarray(value, dtype=np.float64))
+
+    # -- I/O (fm.py:497-546) ---------------------------------------------------
+    def read(self) -> bool:
+        """fm.py:497-506, with up to `batch` frames decoded ahead and processed in one launch."""
+        if not self._ahead:
+            frames = []
+            for _ in range(self.batch):
+                ok, fr = self.cap.read()
+                if not ok:
+                    break
+                frames.append(fr)
+            if not frames:
+                return False
+            self._process(frames)
+        self.current_frame = self._ahead.popleft()
+        return True
+
+    def _process(self, raws: list) -> None:
+        """The hot path for a run of frames of this stream (single-stream engine)."""
+        eng = self._engine
+        if eng.n_streams != 1:
+            raise RuntimeError("a shared multi-stream engine is driven by StreamGroup")
+        vfs = [VideoFrame(r, self.show) for r in raws]
+        eng.submit(np.stack([r[None] for r in raws]))
+        eng.wait()
+        self.bind_results(vfs, eng, 0)
+        self._ahead.extend(vfs)
+
+    def bind_results(self, vfs, eng, stream: int) -> None:
+        for t, vf in enumerate(vfs):
+            vf._bound = _Bound(eng, eng.generation, t, stream)
+            vf.contours = eng.contours(t, stream)
+            vf.processed = True
+            vf.index = self.frames_read
+            self.frames_read += 1
+
+    def _make_outfile(self) -> None:
+        """fm.py:447-475"""
+        self.outfiles += 1
+        if self.outfiles > 1 and self.outfile is not None:
+            self.outfile.release()
+        outname = str(self.filename) + "_" + str(self.outfiles)
+        if self.outdir in ("", "."):
+            self.outfile_name = outname + "_motion.avi"
+        else:
+            self.outfile_name = os.path.join(self.outdir, os.path.basename(outname)) + "_motion.avi"
+        self.outfile = videoio.open_writer(self.outfile_name, self.codec, self.fps,
+                                           (self.frame_width, self.frame_height))
+
+    def output_frame(self, frame: VideoFrame = None) -> None:
+        """fm.py:509-530"""
+        frame = self.current_frame if frame is None else frame
+        if self.show and videoio.cv2 is not None:
+            videoio.cv2.imshow("frame", frame.frame)
+        self._write(frame.raw, getattr(frame, "index", -1))
+
+    def output_raw_frame(self, frame: np.ndarray = None, index: int = -1) -> None:
+        """fm.py:533-546"""
+        self._write(frame, index)
+
+    def _write(self, raw, index):
+        if not self.wrote_frames:
+            self._make_outfile()
+            self.wrote_frames = True
+        try:
+            self.outfile.write(raw)
+        except Exception as e:  # noqa: BLE001 (fm.py:527-530)
+            self.log.warning("Having to create output file due to exception: {}".format(e))
+            self._make_outfile()
+            self.outfile.write(raw)
+        self.written_indices.append(index)
+
+    # -- the hot path (fm.py:487-494, 619-636, 638-662) ------------------------
+    def blur_frame(self, frame: VideoFrame = None) -> None:
+        """resize -> cvtColor -> GaussianBlur: runs (fused with the rest) on the GPU at read()."""
+        frame = self.current_frame if frame is None else frame
+        if not frame.processed:
+            if self._ahead:
+                raise RuntimeError("cannot process an external frame while decoded frames are pending")
+            self._process_external(frame)
+
+    def _process_external(self, frame: VideoFrame) -> None:
+        eng = self._engine
+        eng.submit(np.asarray(frame.raw, dtype=np.uint8)[None, None])
+        eng.wait()
+        self.bind_results([frame], eng, self._stream)
+
+    def mask_off_areas(self, frame: VideoFrame = None):
+        """Masks are rasterised once per video (_load_video) and applied inside the fused kernel."""
+        return None
+
+    def find_diff(self, frame: VideoFrame = None) -> None:
+        """absdiff/threshold/accumulateWeighted/dilate/findContours: done on the GPU with blur_frame."""
+        frame = self.current_frame if frame is None else frame
+        if not frame.processed:
+            raise Exception("Blur frame is None")  # fm.py:648-649
+
+    # -- consumer state machine (fm.py:549-601, 665-700) -----------------------
+    def find_movement(self, frame: VideoFrame = None) -> None:
+        """fm.py:665-700.  The area filter of fm.py:684 can only skip a contour when
+        max_area < min_area, which _load_video rejects, so every contour counts."""
+        frame = self.current_frame if frame is None else frame
+        self.movement = False
+        self.movement_decay -= 1 if self.movement_decay > 0 else 0
+        if frame.contours is not None and len(frame.contours) > 0:
+            for contour in frame.contours:
+                if self.show:
+                    self.draw_box(self.make_box(contour, frame), frame)
+                self.movement_counter += 1
+                self.movement = True
+        if not self.movement:
+            self.movement_counter = 0
+
+    def decide_output(self) -> None:
+        """fm.py:549-589"""
+        if (self.movement_counter >= self.min_movement_frames) or (self.movement_decay > 0):
+            if self.movement:
+                self.movement_decay = self.cache_frames
+                for frame in self.frame_cache:
+                    if frame is not None:
+                        self.output_raw_frame(frame.raw, getattr(frame, "index", -1))
+                        if self.cleanup_flag:
+                            frame.in_cache = False
+                            frame.cleanup()
+                self.frame_cache.clear()
+            objects = self.find_objects()
+            if objects:
+                self.seen_objects.update(objects)
+            if self.show:
+                self.draw_text()
+            self.output_frame()
+        else:
+            if self.cleanup_flag:
+                self.cleanup_cache()
+            self.frame_cache.append(self.current_frame)
+            self.current_frame.in_cache = True
+
+    def cleanup_cache(self) -> None:
+        """fm.py:592-601"""
+        if len(self.frame_cache) == self.cache_frames and self.cache_frames > 0:
+            f = self.frame_cache.popleft()
+            if f is not None:
+                f.in_cache = False
+                f.cleanup()
+
+    def is_open(self) -> bool:
+        """fm.py:604-608"""
+        return bool(self._ahead) or self.cap.isOpened()
+
+    @staticmethod
+    def scale_area(area, scale: float) -> list:
+        """fm.py:611-616"""
+        return [(int(a[0] * scale), int(a[1] * scale)) for a in area]
+
+    # -- objects (fm.py:703-762): Haar needs OpenCV; cvlib YOLO is not available offline
+    def find_objects(self, frame: VideoFrame = None, width=300, skip=15, scaleFactor=1.1, minNeighbours=5,
+                     confidence=0.25) -> typing.Set[str]:
+        frame = self.current_frame if frame is None else frame
+        self.object_counter += 1
+        if self.object_counter != skip:
+            return set()
+        self.object_counter = 0
+        self.last_objects = {}
+        cv2 = videoio.cv2
+        if cv2 is not None and self.cascades:
+            h = int(frame.raw.shape[0] * (width / float(frame.raw.shape[1])))
+            frame.resized = cv2.resize(frame.raw, (width, h), interpolation=cv2.INTER_AREA)
+            for title, cascade in self.cascades.items():
+                found = cascade.detectMultiScale(frame.resized, scaleFactor=scaleFactor, minNeighbors=minNeighbours)
+                for rect in found:
+                    self.last_objects.setdefault(title, []).append(VideoMotion.make_area_from_rect(rect))
+        return set(self.last_objects.keys())
+
+    # -- display (fm.py:765-821): only with OpenCV and --show
+    @staticmethod
+    def find_centre(area) -> typing.Tuple[int, int]:
+        return ((area[0][0] + area[1][0]) // 2, (area[0][1] + area[1][1]) // 2)
+
+    def draw_text(self, frame: VideoFrame = None) -> None:
+        frame = self.current_frame if frame is None else frame
+        if videoio.cv2 is not None:
+            videoio.cv2.putText(frame.frame, "Status: {}".format("motion" if self.movement else "quiet"), (10, 20),
+                                videoio.cv2.FONT_HERSHEY_SIMPLEX, 0.5, RED, 2)
+
+    def make_box(self, contour, frame: VideoFrame = None):
+        """fm.py:787-792: boundingRect -> ((x, y), (x + w, y + h))"""
+        return VideoMotion.make_area_from_rect(contour.bbox)
+
+    @staticmethod
+    def make_area_from_box(object_tuple):
+        (x1, y1, x2, y2) = object_tuple
+        return ((x1, y1), (x2, y2))
+
+    @staticmethod
+    def make_area_from_rect(object_tuple):
+        (x, y, w, h) = object_tuple
+        return ((x, y), (x + w, y + h))
+
+    def draw_box(self, area, frame: VideoFrame = None) -> None:
+        frame = self.current_frame if frame is None else frame
+        if videoio.cv2 is not None:
+            videoio.cv2.rectangle(frame.frame, *self.scale_area(area, 1 / self.scale), GREEN, 2)
+
+    @staticmethod
+    def key_pressed(key: str) -> bool:
+        """fm.py:816-821 (waitKey only exists with OpenCV)."""
+        cv2 = videoio.cv2
+        return cv2 is not None and (cv2.waitKey(1) & 0xFF) == ord(key)
+
+    def show_frames(self) -> None:
+        cv2 = videoio.cv2
+        if cv2 is None:
+            return
+        cf = self.current_frame
+        for name in ("thresh", "gray", "blur", "raw"):
+            img = getattr(cf, name, None)
+            if img is not None:
+                cv2.imshow(name, img)
+
+    def cleanup(self) -> None:
+        """fm.py:824-849, plus releasing the device context."""
+        if self.cap is not None:
+            self.cap.release()
+        if self.outfile is not None:
+            self.outfile.release()
+        if self.cleanup_flag and self.current_frame is not None:
+            self.current_frame.in_cache = False
+            self.current_frame.cleanup()
+            for frame in self.frame_cache:
+                if frame is not None:
+                    frame.in_cache = False
+                    frame.cleanup()
+            self.frame_cache.clear()
+        if self._own_engine and self._engine is not None:
+            self._engine.close()
+            self._engine = None
+
+    # -- main loop (fm.py:852-904) ---------------------------------------------
+    def step(self) -> None:
+        """Everything the loop does with one frame after the hot path (fm.py:870-892)."""
+        try:
+            self.find_movement()
+        except Exception as e:  # noqa: BLE001 (fm.py:873-876)
+            self.log.error("find_movement: {}".format(e))
+        self.decide_output()
+        if self.show:
+            self.show_frames()
+        self.current_frame.cleanup()
+
+    def find_motion(self) -> tuple:
+        while self.is_open():
+            if not self.read():
+                break
+            self.blur_frame()
+            self.mask_off_areas()
+            self.find_diff()
+            self.step()
+            if self.show and VideoMotion.key_pressed("q"):
+                self.wrote_frames = None
+                self.err_msg = "Closing video at user request"
+                break
+        self.cleanup()
+        return self.wrote_frames, self.err_msg, tuple(self.seen_objects)
+
+
+def run_vid(filename, **kwargs) -> tuple:
+    """fm.py:1021-1037 (the unbound seen_objects of the reference's error path is None here)."""
+    seen_objects = None
+    try:
+        vid = VideoMotion(filename=filename, **kwargs)
+        if vid.loaded:
+            wrote_frames, err_msg, seen_objects = vid.find_motion()
+        else:
+            wrote_frames = None
+            err_msg = "Video did not load successfully"
+            vid.cleanup()
+    except Exception as e:  # noqa: BLE001
+        err_msg = "Error processing video {}: {}".format(filename, e)
+        wrote_frames = None
+    return (wrote_frames, filename, err_msg, seen_objects)
+
+
+class StreamGroup:
+    """S same-sized videos on ONE device, batched into one launch per frame step.
+
+    The reference runs one video per worker process (run_pool, fm.py:1054-1122).
+    On MI355X the streams of a device share one fm_ctx with one background
+    model per stream, so one fused launch covers T frames of all S streams.
+    Each stream keeps its own VideoMotion state machine and writer; results
+    are gathered per stream as run_vid returns them.
+    """
+
+    def __init__(self, filenames: list, batch: int = 8, device: int = 0, captures: list = None, engine=None,
+                 **kwargs):
+        self.filenames = list(filenames)
+        S = len(self.filenames)
+        if S == 0:
+            raise ValueError("More than 0 files needed")
+        caps = [videoio.open_capture(c if c is not None else f)
+                for f, c in zip(self.filenames, captures or [None] * S)]
+        w = {int(c.get(videoio.CAP_PROP_FRAME_WIDTH)) for c in caps}
+        h = {int(c.get(videoio.CAP_PROP_FRAME_HEIGHT)) for c in caps}
+        if len(w) != 1 or len(h) != 1:
+            raise VideoError("StreamGroup streams must share one frame size")
+        W, H = w.pop(), h.pop()
+        box = kwargs.get("box_size", 100)
+        blur_scale = kwargs.get("blur_scale", 20)
+        show = kwargs.get("show", False)
+        dbg = kwargs.get("log_level", logging.INFO) == logging.DEBUG
+        self.batch = max(1, int(batch))
+        make = engine if engine is not None else MotionEngine  # engine: a factory with MotionEngine's signature
+        self.engine = make(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=make_gaussian_size(box, blur_scale),
+                           threshold=kwargs.get("threshold", 7), avg=kwargs.get("avg", 0.1), max_batch=self.batch,
+                           keep_planes=show or dbg, device=device)
+        self.videos = [VideoMotion(filename=f, capture=c, engine=self.engine, stream=s, batch=self.batch, **kwargs)
+                       for s, (f, c) in enumerate(zip(self.filenames, caps))]
+        self._staging = np.empty((self.batch, S, H, W, 3), np.uint8)
+
+    def find_motion(self) -> list:
+        S = len(self.videos)
+        live = [v.loaded for v in self.videos]
+        last = [None] * S
+        while any(live):
+            got = [[] for _ in range(S)]
+            for s, v in enumerate(self.videos):
+                while live[s] and len(got[s]) < self.batch:
+                    ok, fr = v.cap.read()
+                    if not ok:
+                        live[s] = False
+                        break
+                    got[s].append(fr)
+            T = max(len(g) for g in got)
+            if T == 0:
+                break
+            for s in range(S):
+                for t in range(T):
+                    if t < len(got[s]):
+                        self._staging[t, s] = got[s][t]
+                        last[s] = got[s][t]
+                    elif last[s] is not None:
+                        self._staging[t, s] = last[s]  # ended stream: padding, results dropped
+            self.engine.submit(self._staging[:T])
+            self.engine.wait()
+            for s, v in enumerate(self.videos):
+                vfs = [VideoFrame(r, v.show) for r in got[s]]
+                v.bind_results(vfs, self.engine, s)
+                for vf in vfs:
+                    v.current_frame = vf
+                    v.step()
+        out = []
+        for f, v in zip(self.filenames, self.videos):
+            v.cleanup()
+            out.append((v.wrote_frames if v.loaded else None, f, v.err_msg if v.loaded else
+                        "Video did not load successfully", tuple(v.seen_objects) if v.loaded else None))
+        self.engine.close()
+        return out

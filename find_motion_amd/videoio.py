@@ -1,0 +1,293 @@
+"""Frame sources and sinks for the host side of the motion loop.
+
+The reference reads with cv2.VideoCapture (fm.py:413, 501) and writes the
+motion frames with cv2.VideoWriter (fm.py:447-475).  Decode/encode stay on
+the host (BASELINE.json north_star), so this module only adapts what is
+available:
+
+* OpenCV, when importable: cv2.VideoCapture / cv2.VideoWriter, as the
+  reference does;
+* otherwise (this image has no cv2): uncompressed RIFF AVI (BI_RGB, 24-bit
+  BGR, bottom-up rows), read and written here -- the container OpenCV itself
+  writes for fourcc 'DIB ' and reads through FFmpeg's rawvideo decoder;
+* in-memory sources for tests, benchmarks and embedding: ArrayCapture over a
+  [N][H][W][3] uint8 array and SyntheticCapture over the deterministic
+  synthetic video of find_motion_amd.synthetic.
+
+Every capture implements the subset of the cv2.VideoCapture protocol the
+reference uses: isOpened(), read() -> (ok, frame), get(CAP_PROP_*), release().
+"""
+from __future__ import annotations
+
+import logging
+import os
+import struct
+
+import numpy as np
+
+log = logging.getLogger("find_motion_amd.videoio")
+
+try:  # pragma: no cover - OpenCV is not installed in the build image
+    import cv2  # type: ignore
+except Exception:  # noqa: BLE001
+    cv2 = None
+
+# cv2.CAP_PROP_* values (videoio.hpp)
+CAP_PROP_FPS = 5
+CAP_PROP_FRAME_WIDTH = 3
+CAP_PROP_FRAME_HEIGHT = 4
+CAP_PROP_FRAME_COUNT = 7
+
+
+class ArrayCapture:
+    """VideoCapture protocol over an in-memory uint8 array [N][H][W][3] (BGR)."""
+
+    def __init__(self, frames, fps: float = 30.0):
+        self._frames = frames
+        self._i = 0
+        self._open = True
+        self._fps = float(fps)
+
+    def isOpened(self) -> bool:  # noqa: N802 (cv2 protocol)
+        return self._open
+
+    def read(self):
+        if not self._open or self._i >= len(self._frames):
+            return False, None
+        f = np.ascontiguousarray(self._frames[self._i], dtype=np.uint8)
+        self._i += 1
+        return True, f
+
+    def get(self, prop: int) -> float:
+        n = len(self._frames)
+        if prop == CAP_PROP_FRAME_COUNT:
+            return float(n)
+        if n == 0:
+            return 0.0
+        shape = self._frames[0].shape
+        if prop == CAP_PROP_FRAME_WIDTH:
+            return float(shape[1])
+        if prop == CAP_PROP_FRAME_HEIGHT:
+            return float(shape[0])
+        if prop == CAP_PROP_FPS:
+            return self._fps
+        return 0.0
+
+    def release(self) -> None:
+        self._open = False
+
+
+class SyntheticCapture(ArrayCapture):
+    """The seeded synthetic stream of find_motion_amd.synthetic as a capture (frames made on demand)."""
+
+    def __init__(self, width: int, height: int, n_frames: int, stream: int = 0, seed: int = 1000, start: int = 0):
+        from .synthetic import SyntheticVideo
+
+        self.video = SyntheticVideo(width, height, stream, seed=seed)
+        self.n_frames, self.start = int(n_frames), int(start)
+
+        class _Lazy:
+            def __len__(s):  # noqa: N805
+                return self.n_frames
+
+            def __getitem__(s, i):  # noqa: N805
+                return self.video.frame(self.start + i)
+
+            @property
+            def shape(s):  # noqa: N805
+                return (self.n_frames, height, width, 3)
+
+        super().__init__(_Lazy())
+        self._first_shape = (height, width, 3)
+
+    def get(self, prop: int) -> float:
+        if prop == CAP_PROP_FRAME_COUNT:
+            return float(self.n_frames)
+        if prop == CAP_PROP_FRAME_WIDTH:
+            return float(self._first_shape[1])
+        if prop == CAP_PROP_FRAME_HEIGHT:
+            return float(self._first_shape[0])
+        return super().get(prop)
+
+
+# ---------------------------------------------------------------------------
+# uncompressed AVI
+
+def _fourcc(s: str) -> bytes:
+    return s.encode("ascii")[:4].ljust(4, b" ")
+
+
+class RawAviWriter:
+    """Uncompressed 24-bit BGR AVI (RIFF, one video stream, idx1 index)."""
+
+    def __init__(self, path: str, fps: float, size):
+        self.path = path
+        self.w, self.h = int(size[0]), int(size[1])
+        self.fps = max(1, int(round(fps)))
+        self.row = (self.w * 3 + 3) & ~3
+        self.frame_bytes = self.row * self.h
+        self.n = 0
+        self.index = []
+        self.f = open(path, "wb")
+        self._write_headers()
+
+    def _write_headers(self):
+        f = self.f
+        f.write(b"RIFF" + struct.pack("<I", 0) + b"AVI ")
+        hdrl = bytearray()
+        avih = struct.pack("<IIIIIIIIII16x", 1000000 // self.fps, self.frame_bytes * self.fps, 0, 0x10, 0, 0, 1,
+                           self.frame_bytes, self.w, self.h)
+        hdrl += b"avih" + struct.pack("<I", len(avih)) + avih
+        strh = struct.pack("<4s4sIHHIIIIIIIIhhhh", b"vids", b"DIB ", 0, 0, 0, 0, 1, self.fps, 0, 0, self.frame_bytes,
+                           0xFFFFFFFF, 0, 0, 0, self.w, self.h)
+        strf = struct.pack("<IiiHHIIiiII", 40, self.w, self.h, 1, 24, 0, self.frame_bytes, 0, 0, 0, 0)
+        strl = b"strl" + b"strh" + struct.pack("<I", len(strh)) + strh + b"strf" + struct.pack("<I", len(strf)) + strf
+        hdrl += b"LIST" + struct.pack("<I", len(strl)) + strl
+        f.write(b"LIST" + struct.pack("<I", len(hdrl) + 4) + b"hdrl" + hdrl)
+        self._avih_frames_at = 12 + 8 + 4 + 8 + 16  # RIFF hdr, LIST hdr, 'hdrl', 'avih' hdr, 4 dwords
+        self._strh_len_at = 12 + 8 + 4 + 8 + len(avih) + 8 + 4 + 8 + 32
+        self._movi_at = f.tell()
+        f.write(b"LIST" + struct.pack("<I", 0) + b"movi")
+
+    def isOpened(self) -> bool:  # noqa: N802
+        return self.f is not None
+
+    def write(self, frame: np.ndarray) -> None:
+        frame = np.asarray(frame, dtype=np.uint8)
+        if frame.shape != (self.h, self.w, 3):
+            raise ValueError(f"frame shape {frame.shape} != ({self.h}, {self.w}, 3)")
+        buf = np.zeros((self.h, self.row), np.uint8)
+        buf[:, : self.w * 3] = frame[::-1].reshape(self.h, self.w * 3)  # bottom-up rows
+        off = self.f.tell() - (self._movi_at + 8)
+        self.f.write(b"00db" + struct.pack("<I", self.frame_bytes))
+        self.f.write(buf.tobytes())
+        self.index.append(off)
+        self.n += 1
+
+    def release(self) -> None:
+        if self.f is None:
+            return
+        f = self.f
+        movi_end = f.tell()
+        f.write(b"idx1" + struct.pack("<I", 16 * len(self.index)))
+        for off in self.index:
+            f.write(b"00db" + struct.pack("<III", 0x10, off, self.frame_bytes))
+        end = f.tell()
+        f.seek(4)
+        f.write(struct.pack("<I", end - 8))
+        f.seek(self._movi_at + 4)
+        f.write(struct.pack("<I", movi_end - self._movi_at - 8))
+        f.seek(self._avih_frames_at)
+        f.write(struct.pack("<I", self.n))
+        f.seek(self._strh_len_at)
+        f.write(struct.pack("<I", self.n))
+        f.close()
+        self.f = None
+
+
+class RawAviCapture:
+    """Reader for uncompressed 24-bit AVI (what RawAviWriter and OpenCV's 'DIB ' writer produce)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self._offsets = []
+        self.w = self.h = 0
+        self.fps = 30.0
+        self._i = 0
+        self._open = False
+        try:
+            self._parse()
+            self._open = self.w > 0 and self.h > 0
+        except (OSError, ValueError, struct.error) as e:
+            log.error("cannot read %s as uncompressed AVI: %s", path, e)
+
+    def _parse(self):
+        with open(self.path, "rb") as f:
+            data = f.read(12)
+            if len(data) < 12 or data[:4] != b"RIFF" or data[8:12] != b"AVI ":
+                raise ValueError("not a RIFF AVI file")
+            size = os.path.getsize(self.path)
+            self._walk(f, 12, size, depth=0)
+        self._mm = np.memmap(self.path, dtype=np.uint8, mode="r")
+
+    def _walk(self, f, start, end, depth):
+        pos = start
+        while pos + 8 <= end:
+            f.seek(pos)
+            ck, ln = struct.unpack("<4sI", f.read(8))
+            body = pos + 8
+            if ck == b"LIST":
+                kind = f.read(4)
+                if kind in (b"hdrl", b"strl", b"movi", b"rec ") and depth < 4:
+                    self._walk(f, body + 4, min(body + ln, end), depth + 1)
+            elif ck == b"avih":
+                vals = struct.unpack("<10I", f.read(40))
+                if vals[0]:
+                    self.fps = 1e6 / vals[0]
+            elif ck == b"strf" and not self.w:
+                bi = struct.unpack("<IiiHHI", f.read(20))
+                if bi[4] != 24 or bi[5] != 0:
+                    raise ValueError(f"only uncompressed 24-bit BGR AVI is readable without OpenCV "
+                                     f"(bitcount {bi[4]}, compression {bi[5]})")
+                self.w, self.h = bi[1], bi[2]
+                self._bottom_up = self.h > 0
+                self.h = abs(self.h)
+                self.row = (self.w * 3 + 3) & ~3
+            elif ck[2:] in (b"db", b"dc") and ln > 0:
+                self._offsets.append((body, ln))
+            pos = body + ln + (ln & 1)
+
+    def isOpened(self) -> bool:  # noqa: N802
+        return self._open
+
+    def read(self):
+        if not self._open or self._i >= len(self._offsets):
+            return False, None
+        off, ln = self._offsets[self._i]
+        self._i += 1
+        if ln < self.row * self.h:
+            return False, None
+        rows = np.asarray(self._mm[off: off + self.row * self.h]).reshape(self.h, self.row)[:, : self.w * 3]
+        if self._bottom_up:
+            rows = rows[::-1]
+        return True, np.ascontiguousarray(rows).reshape(self.h, self.w, 3)
+
+    def get(self, prop: int) -> float:
+        return {CAP_PROP_FRAME_COUNT: float(len(self._offsets)), CAP_PROP_FRAME_WIDTH: float(self.w),
+                CAP_PROP_FRAME_HEIGHT: float(self.h), CAP_PROP_FPS: self.fps}.get(prop, 0.0)
+
+    def release(self) -> None:
+        self._open = False
+        self._mm = None
+
+
+def open_capture(source):
+    """cv2.VideoCapture(source) when OpenCV exists (fm.py:413); otherwise the readers above.
+
+    `source` may also be an object that already speaks the capture protocol,
+    a uint8 array [N][H][W][3], or "synthetic:WxH:N[:stream]".
+    """
+    if hasattr(source, "read") and hasattr(source, "isOpened"):
+        return source
+    if isinstance(source, np.ndarray):
+        return ArrayCapture(source)
+    if isinstance(source, str) and source.startswith("synthetic:"):
+        parts = source.split(":")
+        w, h = (int(v) for v in parts[1].lower().split("x"))
+        return SyntheticCapture(w, h, int(parts[2]), int(parts[3]) if len(parts) > 3 else 0)
+    if isinstance(source, str) and source.endswith(".npy"):
+        return ArrayCapture(np.load(source, mmap_mode="r", allow_pickle=False))
+    if cv2 is not None:
+        return cv2.VideoCapture(source)
+    if isinstance(source, int):
+        raise OSError(f"camera {source}: camera capture needs OpenCV, which is not installed")
+    return RawAviCapture(str(source))
+
+
+def open_writer(path: str, codec: str, fps: float, size):
+    """cv2.VideoWriter(path, fourcc(codec), fps, size) (fm.py:468-470), else an uncompressed AVI."""
+    if cv2 is not None:
+        return cv2.VideoWriter(path, cv2.VideoWriter_fourcc(*codec), fps, size)
+    if codec not in ("DIB ", "RGB ", "raw ", None):
+        log.debug("OpenCV absent: writing %s as uncompressed AVI instead of codec %s", path, codec)
+    return RawAviWriter(path, fps, size)

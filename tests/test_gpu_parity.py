@@ -139,3 +139,92 @@ def test_heavy_tiles_stripes_and_rings():
     checker[::7, ::7] = True
     frames = _pattern_frames([stripes, rings, checker])
     run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
+
+
+# --- committed golden fixtures through the C ABI -------------------------------
+
+from golden_cases import boxes_of, chain_files, contour_cases, load_chain, origins_of  # noqa: E402
+
+
+@pytest.mark.parametrize("path", chain_files(), ids=lambda p: p.rsplit("/", 1)[-1])
+@pytest.mark.parametrize("batch", [1, 0])  # 1 frame per submit, or the whole sequence in one launch
+def test_golden_chain_fixture(path, batch):
+    c = load_chain(path)
+    T = c["T"] if batch == 0 else batch
+    eng = MotionEngine(n_streams=1, src_w=c["W"], src_h=c["H"], box_size=c["box"], ksize=c["ksize"],
+                       threshold=c["thresh"], avg=c["alpha"], max_batch=T, keep_planes=True)
+    if c["has_keep"]:
+        eng.set_mask(0, c["keep"])
+    for t0 in range(0, c["T"], T):
+        fr = c["frames"][t0:t0 + T]
+        eng.submit(fr[:, None])
+        eng.wait()
+        counts = eng.counts()
+        for i in range(fr.shape[0]):
+            t = t0 + i
+            for plane, name in ((PLANE_GRAY, "gray"), (PLANE_BLUR, "blur"), (PLANE_DELTA, "delta")):
+                np.testing.assert_array_equal(eng.plane(plane, i, 0), c[name][t], err_msg=f"{name} frame {t}")
+            np.testing.assert_array_equal(eng.mask(i, 0), c["mask"][t], err_msg=f"mask frame {t}")
+            assert counts[i, 0] == c["count"][t]
+            assert [x.bbox for x in eng.contours(i, 0)] == boxes_of(c, t)
+            assert [x.origin for x in eng.contours(i, 0)] == origins_of(c, t)
+    np.testing.assert_array_equal(eng.background(0), c["bg"])
+    eng.close()
+
+
+@pytest.mark.parametrize("name", sorted(contour_cases()))
+def test_golden_contour_fixture(name):
+    """The fixture pattern enters as frame 1 after a black frame 0 (ksize 1, threshold 0), so the
+    threshold mask is the pattern and the kernel dilates it; the GPU's contours of the dilated pattern
+    are compared with the oracle's."""
+    case = contour_cases()[name]
+    m = case["mask"]
+    H, W = m.shape
+    fr = np.zeros((2, 1, H, W, 3), np.uint8)
+    fr[1, 0] = m[..., None]
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.5, max_batch=2)
+    eng.submit(fr)
+    eng.wait()
+    d = oracle.dilate5(m)
+    np.testing.assert_array_equal(eng.mask(1, 0), d)
+    want = oracle.find_contours_ext(d)
+    assert eng.counts()[1, 0] == len(want)
+    assert [c.bbox for c in eng.contours(1, 0)] == [c["bbox"] for c in want]
+    eng.close()
+
+
+# --- the drop-in VideoMotion on the real engine ---------------------------------
+
+@pytest.mark.parametrize("batch", [1, 8])
+def test_video_motion_dropin_decisions(tmp_path, batch):
+    from find_motion_amd import motion, videoio
+    from oracle.decision import written_indices
+
+    W, H, n = 480, 270, 48
+    vm = motion.VideoMotion(filename=str(tmp_path / "v"), capture=videoio.SyntheticCapture(W, H, n, 0),
+                            box_size=100, threshold=12, cache_time=0.3, min_time=0.1, batch=batch,
+                            outdir=str(tmp_path))
+    vm.find_motion()
+    cfg = oracle.OracleConfig(H=H, W=W, box=100, ksize=5)
+    st = oracle.OracleStream(cfg)
+    vid = videoio.SyntheticCapture(W, H, n, 0).video
+    counts = [st.step(vid.frame(i))["count"] for i in range(n)]
+    assert vm.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3)
+    assert vm.written_indices
+
+
+def test_stream_group_on_gpu(tmp_path):
+    from find_motion_amd import motion, videoio
+    from oracle.decision import written_indices
+
+    W, H, n, S = 320, 180, 24, 4
+    caps = [videoio.SyntheticCapture(W, H, n, s) for s in range(S)]
+    grp = motion.StreamGroup([str(tmp_path / f"s{s}") for s in range(S)], batch=6, captures=caps, box_size=320,
+                             blur_scale=64, threshold=12, cache_time=0.3, min_time=0.1, outdir=str(tmp_path))
+    grp.find_motion()
+    cfg = oracle.OracleConfig(H=H, W=W, box=320, ksize=5)
+    for s, v in enumerate(grp.videos):
+        st = oracle.OracleStream(cfg)
+        vid = videoio.SyntheticCapture(W, H, n, s).video
+        counts = [st.step(vid.frame(i))["count"] for i in range(n)]
+        assert v.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3), s
