@@ -38,9 +38,9 @@ def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
     S, T = cfg["streams_per_gpu"], cfg["frames_per_step"]
     H, W, h, w = cfg["H"], cfg["W"], cfg["h"], cfg["w"]
     if kernel == "fused":
-        # one launch = T frames of every stream: per frame BGR read 3 B + dilated mask write 1 B +
-        # mask bit rows 1/8 B; per batch the f64 background read + write 16 B (kept in registers)
-        return S * T * h * w * (3 + 1 + 0.125) + S * h * w * 16
+        # one launch = T frames of every stream: per frame BGR read 3 B + dilated mask write 1 B;
+        # per batch the f64 background read + write 16 B (held in registers across the batch)
+        return S * T * h * w * (3 + 1) + S * h * w * 16
     if kernel == "pixel":
         # one launch = one frame of every stream: BGR read 3 B + mask write 1 B + f64 background r/w 16 B
         return S * h * w * (3 + 1 + 16)
