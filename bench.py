@@ -37,7 +37,7 @@ def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
     """Algorithmic HBM bytes of ONE launch of `kernel` (DESIGN.md 'Kernels')."""
     S, T = cfg["streams_per_gpu"], cfg["frames_per_step"]
     H, W, h, w = cfg["H"], cfg["W"], cfg["h"], cfg["w"]
-    if kernel == "fused":
+    if kernel in ("fused", "pix"):
         # one launch = T frames of every stream: per frame BGR read 3 B + dilated mask write 1 B;
         # per batch the f64 background read + write 16 B (held in registers across the batch)
         return S * T * h * w * (3 + 1) + S * h * w * 16

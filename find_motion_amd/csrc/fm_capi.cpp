@@ -61,10 +61,12 @@ struct fm_ctx {
     int32_t* d_rec_dev = nullptr;   // device-resident records for the pixel-level CCL (uses atomics)
     // tile-summary CCL (fused path)
     bool use_fused = false;
+    bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;
     TileRec* d_tiles = nullptr;
     int32_t* d_heavy = nullptr;
-    uint64_t* d_bits = nullptr;
+    uint64_t* d_bits = nullptr;    // threshold bit rows (k_pix output)
+    uint64_t* d_dbits = nullptr;   // dilated bit rows = VideoFrame.thresh
     NodeRec* d_nodes = nullptr;
     int32_t* h_overflow = nullptr;  // pinned [T*S]
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
@@ -322,8 +324,13 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &c->d_work, px * 3))) return rc;
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
+    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024;
+    c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
+                 std::getenv("FM_NO_PIX") == nullptr;
+    // dilated masks stay as bit rows on the fused paths; d_mask is one plane there
+    // (fm_read_mask expansion target, pixel-CCL fallback input)
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
-        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, px)) ||
+        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, c->use_fused ? c->work_plane : px)) ||
         (rc = dalloc(cp, &c->d_count, 2 * frames + 1)))
         return rc;
     // contour records: mapped pinned host memory written directly by the
@@ -331,13 +338,15 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     // capacity-sized buffer)
     HIP_TRY(cp, hipHostMalloc((void**)&c->h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
     HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
-    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024;
     if (c->use_fused) {
         c->ntx = (c->w + 63) / 64;
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
         c->nnodes = c->ntiles * kTileMaxRuns;
-        if ((rc = dalloc(cp, &c->d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64)) || (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
+        if ((rc = dalloc(cp, &c->d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) ||
+            (rc = dalloc(cp, &c->d_dbits, frames * c->ntiles * 64)) ||
+            (c->use_pix && (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64))) ||
+            (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
             return rc;
     }
     // pixel-level CCL buffers: the whole batch on the v1 path, one frame for the
@@ -380,7 +389,7 @@ void fm_destroy(fm_ctx* c) {
     dfree(c->d_in); dfree(c->d_work); dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep);
     dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask); dfree(c->d_planes); dfree(c->d_label);
     dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec_dev); c->d_rec = nullptr;
-    dfree(c->d_tiles); dfree(c->d_heavy); dfree(c->d_bits); dfree(c->d_nodes);
+    dfree(c->d_tiles); dfree(c->d_heavy); dfree(c->d_bits); dfree(c->d_dbits); dfree(c->d_nodes);
     if (c->h_overflow) (void)hipHostFree(c->h_overflow);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     if (c->h_init) (void)hipHostFree(c->h_init);
@@ -477,9 +486,10 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.keep = c->d_keep;
         fa.has_keep = c->d_has_keep;
         fa.init = any_init ? c->d_init : nullptr;
-        fa.mask_out = c->d_mask;
+        fa.mask_out = nullptr;
         fa.planes = c->d_planes;
         fa.bits = c->d_bits;
+        fa.dbits = c->d_dbits;
         fa.tiles = c->d_tiles;
         fa.nodes = c->d_nodes;
         fa.count = c->d_count;
@@ -502,8 +512,36 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.acc_vec_end = npx - npx % 16;
         fa.dbg_skip = c->dbg_skip;
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
-        HIP_TRY(c, launch_fused(c->stream, fa, &c->timer));
-        c->bg_cur ^= 1;
+        fa.t_begin = 0;
+        fa.t_end = n;
+        if (c->use_pix) {
+            const bool planes = c->d_planes != nullptr;
+            // each launch reads d_bg[cur] and writes d_bg[cur ^ 1]
+            auto run = [&](int t0, int t1, bool init, const char* name) -> int {
+                FusedArgs fp = fa;
+                fp.t_begin = t0;
+                fp.t_end = t1;
+                fp.bg_in = c->d_bg[c->bg_cur];
+                fp.bg_out = c->d_bg[c->bg_cur ^ 1];
+                if (!init) fp.init = nullptr;
+                int tok = c->timer.begin(name);
+                HIP_TRY(c, launch_pix(c->stream, fp, planes, init));
+                c->timer.end(tok);
+                c->bg_cur ^= 1;
+                return FM_OK;
+            };
+            int rc;
+            if (any_init) {  // first frames in their own launch: the steady-state kernel has no init select
+                if ((rc = run(0, 1, true, "pix_init"))) return rc;
+                if (n > 1 && (rc = run(1, n, false, "pix"))) return rc;
+            } else if ((rc = run(0, n, false, "pix"))) {
+                return rc;
+            }
+        } else {
+            HIP_TRY(c, launch_fused(c->stream, fa, &c->timer));
+            c->bg_cur ^= 1;
+        }
+        HIP_TRY(c, launch_tile_ccl(c->stream, fa, c->use_pix, &c->timer));
         HIP_TRY(c, hipMemcpyAsync(c->h_overflow, c->d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     } else {
     PixelArgs a{};
@@ -570,7 +608,8 @@ int fm_wait(fm_ctx* c) {
             const size_t cap = c->p.max_contours;
             HIP_TRY(c, hipMemsetAsync(c->d_count + f, 0, sizeof(int32_t), c->stream));
             HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, c->stream));
-            CclArgs ca{c->d_mask + f * c->work_plane, c->d_label, c->d_outer, c->d_cid, c->d_count + f,
+            HIP_TRY(c, launch_expand_bits(c->stream, c->d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+            CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count + f,
                        c->d_rec_dev, 1, c->h, c->w, c->p.max_contours};
             HIP_TRY(c, launch_ccl(c->stream, ca, nullptr));
             HIP_TRY(c, hipMemcpyAsync(c->h_rec + f * cap * 5, c->d_rec_dev, cap * 5 * sizeof(int32_t),
@@ -629,7 +668,12 @@ int fm_read_mask(fm_ctx* c, int frame, int stream, uint8_t* out) {
     if (int rc = check_frame(c, frame, stream)) return rc;
     HIP_TRY(c, hipSetDevice(c->p.device));
     const size_t f = (size_t)frame * c->p.n_streams + stream;
-    HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+    if (c->use_fused) {
+        HIP_TRY(c, launch_expand_bits(c->stream, c->d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return FM_OK;
 }

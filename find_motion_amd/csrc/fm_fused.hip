@@ -514,25 +514,9 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
             if (vc < 64) o &= (1ull << vc) - 1;
             if (y0 + ln >= h) o = 0;
             Ob[ln] = o;
-            a.bits[(f * a.ntiles + ti) * 64 + ln] = o;
+            a.dbits[(f * a.ntiles + ti) * 64 + ln] = o;
         }
         lds_barrier();
-
-        // ---- mask bytes out: 8 px per thread
-        if (!(dbg & 8)) {
-            const int row = tid >> 3, oc = tid & 7;
-            const int y = y0 + row, xs = x0 + 8 * oc;
-            if (y < h && xs < w) {
-                const uint32_t b = (uint32_t)(Ob[row] >> (8 * oc)) & 0xFFu;
-                uint8_t* dst = a.mask_out + f * plane + (size_t)y * w + xs;
-                const uint2 v = make_uint2(nib2bytes(b & 15), nib2bytes(b >> 4));
-                if (xs + 8 <= w && (((uintptr_t)dst) & 7) == 0) {
-                    *reinterpret_cast<uint2*>(dst) = v;
-                } else {
-                    for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = (uint8_t)((((i < 4 ? v.x : v.y) >> (8 * (i & 3))) & 0xFF));
-                }
-            }
-        }
 
     }
 
@@ -565,7 +549,7 @@ struct CclScratch {
 
 // returns false (nothing written) if the tile has more than CAP runs
 template <int CAP>
-__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, const CclScratch& sc) {
+__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const CclScratch& sc) {
     int* par = sc.par;
     int* amin = sc.amin;
     int* amax = sc.amax;
@@ -579,7 +563,6 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, const Ccl
     const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
     TileRec* TR = a.tiles + f * a.ntiles + ti;
     NodeRec* NR = a.nodes + f * (size_t)a.nnodes + (size_t)ti * MAXR;
-    const uint64_t m = a.bits[(f * a.ntiles + ti) * 64 + ln];
 
     if (__ballot(m != 0) == 0) {  // empty tile: one background component (run 0)
         TR->edges[ln] = 0;
@@ -715,21 +698,66 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, const Ccl
 constexpr int LIGHT_RUNS = 256;   // most tiles: empty or a few blobs
 constexpr int CCL_WAVES = 4;
 
+// 5x5 dilation (dilate(thresh, None, iterations=2), fm.py:266) of one tile's
+// threshold bit rows, lane = row: the 68-bit row (2 columns of each side
+// neighbour) is ORed over 5 shifts, then over 5 rows through LDS (2 halo rows
+// from the tiles above and below).  Out-of-image pixels are 0 in the input and
+// cleared in the output.
+__device__ __forceinline__ uint64_t hdil(uint64_t L, uint64_t C, uint64_t R) {
+    const uint64_t lo = (L >> 62) | (C << 2), hi = (C >> 62) | ((R & 3) << 2);
+    return lo | ((lo >> 1) | (hi << 63)) | ((lo >> 2) | (hi << 62)) | ((lo >> 3) | (hi << 61)) | ((lo >> 4) | (hi << 60));
+}
+
+__device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, int ti, int ln, uint64_t* hv) {
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const uint64_t* B = a.bits + f * (size_t)a.ntiles * 64;
+    auto row = [&](int t, int r) -> uint64_t { return B[(size_t)t * 64 + r]; };
+    const bool hl = tx > 0, hr = tx + 1 < a.ntx;
+    hv[ln + 2] = hdil(hl ? row(ti - 1, ln) : 0, row(ti, ln), hr ? row(ti + 1, ln) : 0);
+    if (ln < 4) {  // halo rows -2, -1 (tile above, rows 62, 63) and 64, 65 (tile below, rows 0, 1)
+        const int dy = ln < 2 ? -1 : 1;
+        const int rr = ln < 2 ? 62 + ln : ln - 2;
+        const int tyy = ty + dy;
+        uint64_t v = 0;
+        if (tyy >= 0 && tyy < a.nty) {
+            const int tt = tyy * a.ntx + tx;
+            v = hdil(hl ? row(tt - 1, rr) : 0, row(tt, rr), hr ? row(tt + 1, rr) : 0);
+        }
+        hv[ln < 2 ? ln : 64 + ln] = v;
+    }
+    lds_fence();
+    uint64_t o = hv[ln] | hv[ln + 1] | hv[ln + 2] | hv[ln + 3] | hv[ln + 4];
+    const int x0 = tx * TS, y0 = ty * TS;
+    const int vc = a.w - x0;
+    if (vc < 64) o &= (1ull << vc) - 1;
+    if (y0 + ln >= a.h) o = 0;
+    return o;
+}
+
 // light pass: one wave per tile, 4 tiles per workgroup, small LDS; tiles with
 // more runs are appended to a work list for the heavy pass
+template <bool DILATE>
 __global__ __launch_bounds__(64 * CCL_WAVES) void k_tile_ccl(FusedArgs a) {
     __shared__ int par[CCL_WAVES][LIGHT_RUNS], amin[CCL_WAVES][LIGHT_RUNS], amax[CCL_WAVES][LIGHT_RUNS],
         ay[CCL_WAVES][LIGHT_RUNS];
     __shared__ uint8_t rx0[CCL_WAVES][LIGHT_RUNS], rx1[CCL_WAVES][LIGHT_RUNS], rf[CCL_WAVES][LIGHT_RUNS];
     __shared__ int rb[CCL_WAVES][66];
+    __shared__ uint64_t hv[CCL_WAVES][68];
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const long long item = (long long)blockIdx.x * CCL_WAVES + wv;
     const long long nitems = (long long)a.T * a.S * a.ntiles;
     if (item >= nitems) return;
     const size_t f = item / a.ntiles;
     const int ti = (int)(item - (long long)f * a.ntiles);
+    uint64_t m;
+    if (DILATE) {
+        m = dilate_tile(a, f, ti, ln, hv[wv]);
+        a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
+    } else {
+        m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
+    }
     CclScratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv]};
-    if (!tile_ccl<LIGHT_RUNS>(a, f, ti, ln, sc) && ln == 0) {
+    if (!tile_ccl<LIGHT_RUNS>(a, f, ti, ln, m, sc) && ln == 0) {
         const size_t F = (size_t)a.T * a.S;
         const int slot = atomicAdd(&a.count[2 * F], 1);
         a.heavy[slot] = (int)item;
@@ -747,7 +775,8 @@ __global__ __launch_bounds__(64) void k_tile_ccl_heavy(FusedArgs a) {
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         const size_t f = item / a.ntiles;
-        tile_ccl<MAXR>(a, f, (int)(item - (long long)f * a.ntiles), threadIdx.x, sc);
+        const int ti = (int)(item - (long long)f * a.ntiles);
+        tile_ccl<MAXR>(a, f, ti, threadIdx.x, a.dbits[(f * a.ntiles + ti) * 64 + threadIdx.x], sc);
     }
 }
 
@@ -888,13 +917,17 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
         hipLaunchKernelGGL(fz::k_fused<0>, grid, dim3(fz::NT), bytes, st, a);
     }
     if (tm) tm->end(tok);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
+    hipError_t e;
     dim3 gm(a.ntiles, a.T * a.S);
-    tok = tm ? tm->begin("tile_ccl") : -1;
+    int tok = tm ? tm->begin("tile_ccl") : -1;
     const long long items = (long long)a.T * a.S * a.ntiles;
-    hipLaunchKernelGGL(fz::k_tile_ccl, dim3((unsigned)((items + fz::CCL_WAVES - 1) / fz::CCL_WAVES)),
-                       dim3(64 * fz::CCL_WAVES), 0, st, a);
+    const dim3 gl((unsigned)((items + fz::CCL_WAVES - 1) / fz::CCL_WAVES));
+    if (dilate) hipLaunchKernelGGL(fz::k_tile_ccl<true>, gl, dim3(64 * fz::CCL_WAVES), 0, st, a);
+    else hipLaunchKernelGGL(fz::k_tile_ccl<false>, gl, dim3(64 * fz::CCL_WAVES), 0, st, a);
     hipLaunchKernelGGL(fz::k_tile_ccl_heavy, dim3(512), dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -909,6 +942,26 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
     tok = tm ? tm->begin("tile_resolve2") : -1;
     hipLaunchKernelGGL(fz::k_tile_resolve2, gm, dim3(64), 0, st, a);
     if (tm) tm->end(tok);
+    return hipGetLastError();
+}
+
+// one thread per 8 mask bytes of one frame
+__global__ __launch_bounds__(256) void k_expand_bits(const uint64_t* __restrict__ dbits, uint8_t* __restrict__ out, int h,
+                                                     int w, int ntx) {
+    const int x8 = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    const int xs = 8 * x8;
+    if (xs >= w) return;
+    const int tx = xs >> 6, ty = y >> 6;
+    const uint64_t row = dbits[((size_t)ty * ntx + tx) * 64 + (y & 63)];
+    const uint32_t b = (uint32_t)(row >> (xs & 63)) & 0xFFu;
+    uint8_t* dst = out + (size_t)y * w + xs;
+    for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = ((b >> i) & 1) ? 255 : 0;
+}
+
+hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, uint8_t* out, int h, int w, int ntx, int) {
+    dim3 grid((unsigned)(((w + 7) / 8 + 255) / 256), (unsigned)h);
+    hipLaunchKernelGGL(k_expand_bits, grid, dim3(256), 0, st, dbits, out, h, w, ntx);
     return hipGetLastError();
 }
 

@@ -78,13 +78,16 @@ struct FusedArgs {
     const uint8_t* init;         // [S] or nullptr: 1 => bg := blur at the batch's first frame
     uint8_t* mask_out;           // [T][S][h*w] dilated threshold
     uint8_t* planes;             // optional [3][T][S][h*w] gray, blur, frame_delta
-    uint64_t* bits;              // [F][ntiles][64] dilated tile rows as bit masks (input of k_tile_ccl)
+    uint64_t* bits;              // [F][ntiles][64] threshold rows as bit masks (k_pix output, k_dilate_ccl input)
+    uint64_t* dbits;             // [F][ntiles][64] dilated rows (VideoFrame.thresh as bits; == bits when the
+                                 // pixel kernel dilates itself, i.e. the generic-k k_fused path)
     TileRec* tiles;              // [F][ntiles]
     NodeRec* nodes;              // [F][nnodes]
     int32_t* count;              // [2F+1]: [f] external contours, [F+f] overflow flag, [2F] heavy-tile count
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
     int32_t* rec;                // [F][cap][5]
     int T, S, h, w, ksize, thresh;
+    int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     double alpha, beta;
@@ -105,6 +108,15 @@ hipError_t launch_ccl(hipStream_t st, const CclArgs& a, KernelTimer* timer);
 hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* timer);
 int fused_lds_bytes(int ksize);
 int fused_max_ksize();
+// k_pix (fm_pix.hip): chain once per pixel, threshold bits out; dilation in the CCL kernel
+// frames [a.t_begin, a.t_end) of the batch; init: a.init may mark first frames (only at t_begin)
+hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init);
+int pix_lds_bytes(int ksize);
+bool pix_supported(int ksize);
+// CCL over tile summaries; dilate = true: a.bits are threshold rows to dilate into a.dbits
+hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer);
+// dilated bit rows of one frame -> mask bytes (VideoFrame.thresh) [h][w]
+hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, uint8_t* out, int h, int w, int ntx, int ntiles);
 
 // Optional per-kernel event timing (FM_FLAG_PROFILE): events are recorded on
 // the launch stream around each kernel and read back after the stream syncs.

@@ -1,0 +1,506 @@
+// fm_pix.hip — the per-pixel motion chain, temporally blocked (gfx950).
+//
+// One workgroup (512 threads = 8 waves) owns a 64x64 tile of one stream for
+// all T frames of a batch and computes, per frame (reference = fm.py):
+//
+//   gray    cvtColor(BGR2GRAY)                     fm.py:493   4 px/lane, v_perm + v_dot2
+//   blur    GaussianBlur(k,k), fixed point,        fm.py:494   horizontal: v_dot4 over byte
+//           REFLECT_101                                        windows; vertical: v_dot2 over
+//                                                              transposed u16 pairs in LDS
+//   mask    keep-mask (mask_off_areas)             fm.py:619-636
+//   diff    absdiff(blur, convertScaleAbs(bg))     fm.py:250
+//   thresh  delta > t                              fm.py:257   -> one bit per pixel (ballot)
+//   accum   accumulateWeighted(blur, bg, a), f64   fm.py:659   bg lives in registers
+//
+// Every pixel's chain runs exactly once: the 5x5 dilation (fm.py:266) is NOT
+// done here but on the threshold bit rows by k_dilate_ccl, which needs the
+// 2-px halo of neighbouring tiles' bits, not their chains.  Outputs per
+// frame: 64 threshold bit rows per tile (1/8 B per pixel), plus gray / blur /
+// frame_delta planes when the caller keeps them (show / debug).
+//
+// HBM per launch (T frames, S streams): BGR 3 B/px/frame read once (the
+// 2..12-px gray halo re-read comes from L2/MALL: tiles are swizzled so that
+// horizontally adjacent tiles run on the same XCD), f64 background 16 B/px
+// per batch, bits 1/8 B/px/frame.
+#include "fm_internal.h"
+
+namespace fm {
+namespace px {
+
+constexpr int TS = 64;          // tile edge
+constexpr int NT = 512;         // threads
+constexpr int NW = NT / 64;     // waves; wave w owns tile rows [8w, 8w + 8)
+constexpr int RPWV = TS / NW;   // rows per wave in the chain stage
+
+__host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
+
+// Geometry of the gray (G) region for blur radius r: rows y0-r .. y0+63+r,
+// columns x0-PC .. x0+63+PC with PC = 4*ceil(r/4) (quad aligned)
+struct Geo {
+    int r, PC, GW, NQ, GH, RS, CPR, nchunks, RSH;
+    int o_raw, o_H, o_rowy, o_colx, o_roff, bytes;
+    int raw_bytes, H_bytes, roff_bytes;  // per buffer; raw, H and roff are double buffered
+    __host__ __device__ explicit Geo(int rr) {
+        r = rr;
+        PC = 4 * ((r + 3) / 4);
+        GW = TS + 2 * PC;
+        NQ = GW / 4;
+        GH = TS + 2 * r;
+        RS = a16(3 * GW + 15);  // aligned-down row start (<= 15 B early) + 3 B per gray column
+        CPR = RS / 16;
+        nchunks = GH * CPR;
+        RSH = (GH + 3) & ~3;  // transposed H row (u16 per G row), 8-B aligned
+        raw_bytes = GH * RS;
+        H_bytes = a16(TS * RSH * 2);
+        roff_bytes = a16(GH * 4);
+        o_raw = 0;
+        o_H = o_raw + 2 * raw_bytes;
+        o_rowy = o_H + 2 * H_bytes;
+        o_colx = o_rowy + a16(GH * 4);
+        o_roff = o_colx + a16(GW * 4);
+        bytes = o_roff + 2 * roff_bytes;
+    }
+};
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = (p < 0) ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+// LDS-only barrier: the next frame's raw prefetch (global loads) stays in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+// BGR2GRAY of 4 consecutive pixels packed in 3 dwords (B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3)
+__device__ __forceinline__ uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
+    const u16x2_t cbg = __builtin_bit_cast(u16x2_t, 1868u | (9617u << 16));
+    const uint32_t p0 = __builtin_amdgcn_perm(d0, d0, 0x0C010C00u);
+    const uint32_t p1 = __builtin_amdgcn_perm(d1, d0, 0x0C040C03u);
+    const uint32_t p2 = __builtin_amdgcn_perm(d1, d1, 0x0C030C02u);
+    const uint32_t p3 = __builtin_amdgcn_perm(d2, d2, 0x0C020C01u);
+    const uint32_t g0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p0), cbg, __umul24((d0 >> 16) & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p1), cbg, __umul24((d1 >> 8) & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g2 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p2), cbg, __umul24(d2 & 0xFF, 4899u) + 8192u, false) >> 14;
+    const uint32_t g3 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p3), cbg, __umul24(d2 >> 24, 4899u) + 8192u, false) >> 14;
+    return g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);
+}
+
+__device__ __forceinline__ uint32_t gray1(const uint8_t* p) {
+    return ((uint32_t)p[0] * 1868u + (uint32_t)p[1] * 9617u + (uint32_t)p[2] * 4899u + 8192u) >> 14;
+}
+
+// window of 4 bytes starting at byte p of the little-endian concatenation q[0], q[1], ...
+template <int P, int N>
+__device__ __forceinline__ uint32_t win4(const uint32_t (&q)[N]) {
+    if constexpr ((P & 3) == 0) return q[P >> 2];
+    else return __builtin_amdgcn_alignbyte(q[(P >> 2) + 1], q[P >> 2], P & 3);
+}
+
+// horizontal taps of output I of a quad: sum_t c[t] * g[I + OFF + t]; NG dot4 groups
+template <int I, int OFF, int NG, int G, int N>
+__device__ __forceinline__ uint32_t htap(const uint32_t (&q)[N], const uint32_t (&cpk)[NG], uint32_t acc) {
+    if constexpr (G == NG) return acc;
+    else return htap<I, OFF, NG, G + 1, N>(q, cpk, __builtin_amdgcn_udot4(win4<I + OFF + 4 * G, N>(q), cpk[G], acc, false));
+}
+
+// 16-B raw chunks of the G region of one frame: chunk c -> row c / CPR, 16 B at
+// the row's aligned start + 16 * (c % CPR); chunks past the row's last byte are skipped
+template <int NCH>
+struct Raw {
+    uint4 v[NCH];
+};
+
+__device__ __attribute__((noinline)) uint4 load_partial(const uint8_t* ca, const uint8_t* fb, const uint8_t* fe) {
+    uint32_t wds[4] = {0, 0, 0, 0};
+    for (int b = 0; b < 16; b++)
+        if (ca + b >= fb && ca + b < fe) wds[b >> 2] |= (uint32_t)ca[b] << (8 * (b & 3));
+    return make_uint4(wds[0], wds[1], wds[2], wds[3]);
+}
+
+// Per-thread chunk plan, frame invariant: chunk i of this thread starts at byte
+// rel0[i] - mis of its frame, where rel0 = (row offset + 3*cx0) + 16*k and
+// mis = (frame address + rel0) & 15 aligns the row start down to 16 B.
+template <int NCH>
+struct ChunkPlan {
+    uint32_t rel0[NCH];
+    uint32_t k16[NCH];  // 16*k, or 0xFFFF for a slot past the last chunk
+};
+
+template <int NCH>
+__device__ __forceinline__ void plan_chunks(ChunkPlan<NCH>& P, const int* rowy, const Geo& g, int cx0, int w, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const int c = tid + NT * i;
+        const int gy = c / g.CPR, k = c - gy * g.CPR;
+        const bool live = c < g.nchunks;
+        P.rel0[i] = live ? (uint32_t)(rowy[gy] * w + cx0) * 3u + 16u * k : 0u;
+        P.k16[i] = live ? 16u * k : 0xFFFFu;
+    }
+}
+
+template <int NCH>
+__device__ __forceinline__ void load_raw(Raw<NCH>& R, const uint8_t* fsrc, uint32_t fbytes, const ChunkPlan<NCH>& P,
+                                         uint32_t span) {
+    const uint32_t flo = (uint32_t)(uintptr_t)fsrc;
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const uint32_t mis = (flo + P.rel0[i]) & 15u;
+        const int rel = (int)P.rel0[i] - (int)mis;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (P.k16[i] < span + mis) {  // chunk starts before the row segment's last byte
+            if (__builtin_expect(rel >= 0 && (uint32_t)rel + 16u <= fbytes, 1))
+                val = *reinterpret_cast<const uint4*>(fsrc + rel);
+            else
+                val = load_partial(fsrc + rel, fsrc, fsrc + fbytes);
+        }
+        R.v[i] = val;
+    }
+}
+
+template <int NCH>
+__device__ __forceinline__ void store_raw(const Raw<NCH>& R, uint8_t* raw, const Geo& g, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const int c = tid + NT * i;
+        if (c < g.nchunks) {
+            const int gy = c / g.CPR, k = c - gy * g.CPR;
+            *reinterpret_cast<uint4*>(raw + gy * g.RS + 16 * k) = R.v[i];
+        }
+    }
+}
+
+// XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8
+// XCDs, so block b runs on XCD b % 8; give each XCD a contiguous run of tiles
+// (row-major), so left/right neighbours share that XCD's L2 for the halo.
+__device__ __forceinline__ int swizzle_tile(int b, int n) {
+    const int full = n & ~7;
+    if (b >= full) return b;
+    return (b & 7) * (full >> 3) + (b >> 3);
+}
+
+// OpenCV's 8-bit fixed-point Gaussian taps (getGaussianKernelBitExact +
+// error-diffusion rounding, restated in fm_capi.cpp gaussian_taps); fixed at
+// compile time so they are instruction literals.  launch_pix checks them
+// against the context's taps.
+template <int K> struct Taps;
+template <> struct Taps<3> { static constexpr int c[3] = {64, 128, 64}; };
+template <> struct Taps<5> { static constexpr int c[5] = {16, 64, 96, 64, 16}; };
+template <> struct Taps<7> { static constexpr int c[7] = {8, 28, 56, 72, 56, 28, 8}; };
+template <> struct Taps<21> {
+    static constexpr int c[21] = {0, 2, 2, 4, 6, 11, 15, 20, 25, 28, 30, 28, 25, 20, 15, 11, 6, 4, 2, 2, 0};
+};
+template <int K> constexpr uint32_t tap4(int g) {
+    uint32_t v = 0;
+    for (int b = 0; b < 4; b++)
+        if (4 * g + b < K) v |= (uint32_t)Taps<K>::c[4 * g + b] << (8 * b);
+    return v;
+}
+template <int K> constexpr uint32_t tap2(int t) {
+    return (uint32_t)Taps<K>::c[2 * t] | (2 * t + 1 < K ? (uint32_t)Taps<K>::c[2 * t + 1] << 16 : 0u);
+}
+
+// Per-frame, per-wave constants of the chain stage (computed once per tile).
+struct ChainCtx {
+    uint64_t colmask;   // lanes whose column is inside the image
+    uint32_t rowvalid;  // bit j: tile row 8*wv + j is inside the image
+    uint32_t keep_lo, keep_hi;  // keep-mask bytes of the wave's 8 rows for this lane's column (1 = keep)
+    bool hk;            // stream has a keep-mask
+    uint32_t vec;       // every pixel of the wave's rows lies in accumulateWeighted's vector body
+};
+
+// One frame's vertical taps + per-pixel chain for the wave's 8 rows.
+// INIT: the launch may hold a stream's first frame (bg := blur before the diff,
+// fm.py:651-652); `init` says whether this frame is one.
+template <int KC, bool PLANES, bool INIT>
+__device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const Geo& g, double (&bg)[RPWV],
+                                           int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
+                                           bool init, uint64_t& mybits) {
+    constexpr int R = KC >> 1;
+    constexpr int NV = RPWV + 2 * R;       // H rows feeding the wave's 8 outputs
+    constexpr int NP = (NV + 1) / 2;       // u16 pairs
+    const int w = a.w;
+    // transposed H: column ln, rows 8*wv .. 8*wv + NV - 1, read as pairs
+    uint32_t P[NP + 1];
+    {
+        const uint32_t* col = reinterpret_cast<const uint32_t*>(Hs + ln * g.RSH + RPWV * wv);
+#pragma unroll
+        for (int i = 0; i < NP; i += 2) {
+            if (i + 1 < NP) {
+                const uint2 v = *reinterpret_cast<const uint2*>(col + i);
+                P[i] = v.x;
+                P[i + 1] = v.y;
+            } else {
+                P[i] = col[i];
+            }
+        }
+        P[NP] = 0;
+    }
+    const double alpha = a.alpha, beta = a.beta;
+    const int thresh = a.thresh;
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) {
+        // acc = sum_t c[t] * H[j + t] + 2^15 over u16 pairs (H[e], H[e+1])
+        uint32_t acc = 32768u;
+#pragma unroll
+        for (int t = 0; t < (KC + 1) / 2; t++) {
+            const int e = j + 2 * t;
+            const uint32_t pr = (e & 1) ? __builtin_amdgcn_alignbit(P[(e >> 1) + 1], P[e >> 1], 16) : P[e >> 1];
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, pr), __builtin_bit_cast(u16x2_t, tap2<KC>(t)), acc, false);
+        }
+        // keep bytes are 0xFF (keep) / 0x00 (masked off, fm.py:619-636); all 0xFF without a mask
+        const uint32_t blur = (acc >> 16) & ((j < 4 ? cc.keep_lo >> (8 * j) : cc.keep_hi >> (8 * (j - 4))) & 0xFFu);
+        double b = bg[j];
+        if (INIT && init) b = (double)blur;
+        // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8
+        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 0, 0u);
+        const uint32_t d = __builtin_amdgcn_sad_u8(blur, q, 0u);  // absdiff
+        const uint64_t bits = __builtin_amdgcn_ballot_w64((int)d > thresh);
+        const double bl = __dmul_rn((double)blur, alpha);
+        double nb = __fma_rn(b, beta, bl);
+        if (!cc.vec) {  // the tile holding accumulateWeighted's scalar tail: two products, one add there
+            const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
+            if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
+        }
+        const bool rv = (cc.rowvalid >> j) & 1;
+        bg[j] = nb;  // out-of-image pixels compute values that are never stored
+        if (ln == j) mybits = rv ? (bits & cc.colmask) : 0;
+        if (PLANES && rv && ((cc.colmask >> ln) & 1)) {
+            const size_t plane = (size_t)a.h * w;
+            const size_t li = (size_t)(y0 + RPWV * wv + j) * w + x0 + ln;
+            a.planes[(size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)blur;
+            a.planes[2 * (size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)d;
+        }
+    }
+}
+
+template <int KC, bool PLANES, bool INIT>
+__global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int R = KC >> 1;
+    const Geo g(R);
+    uint8_t* raw = smem + g.o_raw;
+    uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + g.o_H);
+    int* rowy = reinterpret_cast<int*>(smem + g.o_rowy);
+    int* colx = reinterpret_cast<int*>(smem + g.o_colx);
+    int* roff = reinterpret_cast<int*>(smem + g.o_roff);
+
+    const int tid = threadIdx.x, ln = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int s = blockIdx.y;
+    const int ti = swizzle_tile(blockIdx.x, a.ntiles);
+    const int h = a.h, w = a.w, S = a.S;
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const int x0 = tx * TS, y0 = ty * TS;
+    const size_t plane = (size_t)h * w;
+    const size_t fbytes = plane * 3;
+    const bool hk = a.has_keep[s] != 0;
+    const uint8_t* keep = a.keep + (size_t)s * plane;
+    const bool init0 = INIT && a.init != nullptr && a.init[s] != 0;
+    // loaded source columns [cx0, cx1); interior tiles need no reflection
+    const int gx0 = x0 - g.PC;
+    const int cx0 = max(gx0, 0), cx1 = min(gx0 + g.GW, w);
+    const bool interior = gx0 >= 0 && gx0 + g.GW <= w;
+
+    for (int i = tid; i < g.GH; i += NT) rowy[i] = reflect101(y0 - R + i, h);
+    for (int i = tid; i < g.GW; i += NT) colx[i] = 3 * (min(max(reflect101(gx0 + i, w), cx0), cx1 - 1) - cx0);
+    __syncthreads();
+
+    // background of the wave's 8 rows x 64 columns -> registers; keep bytes likewise
+    double bg[RPWV];
+    ChainCtx cc;
+    {
+        const double* bgi = a.bg_in + (size_t)s * plane;
+        const int x = x0 + ln;
+        cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
+        cc.rowvalid = 0;
+        cc.keep_lo = cc.keep_hi = 0;
+        cc.hk = hk;
+#pragma unroll
+        for (int j = 0; j < RPWV; j++) {
+            const int y = y0 + RPWV * wv + j;
+            const bool in = x < w && y < h;
+            if (y < h) cc.rowvalid |= 1u << j;
+            bg[j] = (!init0 && in) ? bgi[(size_t)y * w + x] : 0.0;
+            const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
+            if (j < 4) cc.keep_lo |= kb << (8 * j);
+            else cc.keep_hi |= kb << (8 * (j - 4));
+        }
+        const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
+        cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
+    }
+    // consume those loads here (the asm is a use, so the compiler waits before it):
+    // inside the frame loop only the raw prefetch is then in flight and the chain
+    // stage never waits for it
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
+    asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
+
+    // horizontal stage geometry: lane -> (row group rg, gray quad q)
+    constexpr int PCc = 4 * ((R + 3) / 4);
+    constexpr int NQc = (TS + 2 * PCc) / 4;
+    constexpr int GHc = TS + 2 * R;
+    constexpr int RPW = 64 / NQc;
+    constexpr int NIT = (GHc + RPW * NW - 1) / (RPW * NW);
+    constexpr int OFF = PCc - R;
+    constexpr int NQN = (3 + OFF + 2 * R) / 4 + 1;   // gray quads holding a quad's taps
+    constexpr int NG = (KC + 3) / 4;                   // dot4 groups (last one zero padded)
+    constexpr int NQW = (6 + OFF + 4 * (NG - 1)) / 4 + 1;  // quads the 4-byte windows touch
+    const int rg = ln / NQc, q = ln - rg * NQc;
+    uint32_t cpk[NG];
+#pragma unroll
+    for (int gi = 0; gi < NG; gi++) cpk[gi] = tap4<KC>(gi);
+
+    constexpr int NCH = (GHc * (a16(3 * (TS + 2 * PCc) + 15) / 16) + NT - 1) / NT;
+    ChunkPlan<NCH> plan;
+    plan_chunks(plan, rowy, g, cx0, w, tid);
+    const uint32_t span = 3u * (uint32_t)(cx1 - cx0), fb32 = (uint32_t)fbytes;
+    // ---- gray (4 px per lane) + horizontal taps of frame f -> transposed H (u16)
+    auto gray_stage = [&](const uint8_t* rawb, const int* roffb, uint16_t* Hb, size_t f) {
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int gy = (it * NW + wv) * RPW + rg;
+            const bool act = rg < RPW && gy < GHc;
+            uint32_t g4 = 0;
+            if (act) {
+                const int ro = roffb[gy];
+                const uint8_t* rowp = rawb + gy * g.RS + ro;
+                if (interior && (ro & 3) == 0) {
+                    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rowp + 12 * q);
+                    g4 = gray4(p32[0], p32[1], p32[2]);
+                } else {  // reflected / unaligned columns
+                    const int c0 = 4 * q;
+                    g4 = gray1(rowp + colx[c0]) | (gray1(rowp + colx[c0 + 1]) << 8) | (gray1(rowp + colx[c0 + 2]) << 16) |
+                         (gray1(rowp + colx[c0 + 3]) << 24);
+                }
+                if (PLANES) {
+                    const int y = y0 - R + gy, xq = gx0 + 4 * q;
+                    if (gy >= R && gy < R + TS && xq >= x0 && xq < x0 + TS && y < h) {
+                        uint8_t* gp = a.planes + f * plane + (size_t)y * w;
+#pragma unroll
+                        for (int b = 0; b < 4; b++)
+                            if (xq + b < w) gp[xq + b] = (uint8_t)(g4 >> (8 * b));
+                    }
+                }
+            }
+            uint32_t qv[NQW];
+            qv[0] = g4;
+#pragma unroll
+            for (int d = 1; d < NQW; d++) qv[d] = d < NQN ? (uint32_t)__shfl_down((int)g4, d, 64) : 0u;  // zero-weight bytes
+            if (act && q < TS / 4) {
+                const uint32_t h0 = htap<0, OFF, NG, 0, NQW>(qv, cpk, 0u);
+                const uint32_t h1 = htap<1, OFF, NG, 0, NQW>(qv, cpk, 0u);
+                const uint32_t h2 = htap<2, OFF, NG, 0, NQW>(qv, cpk, 0u);
+                const uint32_t h3 = htap<3, OFF, NG, 0, NQW>(qv, cpk, 0u);
+                uint16_t* hc = Hb + (4 * q) * g.RSH + gy;
+                hc[0] = (uint16_t)h0;
+                hc[g.RSH] = (uint16_t)h1;
+                hc[2 * g.RSH] = (uint16_t)h2;
+                hc[3 * g.RSH] = (uint16_t)h3;
+            }
+        }
+    };
+    auto stage_raw = [&](const Raw<NCH>& Rr, int buf, size_t f) {
+        store_raw(Rr, raw + buf * g.raw_bytes, g, tid);
+        if (tid < g.GH)
+            roff[buf * (g.roff_bytes / 4) + tid] =
+                (int)(((uintptr_t)(a.src + f * fbytes) + ((size_t)rowy[tid] * w + cx0) * 3) & 15);
+    };
+
+    // Software pipeline, one barrier per frame: iteration t runs the chain of
+    // frame t (H buffer t&1) and the gray/horizontal stage of frame t+1 (raw and
+    // H buffers (t+1)&1), while frame t+2's raw tile is in flight into registers.
+    const int t0 = a.t_begin, t1 = a.t_end;
+    Raw<NCH> Rw;
+    load_raw(Rw, a.src + ((size_t)t0 * S + s) * fbytes, fb32, plan, span);
+    stage_raw(Rw, 0, (size_t)t0 * S + s);
+    if (t0 + 1 < t1) load_raw(Rw, a.src + ((size_t)(t0 + 1) * S + s) * fbytes, fb32, plan, span);
+    lds_barrier();
+    gray_stage(raw, roff, Hs, (size_t)t0 * S + s);
+
+    for (int t = t0; t < t1; t++) {
+        const int b = (t - t0) & 1;
+        const size_t f = (size_t)t * S + s;
+        if (t + 1 < t1) {
+            stage_raw(Rw, b ^ 1, f + S);
+            if (t + 2 < t1) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
+        }
+        lds_barrier();
+
+        // ---- vertical taps + chain for the wave's 8 rows; threshold bits by ballot
+        uint64_t mybits = 0;
+        // launder the per-tile uniforms each frame: otherwise LICM hoists dozens of
+        // per-row exec masks out of the frame loop and they spill
+        ChainCtx ccf = cc;
+        int x0f = x0, y0f = y0, wvf = wv;
+        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+        asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+        chain_rows<KC, PLANES, INIT>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf, init0 && t == t0,
+                                     mybits);
+        if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
+
+        if (t + 1 < t1)
+            gray_stage(raw + (b ^ 1) * g.raw_bytes, roff + (b ^ 1) * (g.roff_bytes / 4), Hs + (b ^ 1) * (g.H_bytes / 2),
+                       f + S);
+    }
+
+    // background out (ping-pong: neighbours never read this batch's update)
+    double* bgo = a.bg_out + (size_t)s * plane;
+    const int x = x0 + ln;
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) {
+        const int y = y0 + RPWV * wv + j;
+        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+    }
+}
+
+}  // namespace px
+
+int pix_lds_bytes(int ksize) { return px::Geo(ksize >> 1).bytes; }
+
+bool pix_supported(int ksize) { return ksize == 5 || ksize == 3 || ksize == 7 || ksize == 21; }
+
+template <int K>
+static bool taps_match(const FusedArgs& a) {
+    for (int i = 0; i < K; i++)
+        if (a.coef[i] != px::Taps<K>::c[i]) return false;
+    return true;
+}
+
+hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init) {
+    const int bytes = px::Geo(a.ksize >> 1).bytes;
+    const bool ok = a.ksize == 3 ? taps_match<3>(a) : a.ksize == 5 ? taps_match<5>(a) : a.ksize == 7 ? taps_match<7>(a)
+                  : a.ksize == 21 ? taps_match<21>(a) : false;
+    if (!ok) return hipErrorInvalidValue;
+    dim3 grid(a.ntiles, a.S);
+#define FM_PIX_LAUNCH(K, P, I)                                                                                  \
+    do {                                                                                                        \
+        (void)hipFuncSetAttribute((const void*)px::k_pix<K, P, I>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
+        hipLaunchKernelGGL((px::k_pix<K, P, I>), grid, dim3(px::NT), bytes, st, a);                             \
+    } while (0)
+#define FM_PIX_CASE(K)                                                    \
+    case K:                                                               \
+        if (planes) {                                                     \
+            if (init) FM_PIX_LAUNCH(K, true, true); else FM_PIX_LAUNCH(K, true, false);   \
+        } else {                                                          \
+            if (init) FM_PIX_LAUNCH(K, false, true); else FM_PIX_LAUNCH(K, false, false); \
+        }                                                                 \
+        break;
+    switch (a.ksize) {
+        FM_PIX_CASE(3)
+        FM_PIX_CASE(5)
+        FM_PIX_CASE(7)
+        FM_PIX_CASE(21)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef FM_PIX_LAUNCH
+#undef FM_PIX_CASE
+    return hipGetLastError();
+}
+
+}  // namespace fm

@@ -228,3 +228,37 @@ def test_stream_group_on_gpu(tmp_path):
         vid = videoio.SyntheticCapture(W, H, n, s).video
         counts = [st.step(vid.frame(i))["count"] for i in range(n)]
         assert v.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3), s
+
+
+@pytest.mark.parametrize("k", [3, 5, 7, 21])
+def test_convert_scale_abs_ties_and_saturation(k):
+    """Background values on exact .5 ties, just off them, negative and > 255 (convertScaleAbs, fm.py:250):
+    the GPU's f64 -> f32 -> rne -> saturate chain and the accumulate must match the oracle bit for bit."""
+    W, H = 96, 40
+    rng = np.random.default_rng(k)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=k, threshold=1, avg=0.25, max_batch=1,
+                       keep_planes=True)
+    base = np.floor(rng.random((H, W)) * 300 - 20)
+    frac = rng.choice([0.5, -0.5, 0.4999999999, 0.5000000001, 0.25, 0.0, 1.5, 2.5], size=(H, W))
+    bg = base + frac
+    bg[0, :8] = [-0.5, -1.5, 255.5, 256.5, 254.5, 0.5, 1e9, -1e9]
+    eng.set_background(0, bg)
+    fr = np.repeat(rng.integers(0, 256, (1, 1, H, W, 1), dtype=np.uint8), 3, axis=-1)
+    eng.submit(fr)
+    eng.wait()
+    blur = oracle.gauss_blur(oracle.bgr2gray(fr[0, 0]), k)
+    np.testing.assert_array_equal(eng.plane(PLANE_BLUR, 0, 0), blur)
+    delta, th = oracle.diff_thresh(blur, bg, 1)
+    np.testing.assert_array_equal(eng.plane(PLANE_DELTA, 0, 0), delta)
+    np.testing.assert_array_equal(eng.mask(0, 0), oracle.dilate5(th))
+    ref = bg.copy()
+    oracle.accumulate(blur, ref, 0.25)
+    np.testing.assert_array_equal(eng.background(0), ref)
+    eng.close()
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (100, 56), (203, 131), (64, 64), (65, 1)])
+def test_batch_split_and_tail_geometries(W, H):
+    """Odd sizes exercise the partial tiles, the unaligned-row gray path, reflected borders and
+    accumulateWeighted's scalar tail (h*w % 16 != 0); batch of 5 includes the init frame launch."""
+    run_pair(W, H, W, ksize=5, T=5, n_batches=2, keep_planes=False)
