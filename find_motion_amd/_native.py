@@ -152,7 +152,7 @@ class MotionEngine:
         self.keep_planes = bool(keep_planes)
         self.generation = 0    # bumped at every wait(): results of older batches are gone
         self._init = [False] * n_streams
-        self._inflight = None  # keeps host frames alive until wait()
+        self._inflight = []    # (n_frames, host frames kept alive) per submitted, not yet waited batch
 
     # -- plumbing ------------------------------------------------------------
     def _check(self, rc: int) -> int:
@@ -219,19 +219,21 @@ class MotionEngine:
         if f.shape[1:] != (self.n_streams,) + self.src_shape:
             raise ValueError(f"frames shape {f.shape} != [n][{self.n_streams}]{self.src_shape}")
         self._check(self._L.fm_submit(self._h, _ptr(f), f.shape[0], 0))
-        self._inflight = f
-        self._pending_n = f.shape[0]
+        self._inflight.append((f.shape[0], f))
 
     def submit_device(self, ptr: int, n_frames: int) -> None:
-        """Frames already in device memory (e.g. a torch CUDA tensor's data_ptr())."""
+        """Frames already in device memory (e.g. a torch CUDA tensor's data_ptr()).
+
+        Up to two batches may be in flight (submit batch i+1 before wait() for
+        batch i): the contour pass of one overlaps the pixel kernel of the next."""
         self._check(self._L.fm_submit(self._h, C.c_void_p(ptr), n_frames, 1))
-        self._inflight = None
-        self._pending_n = n_frames
+        self._inflight.append((n_frames, None))
 
     def wait(self) -> None:
+        """Complete the oldest batch in flight; its results become readable."""
         self._check(self._L.fm_wait(self._h))
-        self._inflight = None
-        self.last_batch = getattr(self, "_pending_n", 0)
+        if self._inflight:
+            self.last_batch = self._inflight.pop(0)[0]
         self.generation += 1
         self._init = [True] * self.n_streams
 

@@ -31,6 +31,28 @@ enum class ResizeMode { Identity, Fast, General };
 
 }  // namespace
 
+// One batch's device results.  The fused paths keep two slots so that batch
+// i's contour pass (CCL stream) overlaps batch i+1's pixel kernel (pixel stream).
+struct BatchSlot {
+    uint8_t* d_in = nullptr;        // host-fed staging [T][S][H][W][3]
+    uint8_t* d_work = nullptr;      // resized BGR [T][S][h][w][3] (mode D)
+    uint8_t* d_planes = nullptr;    // [3][T][S][h*w] gray, blur, frame_delta (FM_FLAG_KEEP_PLANES)
+    uint64_t* d_bits = nullptr;     // threshold bit rows (k_pix output)
+    uint64_t* d_dbits = nullptr;    // dilated bit rows = VideoFrame.thresh
+    TileRec* d_tiles = nullptr;
+    NodeRec* d_nodes = nullptr;
+    int32_t* d_heavy = nullptr;
+    int32_t* d_count = nullptr;     // [2F+1]
+    int32_t* h_count = nullptr;     // pinned [F]
+    int32_t* h_overflow = nullptr;  // pinned [F]
+    int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
+    int32_t* d_rec = nullptr;       // device alias of h_rec
+    uint8_t* h_init = nullptr;      // pinned [S]
+    hipEvent_t ev_pix = nullptr, ev_done = nullptr;
+    int n = 0;                      // frames in flight in this slot (0 = none)
+    uint64_t gen = 0;               // submits into this slot
+};
+
 struct fm_ctx {
     fm_params p{};
     int h = 0, w = 0;
@@ -40,48 +62,41 @@ struct fm_ctx {
     AreaAxis ax, ay;
     std::vector<int32_t> coef;
 
-    hipStream_t own_stream = nullptr, stream = nullptr;
+    // streams: pixel work (caller-replaceable), contour pass, synchronous reads
+    hipStream_t own_stream = nullptr, stream = nullptr, ccl_stream = nullptr, aux_stream = nullptr;
     KernelTimer timer;
 
-    // device buffers
-    uint8_t* d_in = nullptr;      // host-fed staging [T][S][H][W][3]
-    uint8_t* d_work = nullptr;    // resized BGR [T][S][h][w][3]
+    // device state shared by all batches
     double* d_bg[2] = {nullptr, nullptr};
     int bg_cur = 0;
     uint8_t* d_keep = nullptr;    // [S][h*w]
     uint8_t* d_has_keep = nullptr;
     uint8_t* d_init = nullptr;
-    uint8_t* d_mask = nullptr;    // [T][S][h*w]
-    uint8_t* d_planes = nullptr;  // [3][T][S][h*w]
-    int32_t* d_label = nullptr;
+    uint8_t* d_mask = nullptr;    // fused: one plane (fm_read_mask expansion, pixel-CCL fallback); v1: [T][S][h*w]
+    int32_t* d_label = nullptr;   // pixel-level CCL (v1 path, fused-path overflow fallback)
     int32_t* d_cid = nullptr;
     uint8_t* d_outer = nullptr;
-    int32_t* d_count = nullptr;
-    int32_t* d_rec = nullptr;       // device alias of h_rec (mapped)
-    int32_t* d_rec_dev = nullptr;   // device-resident records for the pixel-level CCL (uses atomics)
-    // tile-summary CCL (fused path)
+    int32_t* d_rec_dev = nullptr;
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;
-    TileRec* d_tiles = nullptr;
-    int32_t* d_heavy = nullptr;
-    uint64_t* d_bits = nullptr;    // threshold bit rows (k_pix output)
-    uint64_t* d_dbits = nullptr;   // dilated bit rows = VideoFrame.thresh
-    NodeRec* d_nodes = nullptr;
-    int32_t* h_overflow = nullptr;  // pinned [T*S]
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
     float *d_xwt = nullptr, *d_ywt = nullptr;
 
-    // host state
+    // batches
+    BatchSlot slots[2];
+    int nslots = 1;
+    int next_slot = 0;
+    std::vector<int> inflight;     // FIFO of submitted, not yet waited slots
+    int ready_slot = -1;           // slot of the last waited batch
+    uint64_t ready_gen = 0;
+    int ready = 0;                 // frames of the last waited batch
+    std::vector<int32_t> ready_counts;                    // [ready * S]
+    std::vector<std::vector<fm_contour>> contours;        // per (t*S+s), sorted
+
     std::vector<uint8_t> bg_init, has_keep;
-    uint8_t* h_init = nullptr;    // pinned
-    int32_t* h_count = nullptr;   // pinned [T*S]
-    int32_t* h_rec = nullptr;     // pinned [T*S*cap*5]
-    int pending = 0;              // frames in flight (0 = idle)
-    int ready = 0;                // frames with readable results
-    std::vector<std::vector<fm_contour>> contours;  // per (t*S+s), sorted
     std::string err;
-    int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of the fused kernel (results invalid)
+    int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of k_fused (results invalid)
 };
 
 namespace {
@@ -195,14 +210,16 @@ void dfree(T*& p) {
 }
 
 int check_idle(fm_ctx* c) {
-    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
+    if (!c->inflight.empty()) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
     return FM_OK;
 }
 
-int check_frame(fm_ctx* c, int frame, int stream) {
-    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
+// results of the last waited batch (device-side ones live until its slot is resubmitted)
+int check_frame(fm_ctx* c, int frame, int stream, bool device_data) {
     if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
     if (frame < 0 || frame >= c->ready) return fail(c, FM_EINVAL, "frame %d not in the last batch (%d frames)", frame, c->ready);
+    if (device_data && (c->ready_slot < 0 || c->slots[c->ready_slot].gen != c->ready_gen))
+        return fail(c, FM_ESTATE, "the batch's device results were overwritten by a later submit");
     return FM_OK;
 }
 
@@ -211,8 +228,9 @@ int check_frame(fm_ctx* c, int frame, int stream) {
 // ---------------------------------------------------------------------------
 // KernelTimer
 namespace fm {
-int KernelTimer::begin(const char* name) {
+int KernelTimer::begin(const char* name, hipStream_t st) {
     if (!enabled) return -1;
+    if (!st) st = stream;
     int id = -1;
     for (size_t i = 0; i < names.size(); i++)
         if (names[i] == name || std::strcmp(names[i], name) == 0) id = (int)i;
@@ -229,16 +247,21 @@ int KernelTimer::begin(const char* name) {
     } else {
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
     }
-    (void)hipEventRecord(a, stream);
-    pending.push_back({id, a, b});
+    (void)hipEventRecord(a, st);
+    pending.push_back({id, a, b, st});
     return (int)pending.size() - 1;
 }
 void KernelTimer::end(int token) {
     if (token < 0 || token >= (int)pending.size()) return;
-    (void)hipEventRecord(pending[token].b, stream);
+    (void)hipEventRecord(pending[token].b, pending[token].st);
 }
 void KernelTimer::collect() {
+    std::vector<Rec> keep;
     for (auto& r : pending) {
+        if (hipEventQuery(r.b) == hipErrorNotReady) {  // a later batch still running
+            keep.push_back(r);
+            continue;
+        }
         float t = 0;
         if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
             ms[r.id] += t;
@@ -247,7 +270,7 @@ void KernelTimer::collect() {
         pool.push_back(r.a);
         pool.push_back(r.b);
     }
-    pending.clear();
+    pending.swap(keep);
 }
 void KernelTimer::reset() {
     std::fill(ms.begin(), ms.end(), 0.0);
@@ -312,6 +335,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     fm_ctx* cp = c.get();
     HIP_TRY(cp, hipSetDevice(p.device));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_stream, hipStreamNonBlocking));
+    HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & FM_FLAG_PROFILE) != 0;
     c->timer.stream = c->stream;
@@ -321,42 +346,49 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->src_frame_bytes = (size_t)p.src_h * p.src_w * 3;
     const size_t frames = S * T, px = frames * c->work_plane;
     int rc;
-    if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &c->d_work, px * 3))) return rc;
-    for (int i = 0; i < 2; i++)
-        if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024;
     c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
                  std::getenv("FM_NO_PIX") == nullptr;
-    // dilated masks stay as bit rows on the fused paths; d_mask is one plane there
-    // (fm_read_mask expansion target, pixel-CCL fallback input)
+    c->nslots = c->use_fused ? 2 : 1;
+    for (int i = 0; i < 2; i++)
+        if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
-        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, c->use_fused ? c->work_plane : px)) ||
-        (rc = dalloc(cp, &c->d_count, 2 * frames + 1)))
+        (rc = dalloc(cp, &c->d_init, S)) || (rc = dalloc(cp, &c->d_mask, c->use_fused ? c->work_plane : px)))
         return rc;
-    // contour records: mapped pinned host memory written directly by the
-    // kernels (only the records that exist cross PCIe; no D2H copy of the
-    // capacity-sized buffer)
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
-    HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->d_rec, c->h_rec, 0));
     if (c->use_fused) {
         c->ntx = (c->w + 63) / 64;
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
         c->nnodes = c->ntiles * kTileMaxRuns;
-        if ((rc = dalloc(cp, &c->d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &c->d_tiles, frames * c->ntiles)) ||
-            (rc = dalloc(cp, &c->d_dbits, frames * c->ntiles * 64)) ||
-            (c->use_pix && (rc = dalloc(cp, &c->d_bits, frames * c->ntiles * 64))) ||
-            (rc = dalloc(cp, &c->d_nodes, frames * (size_t)c->nnodes)))
-            return rc;
     }
-    // pixel-level CCL buffers: the whole batch on the v1 path, one frame for the
-    // fused path's overflow fallback
+    for (int i = 0; i < c->nslots; i++) {
+        BatchSlot& b = c->slots[i];
+        if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &b.d_work, px * 3))) return rc;
+        if ((rc = dalloc(cp, &b.d_count, 2 * frames + 1))) return rc;
+        if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
+        if (c->use_fused) {
+            if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_dbits, frames * c->ntiles * 64)) ||
+                (c->use_pix && (rc = dalloc(cp, &b.d_bits, frames * c->ntiles * 64))) ||
+                (rc = dalloc(cp, &b.d_nodes, frames * (size_t)c->nnodes)))
+                return rc;
+        }
+        // contour records: mapped pinned host memory written directly by the kernels
+        // (only the records that exist cross PCIe)
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.d_rec, b.h_rec, 0));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t)));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t)));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
+        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
+        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
+    }
+    // pixel-level CCL: the whole batch on the v1 path, one frame for the fused path's overflow fallback
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
     if ((rc = dalloc(cp, &c->d_label, ccl_px)) || (rc = dalloc(cp, &c->d_cid, ccl_px)) ||
         (rc = dalloc(cp, &c->d_outer, ccl_px)) ||
         (rc = dalloc(cp, &c->d_rec_dev, (c->use_fused ? 1 : frames) * (size_t)p.max_contours * 5)))
         return rc;
-    if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &c->d_planes, px * 3))) return rc;
     HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
     HIP_TRY(cp, hipMemset(c->d_bg[0], 0, S * c->work_plane * sizeof(double)));
     HIP_TRY(cp, hipMemset(c->d_bg[1], 0, S * c->work_plane * sizeof(double)));
@@ -371,9 +403,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
             (rc = up(&c->d_yofs, c->ay.ofs)) || (rc = up(&c->d_ycnt, c->ay.cnt)) || (rc = up(&c->d_ywt, c->ay.wt)))
             return rc;
     }
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_init, S));
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_count, frames * sizeof(int32_t)));
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_overflow, frames * sizeof(int32_t)));
     c->bg_init.assign(S, 0);
     c->has_keep.assign(S, 0);
     if (const char* e = std::getenv("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
@@ -384,18 +413,21 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 void fm_destroy(fm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
-    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_in); dfree(c->d_work); dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep);
-    dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask); dfree(c->d_planes); dfree(c->d_label);
-    dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_count); dfree(c->d_rec_dev); c->d_rec = nullptr;
-    dfree(c->d_tiles); dfree(c->d_heavy); dfree(c->d_bits); dfree(c->d_dbits); dfree(c->d_nodes);
-    if (c->h_overflow) (void)hipHostFree(c->h_overflow);
+    for (hipStream_t st : {c->own_stream, c->stream, c->ccl_stream, c->aux_stream})
+        if (st) (void)hipStreamSynchronize(st);
+    for (auto& b : c->slots) {
+        dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
+        dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count);
+        for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init})
+            if (hp) (void)hipHostFree(hp);
+        if (b.ev_pix) (void)hipEventDestroy(b.ev_pix);
+        if (b.ev_done) (void)hipEventDestroy(b.ev_done);
+    }
+    dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
+    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
-    if (c->h_init) (void)hipHostFree(c->h_init);
-    if (c->h_count) (void)hipHostFree(c->h_count);
-    if (c->h_rec) (void)hipHostFree(c->h_rec);
-    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    for (hipStream_t st : {c->own_stream, c->ccl_stream, c->aux_stream})
+        if (st) (void)hipStreamDestroy(st);
     delete c;
 }
 
@@ -439,45 +471,48 @@ int fm_set_hip_stream(fm_ctx* c, void* s) {
 
 int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
-    if (int rc = check_idle(c)) return rc;
+    if ((int)c->inflight.size() >= c->nslots)
+        return fail(c, FM_ESTATE, "%d batch(es) already in flight: call fm_wait first", (int)c->inflight.size());
     if (!frames || n < 1 || n > c->p.max_batch)
         return fail(c, FM_EINVAL, "n_frames %d outside [1, max_batch=%d] or null frames", n, c->p.max_batch);
     HIP_TRY(c, hipSetDevice(c->p.device));
+    const int si = c->next_slot;
+    BatchSlot& B = c->slots[si];
     const int S = c->p.n_streams;
     const size_t F = (size_t)n * S;
+    hipStream_t ps = c->stream;  // pixel stream: input, resize, pixel kernel (bg recurrence is ordered here)
     const uint8_t* src = frames;
     if (!on_device) {
-        if (!c->d_in) {
-            int rc = dalloc(c, &c->d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
+        if (!B.d_in) {
+            int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
             if (rc) return rc;
         }
-        HIP_TRY(c, hipMemcpyAsync(c->d_in, frames, F * c->src_frame_bytes, hipMemcpyHostToDevice, c->stream));
-        src = c->d_in;
+        HIP_TRY(c, hipMemcpyAsync(B.d_in, frames, F * c->src_frame_bytes, hipMemcpyHostToDevice, ps));
+        src = B.d_in;
     }
     const uint8_t* work = src;
     if (c->rmode == ResizeMode::General) {
-        int tok = c->timer.begin("resize_area");
-        HIP_TRY(c, launch_resize_area(c->stream, src, c->d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w,
-                                      c->d_xofs, c->d_xcnt, c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt,
-                                      c->d_ywt, c->ay.max_taps));
+        int tok = c->timer.begin("resize_area", ps);
+        HIP_TRY(c, launch_resize_area(ps, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->d_xofs, c->d_xcnt,
+                                      c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt, c->d_ywt, c->ay.max_taps));
         c->timer.end(tok);
-        work = c->d_work;
+        work = B.d_work;
     } else if (c->rmode == ResizeMode::Fast) {
-        int tok = c->timer.begin("resize_area_fast");
-        HIP_TRY(c, launch_resize_area_fast(c->stream, src, c->d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w,
-                                           c->fast_sx, c->fast_sy));
+        int tok = c->timer.begin("resize_area_fast", ps);
+        HIP_TRY(c, launch_resize_area_fast(ps, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->fast_sx,
+                                           c->fast_sy));
         c->timer.end(tok);
-        work = c->d_work;
+        work = B.d_work;
     }
     bool any_init = false;
     for (int s = 0; s < S; s++) {
-        c->h_init[s] = c->bg_init[s] ? 0 : 1;
-        any_init |= c->h_init[s] != 0;
+        B.h_init[s] = c->bg_init[s] ? 0 : 1;
+        any_init |= B.h_init[s] != 0;
     }
-    if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, c->h_init, S, hipMemcpyHostToDevice, c->stream));
+    if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, B.h_init, S, hipMemcpyHostToDevice, ps));
 
     const long long npx = (long long)c->work_plane;
-    HIP_TRY(c, hipMemsetAsync(c->d_count, 0, (2 * F + 1) * sizeof(int32_t), c->stream));
+    HIP_TRY(c, hipMemsetAsync(B.d_count, 0, (2 * F + 1) * sizeof(int32_t), ps));
     if (c->use_fused) {
         FusedArgs fa{};
         fa.src = work;
@@ -487,14 +522,14 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.has_keep = c->d_has_keep;
         fa.init = any_init ? c->d_init : nullptr;
         fa.mask_out = nullptr;
-        fa.planes = c->d_planes;
-        fa.bits = c->d_bits;
-        fa.dbits = c->d_dbits;
-        fa.tiles = c->d_tiles;
-        fa.nodes = c->d_nodes;
-        fa.count = c->d_count;
-        fa.heavy = c->d_heavy;
-        fa.rec = c->d_rec;
+        fa.planes = B.d_planes;
+        fa.bits = B.d_bits;
+        fa.dbits = B.d_dbits;
+        fa.tiles = B.d_tiles;
+        fa.nodes = B.d_nodes;
+        fa.count = B.d_count;
+        fa.heavy = B.d_heavy;
+        fa.rec = B.d_rec;
         fa.T = n;
         fa.S = S;
         fa.h = c->h;
@@ -515,7 +550,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.t_begin = 0;
         fa.t_end = n;
         if (c->use_pix) {
-            const bool planes = c->d_planes != nullptr;
+            const bool planes = B.d_planes != nullptr;
             // each launch reads d_bg[cur] and writes d_bg[cur ^ 1]
             auto run = [&](int t0, int t1, bool init, const char* name) -> int {
                 FusedArgs fp = fa;
@@ -524,8 +559,8 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
                 fp.bg_in = c->d_bg[c->bg_cur];
                 fp.bg_out = c->d_bg[c->bg_cur ^ 1];
                 if (!init) fp.init = nullptr;
-                int tok = c->timer.begin(name);
-                HIP_TRY(c, launch_pix(c->stream, fp, planes, init));
+                int tok = c->timer.begin(name, ps);
+                HIP_TRY(c, launch_pix(ps, fp, planes, init));
                 c->timer.end(tok);
                 c->bg_cur ^= 1;
                 return FM_OK;
@@ -538,95 +573,109 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
                 return rc;
             }
         } else {
-            HIP_TRY(c, launch_fused(c->stream, fa, &c->timer));
+            HIP_TRY(c, launch_fused(ps, fa, &c->timer));
             c->bg_cur ^= 1;
         }
-        HIP_TRY(c, launch_tile_ccl(c->stream, fa, c->use_pix, &c->timer));
-        HIP_TRY(c, hipMemcpyAsync(c->h_overflow, c->d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        // contour pass on its own stream, after this batch's pixel kernel
+        HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
+        HIP_TRY(c, hipStreamWaitEvent(c->ccl_stream, B.ev_pix, 0));
+        HIP_TRY(c, launch_tile_ccl(c->ccl_stream, fa, c->use_pix, &c->timer));
+        HIP_TRY(c, hipMemcpyAsync(B.h_overflow, B.d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->ccl_stream));
+        HIP_TRY(c, hipMemcpyAsync(B.h_count, B.d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->ccl_stream));
+        HIP_TRY(c, hipEventRecord(B.ev_done, c->ccl_stream));
     } else {
-    PixelArgs a{};
-    a.bg = nullptr;
-    a.keep = c->d_keep;
-    a.has_keep = c->d_has_keep;
-    a.S = S;
-    a.h = c->h;
-    a.w = c->w;
-    a.ksize = c->p.ksize;
-    a.thresh = c->p.threshold;
-    a.alpha = c->p.avg;
-    a.beta = 1.0 - c->p.avg;
-    a.acc_vec_end = npx - npx % 16;
-    a.cvt_simd = npx >= 16;
-    for (int i = 0; i < c->p.ksize; i++) a.coef[i] = c->coef[i];
-    const size_t step_px = (size_t)S * c->work_plane;
-    for (int t = 0; t < n; t++) {
-        a.src = work + (size_t)t * step_px * 3;  // work image is [T][S][h][w][3] in every resize mode
-        a.init = (t == 0 && any_init) ? c->d_init : nullptr;
-        a.mask_out = c->d_mask + (size_t)t * step_px;
-        if (c->d_planes) {
-            a.gray_out = c->d_planes + (size_t)t * step_px;
-            a.blur_out = c->d_planes + F * c->work_plane + (size_t)t * step_px;
-            a.delta_out = c->d_planes + 2 * F * c->work_plane + (size_t)t * step_px;
+        PixelArgs a{};
+        a.bg = nullptr;
+        a.keep = c->d_keep;
+        a.has_keep = c->d_has_keep;
+        a.S = S;
+        a.h = c->h;
+        a.w = c->w;
+        a.ksize = c->p.ksize;
+        a.thresh = c->p.threshold;
+        a.alpha = c->p.avg;
+        a.beta = 1.0 - c->p.avg;
+        a.acc_vec_end = npx - npx % 16;
+        a.cvt_simd = npx >= 16;
+        for (int i = 0; i < c->p.ksize; i++) a.coef[i] = c->coef[i];
+        const size_t step_px = (size_t)S * c->work_plane;
+        for (int t = 0; t < n; t++) {
+            a.src = work + (size_t)t * step_px * 3;  // work image is [T][S][h][w][3] in every resize mode
+            a.init = (t == 0 && any_init) ? c->d_init : nullptr;
+            a.mask_out = c->d_mask + (size_t)t * step_px;
+            if (B.d_planes) {
+                a.gray_out = B.d_planes + (size_t)t * step_px;
+                a.blur_out = B.d_planes + F * c->work_plane + (size_t)t * step_px;
+                a.delta_out = B.d_planes + 2 * F * c->work_plane + (size_t)t * step_px;
+            }
+            int tok = c->timer.begin("pixel", ps);
+            HIP_TRY(c, launch_pixel_pp(ps, a, c->d_bg[c->bg_cur], c->d_bg[c->bg_cur ^ 1]));
+            c->timer.end(tok);
+            c->bg_cur ^= 1;
         }
-        int tok = c->timer.begin("pixel");
-        HIP_TRY(c, launch_pixel_pp(c->stream, a, c->d_bg[c->bg_cur], c->d_bg[c->bg_cur ^ 1]));
-        c->timer.end(tok);
-        c->bg_cur ^= 1;
+        HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, F * c->work_plane, ps));
+        CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, B.d_count, c->d_rec_dev, (int)F, c->h, c->w, c->p.max_contours};
+        HIP_TRY(c, launch_ccl(ps, ca, &c->timer));
+        HIP_TRY(c, hipMemcpyAsync(B.h_rec, c->d_rec_dev, F * c->p.max_contours * 5 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  ps));
+        HIP_TRY(c, hipMemsetAsync(B.d_count + F, 0, F * sizeof(int32_t), ps));
+        HIP_TRY(c, hipMemcpyAsync(B.h_overflow, B.d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, ps));
+        HIP_TRY(c, hipMemcpyAsync(B.h_count, B.d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, ps));
+        HIP_TRY(c, hipEventRecord(B.ev_done, ps));
     }
-    HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, F * c->work_plane, c->stream));
-    CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count, c->d_rec_dev, (int)F, c->h, c->w, c->p.max_contours};
-    HIP_TRY(c, launch_ccl(c->stream, ca, &c->timer));
-    HIP_TRY(c, hipMemcpyAsync(c->h_rec, c->d_rec_dev, F * c->p.max_contours * 5 * sizeof(int32_t), hipMemcpyDeviceToHost,
-                              c->stream));
-    std::memset(c->h_overflow, 0, F * sizeof(int32_t));
-    }
-    HIP_TRY(c, hipMemcpyAsync(c->h_count, c->d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     for (int s = 0; s < S; s++) c->bg_init[s] = 1;
-    c->pending = n;
-    c->ready = 0;
+    B.n = n;
+    B.gen++;
+    c->inflight.push_back(si);
+    c->next_slot = (si + 1) % c->nslots;
     return FM_OK;
 }
 
 int fm_wait(fm_ctx* c) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
-    if (!c->pending) return FM_OK;
+    if (c->inflight.empty()) return FM_OK;
     HIP_TRY(c, hipSetDevice(c->p.device));
-    hipError_t e = hipStreamSynchronize(c->stream);
+    const int si = c->inflight.front();
+    c->inflight.erase(c->inflight.begin());
+    BatchSlot& B = c->slots[si];
+    hipError_t e = hipEventSynchronize(B.ev_done);
     if (e != hipSuccess) {
-        c->pending = 0;
-        return fail(c, FM_EHIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+        B.n = 0;
+        return fail(c, FM_EHIP, "hipEventSynchronize: %s", hipGetErrorString(e));
     }
+    const int n = B.n, S = c->p.n_streams, cap = c->p.max_contours;
+    const size_t F = (size_t)n * S;
     {
         // Fused path: a tile with more runs than kTileMaxRuns cannot come from a
         // dilated mask (<= 24 runs per 64-px row), but if it ever happens the
         // frame is relabelled on the GPU by the pixel-level CCL.
-        const size_t F = (size_t)c->pending * c->p.n_streams;
         bool redo = false;
         for (size_t f = 0; f < F; f++) {
-            if (!c->h_overflow[f]) continue;
+            if (!B.h_overflow[f]) continue;
             redo = true;
-            const size_t cap = c->p.max_contours;
-            HIP_TRY(c, hipMemsetAsync(c->d_count + f, 0, sizeof(int32_t), c->stream));
-            HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, c->stream));
-            HIP_TRY(c, launch_expand_bits(c->stream, c->d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
-            CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, c->d_count + f,
+            hipStream_t st = c->aux_stream;
+            HIP_TRY(c, hipMemsetAsync(B.d_count + f, 0, sizeof(int32_t), st));
+            HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, st));
+            HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+            CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, B.d_count + f,
                        c->d_rec_dev, 1, c->h, c->w, c->p.max_contours};
-            HIP_TRY(c, launch_ccl(c->stream, ca, nullptr));
-            HIP_TRY(c, hipMemcpyAsync(c->h_rec + f * cap * 5, c->d_rec_dev, cap * 5 * sizeof(int32_t),
-                                      hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipMemcpyAsync(c->h_count + f, c->d_count + f, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, launch_ccl(st, ca, nullptr));
+            HIP_TRY(c, hipMemcpyAsync(B.h_rec + f * cap * 5, c->d_rec_dev, cap * 5 * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipMemcpyAsync(B.h_count + f, B.d_count + f, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipStreamSynchronize(st));
         }
-        if (redo) HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)redo;
     }
     c->timer.collect();
-    const int n = c->pending, S = c->p.n_streams, cap = c->p.max_contours;
-    c->contours.assign((size_t)n * S, {});
-    for (size_t f = 0; f < (size_t)n * S; f++) {
-        const int cnt = std::min(c->h_count[f], cap);
+    c->ready_counts.assign(B.h_count, B.h_count + F);
+    c->contours.assign(F, {});
+    for (size_t f = 0; f < F; f++) {
+        const int cnt = std::min(B.h_count[f], cap);
         auto& v = c->contours[f];
         v.resize(cnt);
         std::vector<std::pair<int32_t, int>> order(cnt);
-        const int32_t* r = c->h_rec + f * cap * 5;
+        const int32_t* r = B.h_rec + f * cap * 5;
         for (int i = 0; i < cnt; i++) order[i] = {r[i * 5], i};
         std::sort(order.begin(), order.end());
         for (int i = 0; i < cnt; i++) {
@@ -642,53 +691,57 @@ int fm_wait(fm_ctx* c) {
         }
     }
     c->ready = n;
-    c->pending = 0;
+    c->ready_slot = si;
+    c->ready_gen = B.gen;
+    B.n = 0;
     return FM_OK;
 }
 
 int fm_get_counts(fm_ctx* c, int32_t* counts) {
     if (!c || !counts) return fail(c, FM_EINVAL, "null argument");
-    if (c->pending) return fail(c, FM_ESTATE, "a submit is in flight: call fm_wait first");
-    std::memcpy(counts, c->h_count, (size_t)c->ready * c->p.n_streams * sizeof(int32_t));
+    std::memcpy(counts, c->ready_counts.data(), c->ready_counts.size() * sizeof(int32_t));
     return FM_OK;
 }
 
 int fm_get_contours(fm_ctx* c, int frame, int stream, fm_contour* out, int cap) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
-    if (int rc = check_frame(c, frame, stream)) return rc;
+    if (int rc = check_frame(c, frame, stream, false)) return rc;
     const size_t f = (size_t)frame * c->p.n_streams + stream;
     const auto& v = c->contours[f];
     const int m = out ? std::min<int>(cap, (int)v.size()) : 0;
     for (int i = 0; i < m; i++) out[i] = v[i];
-    return c->h_count[f];
+    return c->ready_counts[f];
 }
 
 int fm_read_mask(fm_ctx* c, int frame, int stream, uint8_t* out) {
     if (!c || !out) return fail(c, FM_EINVAL, "null argument");
-    if (int rc = check_frame(c, frame, stream)) return rc;
+    if (int rc = check_frame(c, frame, stream, true)) return rc;
     HIP_TRY(c, hipSetDevice(c->p.device));
     const size_t f = (size_t)frame * c->p.n_streams + stream;
+    hipStream_t st = c->aux_stream;
     if (c->use_fused) {
-        HIP_TRY(c, launch_expand_bits(c->stream, c->d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
-        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+        const BatchSlot& B = c->slots[c->ready_slot];
+        HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask, c->work_plane, hipMemcpyDeviceToHost, st));
     } else {
-        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, st));
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipStreamSynchronize(st));
     return FM_OK;
 }
 
 int fm_read_plane(fm_ctx* c, int plane, int frame, int stream, uint8_t* out) {
     if (!c || !out) return fail(c, FM_EINVAL, "null argument");
-    if (!c->d_planes) return fail(c, FM_ESTATE, "planes not kept: create with FM_FLAG_KEEP_PLANES");
+    if (!(c->p.flags & FM_FLAG_KEEP_PLANES)) return fail(c, FM_ESTATE, "planes not kept: create with FM_FLAG_KEEP_PLANES");
     if (plane < 0 || plane > 2) return fail(c, FM_EINVAL, "plane %d", plane);
-    if (int rc = check_frame(c, frame, stream)) return rc;
+    if (int rc = check_frame(c, frame, stream, true)) return rc;
     HIP_TRY(c, hipSetDevice(c->p.device));
+    const BatchSlot& B = c->slots[c->ready_slot];
     const size_t f = (size_t)frame * c->p.n_streams + stream;
     const size_t Fcur = (size_t)c->ready * c->p.n_streams;
-    HIP_TRY(c, hipMemcpyAsync(out, c->d_planes + ((size_t)plane * Fcur + f) * c->work_plane, c->work_plane,
-                              hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpyAsync(out, B.d_planes + ((size_t)plane * Fcur + f) * c->work_plane, c->work_plane,
+                              hipMemcpyDeviceToHost, c->aux_stream));
+    HIP_TRY(c, hipStreamSynchronize(c->aux_stream));
     return FM_OK;
 }
 
@@ -698,6 +751,7 @@ int fm_read_background(fm_ctx* c, int stream, double* out) {
     if (stream < 0 || stream >= c->p.n_streams) return fail(c, FM_EINVAL, "stream %d out of range", stream);
     if (!c->bg_init[stream]) return fail(c, FM_ESTATE, "stream %d has no background yet", stream);
     HIP_TRY(c, hipSetDevice(c->p.device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpyAsync(out, c->d_bg[c->bg_cur] + (size_t)stream * c->work_plane, c->work_plane * sizeof(double),
                               hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));

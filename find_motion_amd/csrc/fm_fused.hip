@@ -908,7 +908,7 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
     const int bytes = fz::Layout(a.ksize >> 1).bytes;
     if (a.ksize > fz::KMAX_FUSED || bytes > 160 * 1024) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
-    int tok = tm ? tm->begin("fused") : -1;
+    int tok = tm ? tm->begin("fused", st) : -1;
     if (a.ksize == 5) {
         (void)hipFuncSetAttribute((const void*)fz::k_fused<5>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         hipLaunchKernelGGL(fz::k_fused<5>, grid, dim3(fz::NT), bytes, st, a);
@@ -923,7 +923,7 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
     hipError_t e;
     dim3 gm(a.ntiles, a.T * a.S);
-    int tok = tm ? tm->begin("tile_ccl") : -1;
+    int tok = tm ? tm->begin("tile_ccl", st) : -1;
     const long long items = (long long)a.T * a.S * a.ntiles;
     const dim3 gl((unsigned)((items + fz::CCL_WAVES - 1) / fz::CCL_WAVES));
     if (dilate) hipLaunchKernelGGL(fz::k_tile_ccl<true>, gl, dim3(64 * fz::CCL_WAVES), 0, st, a);
@@ -931,15 +931,15 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     hipLaunchKernelGGL(fz::k_tile_ccl_heavy, dim3(512), dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_merge") : -1;
+    tok = tm ? tm->begin("tile_merge", st) : -1;
     hipLaunchKernelGGL(fz::k_tile_merge, gm, dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_resolve1") : -1;
+    tok = tm ? tm->begin("tile_resolve1", st) : -1;
     hipLaunchKernelGGL(fz::k_tile_resolve1, gm, dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_resolve2") : -1;
+    tok = tm ? tm->begin("tile_resolve2", st) : -1;
     hipLaunchKernelGGL(fz::k_tile_resolve2, gm, dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     return hipGetLastError();

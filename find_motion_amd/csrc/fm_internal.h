@@ -123,15 +123,15 @@ hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, uint8_t* ou
 struct KernelTimer {
     bool enabled = false;
     hipStream_t stream = nullptr;
-    struct Rec { int id; hipEvent_t a, b; };
+    struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
     std::vector<const char*> names;
     std::vector<double> ms;
     std::vector<int64_t> launches;
-    int begin(const char* name);   // returns a token for end(), -1 when disabled
+    int begin(const char* name, hipStream_t st = nullptr);  // token for end(), -1 when disabled
     void end(int token);
-    void collect();                // after the stream has synchronised
+    void collect();                // folds in every pair whose end event has completed
     void reset();
     ~KernelTimer();
 };

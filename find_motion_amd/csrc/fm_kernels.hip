@@ -464,29 +464,29 @@ hipError_t launch_ccl(hipStream_t st, const CclArgs& a, KernelTimer* tm) {
     const int F = a.F, h = a.h, w = a.w, n = h * w;
     dim3 gb((w + CB - 1) / CB, (h + CB - 1) / CB, F);
     hipError_t e;
-    int tok = tm ? tm->begin("ccl_local") : -1;
+    int tok = tm ? tm->begin("ccl_local", st) : -1;
     hipLaunchKernelGGL(k_ccl_local, gb, dim3(256), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("ccl_merge") : -1;
+    tok = tm ? tm->begin("ccl_merge", st) : -1;
     hipLaunchKernelGGL(k_ccl_merge, gb, dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     dim3 gp((n + 255) / 256, F);
-    tok = tm ? tm->begin("ccl_flatten") : -1;
+    tok = tm ? tm->begin("ccl_flatten", st) : -1;
     hipLaunchKernelGGL(k_ccl_flatten, gp, dim3(256), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     dim3 go((2 * w + 2 * h + 255) / 256, F);
-    tok = tm ? tm->begin("ccl_outer") : -1;
+    tok = tm ? tm->begin("ccl_outer", st) : -1;
     hipLaunchKernelGGL(k_ccl_outer, go, dim3(256), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("ccl_roots") : -1;
+    tok = tm ? tm->begin("ccl_roots", st) : -1;
     hipLaunchKernelGGL(k_ccl_roots, gp, dim3(256), 0, st, a);
     if (tm) tm->end(tok);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("ccl_bbox") : -1;
+    tok = tm ? tm->begin("ccl_bbox", st) : -1;
     hipLaunchKernelGGL(k_ccl_bbox, gp, dim3(256), 0, st, a);
     if (tm) tm->end(tok);
     return hipGetLastError();
