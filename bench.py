@@ -88,8 +88,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
-    ap.add_argument("--batch", type=int, default=16, help="frames per stream per step")
-    ap.add_argument("--ring", type=int, default=32, help="device-resident frames per stream")
+    ap.add_argument("--batch", type=int, default=32, help="frames per stream per step")
+    ap.add_argument("--ring", type=int, default=64, help="device-resident frames per stream")
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
@@ -134,27 +134,31 @@ def main() -> None:
     base = ring.data_ptr()
     n_batches = R // T
 
-    # Pipelined like a live decoder feeding the engine: batch i+1 is submitted before
-    # batch i's results are collected, so batch i's contour pass (CCL stream) overlaps
-    # batch i+1's pixel kernel.  A step = one batch submitted + one batch completed.
+    # Pipelined like a live decoder feeding the engine: up to max_inflight batches are
+    # submitted before the oldest one's results are collected, so the contour passes
+    # of consecutive batches overlap each other and the next pixel kernels.  A step =
+    # one batch submitted + one batch completed; all timed batches are submitted and
+    # completed inside the timed region.
+    depth = eng.max_inflight
+
     def submit(i: int) -> None:
         eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
 
-    submit(0)
-    for i in range(args.warmup):
-        submit(i + 1)
-        eng.wait()
-    eng.wait()
+    def run(first: int, n: int) -> None:
+        for i in range(min(depth, n)):
+            submit(first + i)
+        for i in range(n):
+            eng.wait()  # completes batch i and frees its slot
+            if i + depth < n:
+                submit(first + i + depth)
+
+    run(0, args.warmup)
     eng.reset_kernel_times()
 
     dist.barrier(active)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    submit(args.warmup)  # every timed batch is submitted and completed inside the timed region
-    for i in range(args.steps):
-        if i + 1 < args.steps:
-            submit(args.warmup + i + 1)
-        eng.wait()
+    run(args.warmup, args.steps)
     torch.cuda.synchronize()
     dist.barrier(active)
     elapsed = dist.max_over_ranks(time.perf_counter() - t0, active, device=f"cuda:{local}")

@@ -23,7 +23,7 @@ EXPORTED = (
     "fm_abi_version", "fm_create", "fm_destroy", "fm_last_error", "fm_work_size", "fm_set_mask",
     "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
-    "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks",
+    "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
 )
 
 
@@ -84,6 +84,7 @@ def load() -> C.CDLL:
     L.fm_kernel_times.argtypes = [vp, vp, vp, vp, i32]
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
+    L.fm_max_inflight.argtypes = [vp]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version"):
             getattr(L, name).restype = i32
@@ -144,6 +145,7 @@ class MotionEngine:
         hh, ww = C.c_int(), C.c_int()
         self._check(self._L.fm_work_size(h, C.byref(hh), C.byref(ww)))
         self.work_shape = (hh.value, ww.value)
+        self.max_inflight = self._L.fm_max_inflight(h)
         self.n_streams = n_streams
         self.src_shape = (src_h, src_w, 3)
         self.max_batch = max_batch

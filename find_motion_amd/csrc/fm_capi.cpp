@@ -31,8 +31,12 @@ enum class ResizeMode { Identity, Fast, General };
 
 }  // namespace
 
-// One batch's device results.  The fused paths keep two slots so that batch
-// i's contour pass (CCL stream) overlaps batch i+1's pixel kernel (pixel stream).
+// One batch's device results.  The fused paths keep kSlots slots: the pixel
+// kernels run in submission order on the pixel stream (the background
+// recurrence), each slot's contour pass on its own stream, so the latency-bound
+// contour passes of consecutive batches overlap each other and the next
+// batches' pixel kernels.
+constexpr int kSlots = 3;
 struct BatchSlot {
     uint8_t* d_in = nullptr;        // host-fed staging [T][S][H][W][3]
     uint8_t* d_work = nullptr;      // resized BGR [T][S][h][w][3] (mode D)
@@ -41,6 +45,12 @@ struct BatchSlot {
     uint64_t* d_dbits = nullptr;    // dilated bit rows = VideoFrame.thresh
     TileRec* d_tiles = nullptr;
     NodeRec* d_nodes = nullptr;
+    uint32_t* d_tflag = nullptr;    // [F][ntiles] where tiles have threshold bits
+    uint8_t* d_candf = nullptr;     // [F][ntiles] tiles the contour pass labelled
+    int32_t* d_clist = nullptr;     // [F][ntiles] candidate lists
+    int32_t* d_rlist = nullptr;     // [F][ntiles] empty-region representatives
+    int32_t* d_regrep = nullptr;    // [F][ntiles] empty tile -> region representative
+    int32_t* d_ncr = nullptr;       // [F][2]
     int32_t* d_heavy = nullptr;
     int32_t* d_count = nullptr;     // [2F+1]
     int32_t* h_count = nullptr;     // pinned [F]
@@ -49,6 +59,7 @@ struct BatchSlot {
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
     hipEvent_t ev_pix = nullptr, ev_done = nullptr;
+    hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
     uint64_t gen = 0;               // submits into this slot
 };
@@ -63,7 +74,7 @@ struct fm_ctx {
     std::vector<int32_t> coef;
 
     // streams: pixel work (caller-replaceable), contour pass, synchronous reads
-    hipStream_t own_stream = nullptr, stream = nullptr, ccl_stream = nullptr, aux_stream = nullptr;
+    hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
     KernelTimer timer;
 
     // device state shared by all batches
@@ -84,7 +95,7 @@ struct fm_ctx {
     float *d_xwt = nullptr, *d_ywt = nullptr;
 
     // batches
-    BatchSlot slots[2];
+    BatchSlot slots[kSlots];
     int nslots = 1;
     int next_slot = 0;
     std::vector<int> inflight;     // FIFO of submitted, not yet waited slots
@@ -96,6 +107,10 @@ struct fm_ctx {
 
     std::vector<uint8_t> bg_init, has_keep;
     std::string err;
+    uint64_t* d_ts = nullptr;     // FM_TS: contour-pass phase stamps (profiling)
+    std::vector<double> ts_sum;   // summed phase deltas (cycles)
+    std::vector<int64_t> ts_n;
+    bool serial = false;  // FM_SERIAL: contour pass on the pixel stream (profiling: no overlap)
     int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of k_fused (results invalid)
 };
 
@@ -335,7 +350,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     fm_ctx* cp = c.get();
     HIP_TRY(cp, hipSetDevice(p.device));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-    HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_stream, hipStreamNonBlocking));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & FM_FLAG_PROFILE) != 0;
@@ -346,10 +360,11 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->src_frame_bytes = (size_t)p.src_h * p.src_w * 3;
     const size_t frames = S * T, px = frames * c->work_plane;
     int rc;
-    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024;
+    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
+                   ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
     c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
                  std::getenv("FM_NO_PIX") == nullptr;
-    c->nslots = c->use_fused ? 2 : 1;
+    c->nslots = c->use_fused ? kSlots : 1;
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
@@ -368,6 +383,9 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
         if (c->use_fused) {
             if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_tflag, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_candf, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_clist, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_rlist, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_regrep, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_ncr, frames * 2)) ||
                 (rc = dalloc(cp, &b.d_dbits, frames * c->ntiles * 64)) ||
                 (c->use_pix && (rc = dalloc(cp, &b.d_bits, frames * c->ntiles * 64))) ||
                 (rc = dalloc(cp, &b.d_nodes, frames * (size_t)c->nnodes)))
@@ -380,6 +398,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
+        HIP_TRY(cp, hipStreamCreateWithFlags(&b.ccl_stream, hipStreamNonBlocking));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
     }
@@ -406,18 +425,36 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->bg_init.assign(S, 0);
     c->has_keep.assign(S, 0);
     if (const char* e = std::getenv("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
+    c->serial = std::getenv("FM_SERIAL") != nullptr;
+    if (std::getenv("FM_TS") && c->use_fused) {
+        if ((rc = dalloc(cp, &c->d_ts, frames * c->ntiles * 16))) return rc;
+        c->ts_sum.assign(16, 0.0);
+        c->ts_n.assign(16, 0);
+    }
     *out = c.release();
     return FM_OK;
 }
 
 void fm_destroy(fm_ctx* c) {
     if (!c) return;
+    if (c->d_ts) {
+        std::fprintf(stderr, "[fm] contour-pass phase cycles (mean per labelled tile):");
+        for (int k = 2; k < 16; k++)
+            if (c->ts_n[k]) std::fprintf(stderr, " %d:%.0f(n=%lld)", k, c->ts_sum[k] / c->ts_n[k], (long long)c->ts_n[k]);
+        std::fprintf(stderr, "\n");
+        dfree(c->d_ts);
+    }
     (void)hipSetDevice(c->p.device);
-    for (hipStream_t st : {c->own_stream, c->stream, c->ccl_stream, c->aux_stream})
+    for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream})
         if (st) (void)hipStreamSynchronize(st);
     for (auto& b : c->slots) {
+        if (b.ccl_stream) {
+            (void)hipStreamSynchronize(b.ccl_stream);
+            (void)hipStreamDestroy(b.ccl_stream);
+        }
         dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
-        dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count);
+        dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
+        dfree(b.d_clist); dfree(b.d_rlist); dfree(b.d_regrep); dfree(b.d_ncr);
         for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init})
             if (hp) (void)hipHostFree(hp);
         if (b.ev_pix) (void)hipEventDestroy(b.ev_pix);
@@ -426,10 +463,12 @@ void fm_destroy(fm_ctx* c) {
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
-    for (hipStream_t st : {c->own_stream, c->ccl_stream, c->aux_stream})
+    for (hipStream_t st : {c->own_stream, c->aux_stream})
         if (st) (void)hipStreamDestroy(st);
     delete c;
 }
+
+int fm_max_inflight(const fm_ctx* c) { return c ? c->nslots : fail(nullptr, FM_EINVAL, "null context"); }
 
 int fm_work_size(const fm_ctx* c, int* h, int* w) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
@@ -513,6 +552,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
 
     const long long npx = (long long)c->work_plane;
     HIP_TRY(c, hipMemsetAsync(B.d_count, 0, (2 * F + 1) * sizeof(int32_t), ps));
+    if (B.d_tflag) HIP_TRY(c, hipMemsetAsync(B.d_tflag, 0, F * c->ntiles * sizeof(uint32_t), ps));
     if (c->use_fused) {
         FusedArgs fa{};
         fa.src = work;
@@ -526,6 +566,12 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.bits = B.d_bits;
         fa.dbits = B.d_dbits;
         fa.tiles = B.d_tiles;
+        fa.tflag = B.d_tflag;
+        fa.candf = B.d_candf;
+        fa.clist = B.d_clist;
+        fa.rlist = B.d_rlist;
+        fa.regrep = B.d_regrep;
+        fa.ncr = B.d_ncr;
         fa.nodes = B.d_nodes;
         fa.count = B.d_count;
         fa.heavy = B.d_heavy;
@@ -546,6 +592,8 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.beta = 1.0 - c->p.avg;
         fa.acc_vec_end = npx - npx % 16;
         fa.dbg_skip = c->dbg_skip;
+        fa.dbg_ts = c->d_ts;
+        if (c->d_ts) HIP_TRY(c, hipMemsetAsync(c->d_ts, 0, F * c->ntiles * 16 * sizeof(uint64_t), ps));
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
         fa.t_begin = 0;
         fa.t_end = n;
@@ -577,12 +625,13 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
             c->bg_cur ^= 1;
         }
         // contour pass on its own stream, after this batch's pixel kernel
+        hipStream_t cs = c->serial ? ps : B.ccl_stream;
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
-        HIP_TRY(c, hipStreamWaitEvent(c->ccl_stream, B.ev_pix, 0));
-        HIP_TRY(c, launch_tile_ccl(c->ccl_stream, fa, c->use_pix, &c->timer));
-        HIP_TRY(c, hipMemcpyAsync(B.h_overflow, B.d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->ccl_stream));
-        HIP_TRY(c, hipMemcpyAsync(B.h_count, B.d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, c->ccl_stream));
-        HIP_TRY(c, hipEventRecord(B.ev_done, c->ccl_stream));
+        HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
+        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer));
+        HIP_TRY(c, hipMemcpyAsync(B.h_overflow, B.d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, cs));
+        HIP_TRY(c, hipMemcpyAsync(B.h_count, B.d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, cs));
+        HIP_TRY(c, hipEventRecord(B.ev_done, cs));
     } else {
         PixelArgs a{};
         a.bg = nullptr;
@@ -656,7 +705,8 @@ int fm_wait(fm_ctx* c) {
             hipStream_t st = c->aux_stream;
             HIP_TRY(c, hipMemsetAsync(B.d_count + f, 0, sizeof(int32_t), st));
             HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, st));
-            HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+            HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, B.d_candf + f * c->ntiles, c->d_mask, c->h, c->w,
+                                          c->ntx));
             CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, B.d_count + f,
                        c->d_rec_dev, 1, c->h, c->w, c->p.max_contours};
             HIP_TRY(c, launch_ccl(st, ca, nullptr));
@@ -668,6 +718,21 @@ int fm_wait(fm_ctx* c) {
         (void)redo;
     }
     c->timer.collect();
+    if (c->d_ts) {  // profiling: mean cycles between consecutive stamps of each labelled tile
+        std::vector<uint64_t> ts(F * c->ntiles * 16);
+        HIP_TRY(c, hipMemcpy(ts.data(), c->d_ts, ts.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < F * c->ntiles; i++) {
+            const uint64_t* t = &ts[i * 16];
+            if (!t[1]) continue;
+            uint64_t prev = t[1];
+            for (int k = 2; k < 16; k++) {
+                if (!t[k]) continue;
+                c->ts_sum[k] += (double)(t[k] - prev);
+                c->ts_n[k]++;
+                prev = t[k];
+            }
+        }
+    }
     c->ready_counts.assign(B.h_count, B.h_count + F);
     c->contours.assign(F, {});
     for (size_t f = 0; f < F; f++) {
@@ -721,7 +786,8 @@ int fm_read_mask(fm_ctx* c, int frame, int stream, uint8_t* out) {
     hipStream_t st = c->aux_stream;
     if (c->use_fused) {
         const BatchSlot& B = c->slots[c->ready_slot];
-        HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, c->d_mask, c->h, c->w, c->ntx, c->ntiles));
+        HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, B.d_candf + f * c->ntiles, c->d_mask, c->h, c->w,
+                                      c->ntx));
         HIP_TRY(c, hipMemcpyAsync(out, c->d_mask, c->work_plane, hipMemcpyDeviceToHost, st));
     } else {
         HIP_TRY(c, hipMemcpyAsync(out, c->d_mask + f * c->work_plane, c->work_plane, hipMemcpyDeviceToHost, st));

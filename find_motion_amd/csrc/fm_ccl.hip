@@ -1,0 +1,743 @@
+// fm_ccl.hip — findContours(RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) count + boundingRect
+// on the GPU (gfx950); reference call site fm.py:269-272, consumer fm.py:674-694.
+//
+// Semantics (checked against the literal Suzuki-Abe
+// restatement in oracle/fm_oracle.c): foreground 8-connected, background
+// 4-connected; a foreground component yields one external contour iff the
+// background component left of its raster-first pixel touches the image
+// border (= the 1-px zero pad).  boundingRect = the component's pixel bbox.
+//
+// Work is proportional to motion.  A tile is a CANDIDATE when its dilated mask
+// can be non-empty: it has threshold bits, or a neighbour has them within 2 px
+// of the shared edge/corner (per-tile flags written by the pixel kernel).
+// Every other tile is empty background.  Global union-find nodes are
+// (tile, component ordinal), id = tile * kTileMaxRuns + ordinal, per frame.
+//   k_regions    one workgroup per frame: candidate list; empty tiles grouped
+//                into 4-connected regions in LDS, one node per region (at its
+//                representative tile), "outer" when the region reaches the grid border.
+//   k_tile_ccl   one wave per candidate: 5x5 dilation of its bit rows
+//                (fm.py:266), run-length labelling in LDS, a tile record (edge
+//                labels) and one node per component.
+//   k_tile_heavy tiles with more runs than the light pass holds (never for real
+//                dilated masks: <= 24 runs per 64-px row; kept for safety).
+//   k_merge      one wave per candidate: unions along its edges with candidate
+//                neighbours (right / below) and empty regions (all sides).
+//   k_fold_emit  one workgroup per frame: path compression with outer flags,
+//                bboxes and raster-first pixels folded into the roots (one thread
+//                per candidate or region), then the external test at each
+//                foreground root and the contour records (mapped host memory).
+// A frame with a tile beyond even the heavy pass is flagged (count[F+f]); the
+// host relabels it with the pixel-level CCL of fm_kernels.hip.
+#include "fm_internal.h"
+
+namespace fm {
+namespace cc {
+
+constexpr int TS = 64;
+constexpr int MAXR = kTileMaxRuns;
+constexpr int LIGHT = 256;      // runs held by the light pass
+constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k_merge
+constexpr int GW = 32;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
+constexpr int RG = 512;         // k_regions threads
+constexpr int MAX_REGION_TILES = 8192;
+constexpr uint32_t REF_OUTER = 0x80000000u;
+constexpr uint32_t REF_EDGE = 0x40000000u;
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ int lload(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// find with path halving (a pointer only ever moves to a smaller member of the
+// same set, so halving by atomicMin cannot undo a concurrent link)
+__device__ __forceinline__ int lfind(int* P, int x) {
+    for (;;) {
+        const int p = lload(&P[x]);
+        if (p == x) return x;
+        const int gp = lload(&P[p]);
+        if (gp == p) return p;
+        atomicMin(&P[x], gp);
+        x = gp;
+    }
+}
+// link the larger root under the smaller: a root is its set's smallest member
+__device__ __forceinline__ void lunion(int* P, int a, int b) {
+    for (;;) {
+        a = lfind(P, a);
+        b = lfind(P, b);
+        if (a == b) return;
+        if (a < b) {
+            const int old = atomicMin(&P[b], a);
+            if (old == b) return;
+            b = old;
+        } else {
+            const int old = atomicMin(&P[a], b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+// global union-find over NodeRec::parent (relaxed agent-scope loads bypass the
+// per-CU L1, so a find never follows a stale pointer written by another CU)
+__device__ __forceinline__ int gpar(NodeRec* N, int x) {
+    return __hip_atomic_load(&N[x].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// find with path halving by atomicMin: a pointer only moves to a smaller member
+// of the same set, so it cannot undo a concurrent link
+__device__ __forceinline__ int gfind(NodeRec* N, int x) {
+    for (;;) {
+        const int p = gpar(N, x);
+        if (p == x) return x;
+        const int gp = gpar(N, p);
+        if (gp == p) return p;
+        atomicMin(&N[x].parent, gp);
+        x = gp;
+    }
+}
+__device__ __forceinline__ void gunion(NodeRec* N, int a, int b) {
+    for (;;) {
+        a = gfind(N, a);
+        b = gfind(N, b);
+        if (a == b) return;
+        if (a < b) {
+            const int old = atomicMin(&N[b].parent, a);
+            if (old == b) return;
+            b = old;
+        } else {
+            const int old = atomicMin(&N[a].parent, b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+__device__ __forceinline__ bool tile_on_border(const FusedArgs& a, int ti) {
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    return tx == 0 || ty == 0 || tx == a.ntx - 1 || ty == a.nty - 1;
+}
+
+// ---------------------------------------------------------------------------
+// dilate(thresh, None, iterations=2) = 5x5 max (fm.py:266) on bit rows, lane = row
+__device__ __forceinline__ uint64_t hdil(uint64_t L, uint64_t C, uint64_t R) {
+    const uint64_t lo = (L >> 62) | (C << 2), hi = (C >> 62) | ((R & 3) << 2);
+    return lo | ((lo >> 1) | (hi << 63)) | ((lo >> 2) | (hi << 62)) | ((lo >> 3) | (hi << 61)) | ((lo >> 4) | (hi << 60));
+}
+
+__device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, int ti, int ln, uint64_t* hv) {
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const uint64_t* B = a.bits + f * (size_t)a.ntiles * 64;
+    auto row = [&](int t, int r) -> uint64_t { return B[(size_t)t * 64 + r]; };
+    const bool hl = tx > 0, hr = tx + 1 < a.ntx;
+    hv[ln + 2] = hdil(hl ? row(ti - 1, ln) : 0, row(ti, ln), hr ? row(ti + 1, ln) : 0);
+    if (ln < 4) {  // halo rows -2, -1 (tile above, rows 62, 63) and 64, 65 (tile below, rows 0, 1)
+        const int dy = ln < 2 ? -1 : 1;
+        const int rr = ln < 2 ? 62 + ln : ln - 2;
+        const int tyy = ty + dy;
+        uint64_t v = 0;
+        if (tyy >= 0 && tyy < a.nty) {
+            const int tt = tyy * a.ntx + tx;
+            v = hdil(hl ? row(tt - 1, rr) : 0, row(tt, rr), hr ? row(tt + 1, rr) : 0);
+        }
+        hv[ln < 2 ? ln : 64 + ln] = v;
+    }
+    lds_fence();
+    uint64_t o = hv[ln] | hv[ln + 1] | hv[ln + 2] | hv[ln + 3] | hv[ln + 4];
+    const int x0 = tx * TS, y0 = ty * TS;
+    const int vc = a.w - x0;
+    if (vc < 64) o &= (1ull << vc) - 1;
+    if (y0 + ln >= a.h) o = 0;
+    return o;
+}
+
+// ---------------------------------------------------------------------------
+// Run-length CCL of one dilated 64x64 tile (one wave, lane = tile row).
+// Runs are numbered in raster order; union-find over runs links the larger
+// root under the smaller, so a root is its component's raster-first run.
+// Foreground runs of adjacent rows connect 8-wise (x ranges within 1),
+// background runs 4-wise (x ranges overlap).  Out-of-image pixels are
+// background and, like pixels on the image border, mark their background
+// component "outer".  Output: TileRec (nroots, edge labels as component
+// ordinals | fg << 15) and NodeRec[ordinal].
+struct Scratch {
+    int* par;
+    int* amin;  // fg root: min x0; bg root: outer flag
+    int* amax;
+    int* ay;
+    uint8_t *rx0, *rx1, *rf;
+    int* rb;
+    uint16_t* ord;
+    uint32_t* pairs;  // run pairs (a | b << 16) to union, capacity 2 * CAP
+};
+
+// run index (in the tile's raster numbering) of the run of row `base` / `starts` holding bit p
+__device__ __forceinline__ int run_at(int base, uint64_t starts, int p) {
+    return base + __popcll(starts & ((2ull << p) - 1)) - 1;
+}
+
+#define FM_STAMP(k)                                                                          \
+    do {                                                                                     \
+        if (a.dbg_ts && ln == 0) a.dbg_ts[((size_t)f * a.ntiles + ti) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+// returns false (nothing written) if the tile has more than CAP runs
+template <int CAP>
+__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc) {
+    int* par = sc.par;
+    int* amin = sc.amin;
+    int* amax = sc.amax;
+    int* ay = sc.ay;
+    uint8_t* rx0 = sc.rx0;
+    uint8_t* rx1 = sc.rx1;
+    uint8_t* rf = sc.rf;
+    int* rb = sc.rb;
+    uint16_t* ord = sc.ord;
+    const int h = a.h, w = a.w;
+    const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
+    TileRec* TR = a.tiles + f * a.ntiles + ti;
+    NodeRec* NR = a.nodes + f * (size_t)a.nnodes + (size_t)ti * MAXR;
+
+    if (__ballot(m != 0) == 0) {  // empty tile: one background component
+        TR->edges[ln] = 0;
+        TR->edges[64 + ln] = 0;
+        TR->edges[128 + ln] = 0;
+        TR->edges[192 + ln] = 0;
+        if (ln == 0) {
+            TR->nroots = 1;
+            const bool outer = x0 == 0 || y0 == 0 || x0 + TS - 1 >= w - 1 || y0 + TS - 1 >= h - 1;
+            NodeRec nrec;
+            nrec.key = 0;
+            nrec.parent = ti * MAXR;
+            nrec.flags = outer ? 2u : 0u;
+            nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+            NR[0] = nrec;
+        }
+        return true;
+    }
+
+    const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
+    const int nr = __popcll(starts);
+    int incl = nr;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (ln >= o) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    const int base = incl - nr;
+    if (total > CAP) return false;
+    FM_STAMP(3);
+    rb[ln] = base;
+    if (ln == 63) rb[64] = total;
+    const int gy = y0 + ln;
+    {
+        uint64_t sb = starts;
+        int id = base;
+        while (sb) {
+            const int xs = __builtin_ctzll(sb);
+            sb &= sb - 1;
+            const int xe = sb ? __builtin_ctzll(sb) - 1 : 63;
+            const int fg = (int)((m >> xs) & 1);
+            const int outer = !fg && (x0 + xs == 0 || x0 + xe >= w - 1 || gy == 0 || gy >= h - 1);
+            rx0[id] = (uint8_t)xs;
+            rx1[id] = (uint8_t)xe;
+            rf[id] = (uint8_t)(fg | (outer << 1));
+            par[id] = id;
+            amin[id] = fg ? xs : outer;
+            amax[id] = xe;
+            ay[id] = ln;
+            id++;
+        }
+    }
+    FM_STAMP(4);
+    // Adjacent-row run pairs to union, from the bit masks (no LDS walk): a run B of
+    // row ln+1 touches a contiguous range of same-colour runs of row ln -- window
+    // [b0-1, b1+1] for foreground (8-connected), [b0, b1] for background (4-connected).
+    const uint64_t m2 = __shfl_down(m, 1, 64), s2 = __shfl_down(starts, 1, 64);
+    const int base2 = __shfl_down(base, 1, 64);
+    int npl = 0;
+    // count pass
+    if (ln < 63) {
+        uint64_t sb = s2;
+        while (sb) {
+            const int b0 = __builtin_ctzll(sb);
+            sb &= sb - 1;
+            const int b1 = sb ? __builtin_ctzll(sb) - 1 : 63;
+            const bool fgB = (m2 >> b0) & 1;
+            const int w0 = fgB ? max(b0 - 1, 0) : b0, w1 = fgB ? min(b1 + 1, 63) : b1;
+            const uint64_t win = (w1 == 63 ? ~0ull : ((2ull << w1) - 1)) & ~((1ull << w0) - 1);
+            const uint64_t hits = (fgB ? m : ~m) & win;
+            if (hits) npl += ((run_at(base, starts, 63 - __builtin_clzll(hits)) - run_at(base, starts, __builtin_ctzll(hits))) >> 1) + 1;
+        }
+    }
+    int pin = npl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(pin, o, 64);
+        if (ln >= o) pin += v;
+    }
+    const int np = __shfl(pin, 63, 64);
+    if (np > 2 * CAP) return false;
+    const int pbase = pin - npl;
+    if (ln < 63) {  // write pass
+        uint64_t sb = s2;
+        int id2 = base2;
+        int k = pbase;
+        while (sb) {
+            const int b0 = __builtin_ctzll(sb);
+            sb &= sb - 1;
+            const int b1 = sb ? __builtin_ctzll(sb) - 1 : 63;
+            const bool fgB = (m2 >> b0) & 1;
+            const int w0 = fgB ? max(b0 - 1, 0) : b0, w1 = fgB ? min(b1 + 1, 63) : b1;
+            const uint64_t win = (w1 == 63 ? ~0ull : ((2ull << w1) - 1)) & ~((1ull << w0) - 1);
+            const uint64_t hits = (fgB ? m : ~m) & win;
+            if (hits) {
+                const int ia = run_at(base, starts, __builtin_ctzll(hits));
+                const int ib = run_at(base, starts, 63 - __builtin_clzll(hits));
+                for (int r = ia; r <= ib; r += 2) sc.pairs[k++] = (uint32_t)r | ((uint32_t)id2 << 16);
+            }
+            id2++;
+        }
+    }
+    lds_fence();
+    FM_STAMP(5);
+    // Shiloach-Vishkin style rounds: hook the larger of the two parents under the
+    // smaller (atomicMin, so parents only decrease), then shortcut par[i] = par[par[i]];
+    // at the fixed point every component is a star rooted at its smallest run,
+    // i.e. its raster-first run.
+    for (int round = 0; round < 64; round++) {
+        bool ch = false;
+        for (int p = ln; p < np; p += 64) {
+            const uint32_t pr = sc.pairs[p];
+            const int ra = lload(&par[pr & 0xFFFF]), rb2 = lload(&par[pr >> 16]);
+            if (ra != rb2) {
+                atomicMin(&par[max(ra, rb2)], min(ra, rb2));
+                ch = true;
+            }
+        }
+        lds_fence();
+        for (int i = ln; i < total; i += 64) {
+            const int pi = lload(&par[i]);
+            const int ppi = lload(&par[pi]);
+            if (ppi != pi) {
+                atomicMin(&par[i], ppi);
+                ch = true;
+            }
+        }
+        lds_fence();
+        if (__ballot(ch) == 0) break;
+    }
+    FM_STAMP(6);
+    for (int i = base; i < base + nr; i++) {  // fold into roots (par[] is flat now)
+        const int rt = par[i];
+        if (rt != i) {
+            if (rf[i] & 1) {
+                atomicMin(&amin[rt], (int)rx0[i]);
+                atomicMax(&amax[rt], (int)rx1[i]);
+                atomicMax(&ay[rt], ln);
+            } else if (rf[i] & 2) {
+                atomicOr(&amin[rt], 1);
+            }
+        }
+    }
+    lds_fence();
+    FM_STAMP(7);
+    // ordinals of the roots in raster order
+    int myr = 0;
+    for (int i = base; i < base + nr; i++) myr += (par[i] == i);
+    int rin = myr;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(rin, o, 64);
+        if (ln >= o) rin += v;
+    }
+    if (ln == 63) TR->nroots = rin;
+    {
+        int kk = rin - myr;
+        for (int i = base; i < base + nr; i++)
+            if (par[i] == i) ord[i] = (uint16_t)kk++;
+    }
+    lds_fence();
+    for (int i = base; i < base + nr; i++) {
+        if (par[i] != i) continue;
+        const int fg = rf[i] & 1;
+        NodeRec nrec;
+        nrec.parent = ti * MAXR + ord[i];
+        nrec.key = 0;
+        nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+        if (fg) {
+            const int xs = rx0[i];
+            uint32_t ref;
+            if (x0 + xs == 0) ref = REF_OUTER;
+            else if (xs == 0) ref = REF_EDGE | (uint32_t)ln;
+            else ref = (uint32_t)ord[par[i - 1]];  // the background run left of this run
+            nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
+            nrec.flags = 1u;
+            nrec.minx = x0 + amin[i];
+            nrec.maxx = x0 + amax[i];
+            nrec.maxy = y0 + ay[i];
+        } else {
+            nrec.flags = amin[i] ? 2u : 0u;
+        }
+        NR[ord[i]] = nrec;
+    }
+    const uint64_t mask_c = (2ull << ln) - 1;
+    const uint64_t s0 = __shfl(starts, 0, 64), s63 = __shfl(starts, 63, 64);
+    const uint64_t m0 = __shfl(m, 0, 64), m63 = __shfl(m, 63, 64);
+    const int id0 = rb[0] + __popcll(s0 & mask_c) - 1;
+    const int id63 = rb[63] + __popcll(s63 & mask_c) - 1;
+    TR->edges[ln] = (uint16_t)(ord[par[base]] | ((rf[base] & 1) << 15));
+    TR->edges[64 + ln] = (uint16_t)(ord[par[base + nr - 1]] | ((rf[base + nr - 1] & 1) << 15));
+    TR->edges[128 + ln] = (uint16_t)(ord[par[id0]] | (((m0 >> ln) & 1) << 15));
+    TR->edges[192 + ln] = (uint16_t)(ord[par[id63]] | (((m63 >> ln) & 1) << 15));
+    FM_STAMP(8);
+    return true;
+}
+
+// candidate: the tile's dilated mask can be non-empty.  With threshold bits
+// (dilate) that is: its own bits, or a neighbour's bits within 2 px of the
+// shared edge or corner; with already dilated bits, its own bits.
+__device__ __forceinline__ bool is_candidate(const FusedArgs& a, size_t f, int ti, bool dilate) {
+    const uint32_t* fl = a.tflag + f * a.ntiles;
+    if (fl[ti]) return true;
+    if (!dilate) return false;
+    const int ntx = a.ntx, tx = ti % ntx, ty = ti / ntx;
+    const bool l = tx > 0, r = tx + 1 < ntx, u = ty > 0, d = ty + 1 < a.nty;
+    uint32_t m = 0;
+    if (l) m |= fl[ti - 1] & FLAG_R;
+    if (r) m |= fl[ti + 1] & FLAG_L;
+    if (u) m |= fl[ti - ntx] & FLAG_B;
+    if (d) m |= fl[ti + ntx] & FLAG_T;
+    if (u && l) m |= fl[ti - ntx - 1] & FLAG_BR;
+    if (u && r) m |= fl[ti - ntx + 1] & FLAG_BL;
+    if (d && l) m |= fl[ti + ntx - 1] & FLAG_TR;
+    if (d && r) m |= fl[ti + ntx + 1] & FLAG_TL;
+    return m != 0;
+}
+
+// one workgroup per frame: candidate list, empty-tile regions (4-connected: two
+// empty tiles share a whole background edge), one node per region
+template <bool DILATE>
+__global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
+    __shared__ int uf[MAX_REGION_TILES];
+    __shared__ int s_nc, s_nr;
+    const int f = blockIdx.x;
+    const int nt = a.ntiles, ntx = a.ntx, nty = a.nty;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_nc = s_nr = 0;
+    __syncthreads();
+    for (int t = tid; t < nt; t += RG) {
+        const bool c = is_candidate(a, f, t, DILATE);
+        a.candf[(size_t)f * nt + t] = c ? 1 : 0;
+        uf[t] = c ? -1 : t;
+        if (c) a.clist[(size_t)f * nt + atomicAdd(&s_nc, 1)] = t;
+    }
+    __syncthreads();
+    for (int t = tid; t < nt; t += RG) {
+        if (uf[t] < 0) continue;
+        const int tx = t % ntx;
+        if (tx + 1 < ntx && uf[t + 1] >= 0) lunion(uf, t, t + 1);
+        if (t + ntx < nt && uf[t + ntx] >= 0) lunion(uf, t, t + ntx);
+    }
+    __syncthreads();
+    for (int t = tid; t < nt; t += RG)
+        if (uf[t] >= 0) uf[t] = lfind(uf, t);
+    __syncthreads();
+    // region representative = its smallest tile; "outer" if any tile is on the grid border
+    for (int t = tid; t < nt; t += RG) {
+        const int r = uf[t];
+        if (r < 0) continue;
+        a.regrep[(size_t)f * nt + t] = r;
+        const int tx = t % ntx, ty = t / ntx;
+        NodeRec* rep = a.nodes + (size_t)f * a.nnodes + (size_t)r * MAXR;
+        if (t == r) {
+            rep->parent = r * MAXR;
+            a.rlist[(size_t)f * nt + atomicAdd(&s_nr, 1)] = r;
+        }
+        if (tx == 0 || ty == 0 || tx == ntx - 1 || ty == nty - 1) atomicOr(&rep->flags, 2u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.ncr[2 * f] = s_nc;
+        a.ncr[2 * f + 1] = s_nr;
+    }
+}
+
+// light pass: grid (GW, F); each wave labels candidates of the frame's list with a
+// stride; tiles with too many runs go to the heavy list
+template <bool DILATE>
+__global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
+    __shared__ int par[CW][LIGHT], amin[CW][LIGHT], amax[CW][LIGHT], ay[CW][LIGHT];
+    __shared__ uint8_t rx0[CW][LIGHT], rx1[CW][LIGHT], rf[CW][LIGHT];
+    __shared__ uint16_t ord[CW][LIGHT];
+    __shared__ uint32_t pairs[CW][2 * LIGHT];
+    __shared__ int rb[CW][66];
+    __shared__ uint64_t hv[CW][68];
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    const int nc = a.ncr[2 * f];
+    const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
+    for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
+        const int ti = a.clist[f * a.ntiles + k];
+        FM_STAMP(1);
+        uint64_t m;
+        if (DILATE && !(a.dbg_skip & 128)) {
+            m = dilate_tile(a, f, ti, ln, hv[wv]);
+            a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
+        } else {
+            m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
+        }
+        FM_STAMP(2);
+        if (a.dbg_skip & 64) continue;  // profiling ablation (results invalid)
+        if (!tile_ccl<LIGHT>(a, f, ti, ln, m, sc) && ln == 0) {
+            const int slot = atomicAdd(&a.count[2 * F], 1);
+            a.heavy[slot] = (int)(f * a.ntiles + ti);
+        }
+    }
+}
+
+// heavy pass: persistent workgroups drain the work list with full-size LDS
+__global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
+    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
+    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
+    __shared__ uint16_t ord[MAXR];
+    __shared__ uint32_t pairs[2 * MAXR];
+    __shared__ int rb[66];
+    const size_t F = (size_t)a.T * a.S;
+    const int n = a.count[2 * F];
+    const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int item = a.heavy[i];
+        const size_t f = item / a.ntiles;
+        const int ti = (int)(item - (long long)f * a.ntiles);
+        if (!tile_ccl<MAXR>(a, f, ti, threadIdx.x, a.dbits[(f * a.ntiles + ti) * 64 + threadIdx.x], sc) &&
+            threadIdx.x == 0)
+            a.count[F + f] = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
+__device__ __forceinline__ int enode(int tile, uint16_t e) { return tile * MAXR + (e & 0x7FFF); }
+
+// Background component `nd` of a candidate touches empty region `rep`.  An outer
+// region only contributes its outer-ness, so the node is marked directly (no union:
+// every candidate around a moving object borders the big outer background, and
+// unions into that one root serialise on its atomics); an enclosed region is unioned.
+__device__ __forceinline__ void touch_region(NodeRec* N, int nd, int rep) {
+    if (N[rep * MAXR].flags & 2) atomicOr(&N[nd].flags, 2u);
+    else gunion(N, nd, rep * MAXR);
+}
+
+// one wave per candidate, lane = edge position
+__global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.count[F + f]) return;
+    const int ntx = a.ntx, nt = a.ntiles;
+    const uint8_t* cf = a.candf + f * nt;
+    const int32_t* rr = a.regrep + f * nt;
+    const TileRec* TR = a.tiles + f * nt;
+    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    const int nc = a.ncr[2 * f];
+    for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
+        const int t = a.clist[f * nt + k];
+        const int tx = t % ntx, ty = t / ntx;
+        const bool hasR = tx + 1 < ntx, hasD = ty + 1 < a.nty;
+        // right edge
+        if (hasR) {
+            const uint16_t A = TR[t].edges[64 + ln];
+            const int Ap = __shfl_up((int)A, 1, 64);
+            if (cf[t + 1]) {
+                const uint16_t B = TR[t + 1].edges[ln];
+                const int Bp = __shfl_up((int)B, 1, 64);
+                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(t, A), enode(t + 1, B));
+                if (efg(A)) {
+                    if (ln > 0) {
+                        const uint16_t Bu = TR[t + 1].edges[ln - 1];
+                        if (efg(Bu) && Bu != B) gunion(N, enode(t, A), enode(t + 1, Bu));
+                    }
+                    if (ln < 63) {
+                        const uint16_t Bd = TR[t + 1].edges[ln + 1];
+                        if (efg(Bd) && Bd != B) gunion(N, enode(t, A), enode(t + 1, Bd));
+                    }
+                }
+            } else if (!efg(A) && !(ln > 0 && Ap == A)) {
+                touch_region(N, enode(t, A), rr[t + 1]);
+            }
+        }
+        // bottom edge
+        if (hasD) {
+            const int n = t + ntx;
+            const uint16_t A = TR[t].edges[192 + ln];
+            const int Ap = __shfl_up((int)A, 1, 64);
+            if (cf[n]) {
+                const uint16_t B = TR[n].edges[128 + ln];
+                const int Bp = __shfl_up((int)B, 1, 64);
+                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(t, A), enode(n, B));
+                if (efg(A)) {
+                    if (ln > 0) {
+                        const uint16_t Bl = TR[n].edges[128 + ln - 1];
+                        if (efg(Bl) && Bl != B) gunion(N, enode(t, A), enode(n, Bl));
+                    }
+                    if (ln < 63) {
+                        const uint16_t Br = TR[n].edges[128 + ln + 1];
+                        if (efg(Br) && Br != B) gunion(N, enode(t, A), enode(n, Br));
+                    }
+                }
+            } else if (!efg(A) && !(ln > 0 && Ap == A)) {
+                touch_region(N, enode(t, A), rr[n]);
+            }
+            // corner diagonals (foreground only: both tiles candidates)
+            if (ln == 0 && hasR && cf[n + 1]) {  // (63,63) <-> (0,0) of the down-right tile
+                const uint16_t P = TR[t].edges[192 + 63], Q = TR[n + 1].edges[128];
+                if (efg(P) && efg(Q)) gunion(N, enode(t, P), enode(n + 1, Q));
+            }
+            if (ln == 0 && tx > 0 && cf[n - 1]) {  // (0,63) <-> (63,0) of the down-left tile
+                const uint16_t P = TR[t].edges[192], Q = TR[n - 1].edges[128 + 63];
+                if (efg(P) && efg(Q)) gunion(N, enode(t, P), enode(n - 1, Q));
+            }
+        }
+        // left / top edges against empty regions (candidate pairs are done by the neighbour)
+        if (tx > 0 && !cf[t - 1]) {
+            const uint16_t A = TR[t].edges[ln];
+            const int Ap = __shfl_up((int)A, 1, 64);
+            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(t, A), rr[t - 1]);
+        }
+        if (ty > 0 && !cf[t - ntx]) {
+            const uint16_t A = TR[t].edges[128 + ln];
+            const int Ap = __shfl_up((int)A, 1, 64);
+            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(t, A), rr[t - ntx]);
+        }
+    }
+}
+
+__device__ __forceinline__ void fold_node(NodeRec* N, int n) {
+    const int rt = gfind(N, n);
+    if (rt == n) return;
+    N[n].parent = rt;
+    const uint32_t fl = N[n].flags;
+    if (fl & 1) {
+        atomicMin((unsigned long long*)&N[rt].key, (unsigned long long)N[n].key);
+        atomicMin(&N[rt].minx, N[n].minx);
+        atomicMax(&N[rt].maxx, N[n].maxx);
+        atomicMax(&N[rt].maxy, N[n].maxy);
+    } else if (fl & 2) {
+        atomicOr(&N[rt].flags, 2u);
+    }
+}
+
+// one workgroup per frame: (1) path compression with outer flags, bboxes and first
+// pixels folded into the roots, one thread per candidate tile (all its nodes) or
+// enclosed empty region; (2) after a workgroup barrier, the external test at every
+// foreground root and the contour records.
+constexpr int FT = 256;
+__global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
+    const size_t f = blockIdx.x;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.count[F + f]) return;
+    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    const TileRec* TRf = a.tiles + f * a.ntiles;
+    const uint8_t* cf = a.candf + f * a.ntiles;
+    const int32_t* rr = a.regrep + f * a.ntiles;
+    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
+    for (int i = threadIdx.x; i < nc + nr; i += FT) {
+        if (i < nc) {
+            const int t = a.clist[f * a.ntiles + i];
+            const int k1 = TRf[t].nroots;
+            for (int k = 0; k < k1; k++) fold_node(N, t * MAXR + k);
+        } else {
+            fold_node(N, a.rlist[f * a.ntiles + (i - nc)] * MAXR);
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    for (int i = threadIdx.x; i < nc; i += FT) {
+        const int t = a.clist[f * a.ntiles + i];
+        const int k1 = TRf[t].nroots;
+        for (int k = 0; k < k1; k++) {
+            const int n = t * MAXR + k;
+            // fields other workgroups' threads folded into are read past the L1
+            const int par = __hip_atomic_load(&N[n].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t fl = __hip_atomic_load(&N[n].flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (par != n || !(fl & 1)) continue;
+            const uint64_t key = __hip_atomic_load((unsigned long long*)&N[n].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t first = (uint32_t)(key >> 32), ref = (uint32_t)key;
+            const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
+            bool ext;
+            if (ref & REF_OUTER) {
+                ext = true;
+            } else {
+                const int tf = (fy / TS) * a.ntx + fx / TS;  // tile of the raster-first pixel (a candidate)
+                int bn;
+                if (ref & REF_EDGE) {
+                    const int lt = tf - 1;
+                    bn = cf[lt] ? enode(lt, TRf[lt].edges[64 + (ref & 63)]) : rr[lt] * MAXR;
+                } else {
+                    bn = tf * MAXR + (int)ref;
+                }
+                const int br = __hip_atomic_load(&N[bn].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ext = (__hip_atomic_load(&N[br].flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) != 0;
+            }
+            if (!ext) continue;
+            const int id = atomicAdd(&a.count[f], 1);
+            if (id < a.cap) {
+                int32_t* rec = a.rec + (f * a.cap + id) * 5;
+                rec[0] = (int32_t)first;
+                rec[1] = __hip_atomic_load(&N[n].minx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rec[2] = fy;
+                rec[3] = __hip_atomic_load(&N[n].maxx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rec[4] = __hip_atomic_load(&N[n].maxy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// one thread per 8 mask bytes of one frame; non-candidate tiles are empty
+__global__ __launch_bounds__(256) void k_expand_bits(const uint64_t* __restrict__ dbits, const uint8_t* __restrict__ candf,
+                                                     uint8_t* __restrict__ out, int h, int w, int ntx) {
+    const int x8 = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    const int xs = 8 * x8;
+    if (xs >= w) return;
+    const int tx = xs >> 6, ty = y >> 6;
+    const int ti = ty * ntx + tx;
+    const uint64_t row = candf[ti] ? dbits[(size_t)ti * 64 + (y & 63)] : 0ull;
+    const uint32_t b = (uint32_t)(row >> (xs & 63)) & 0xFFu;
+    uint8_t* dst = out + (size_t)y * w + xs;
+    for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = ((b >> i) & 1) ? 255 : 0;
+}
+
+}  // namespace cc
+
+hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
+    if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;
+    const unsigned F = (unsigned)(a.T * a.S);
+    const dim3 gf(cc::GW, F);
+    int tok = tm ? tm->begin("regions", st) : -1;
+    if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), 0, st, a);
+    else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), 0, st, a);
+    if (tm) tm->end(tok);
+    tok = tm ? tm->begin("tile_ccl", st) : -1;
+    if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), 0, st, a);
+    else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), 0, st, a);
+    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(64), dim3(64), 0, st, a);
+    if (tm) tm->end(tok);
+    tok = tm ? tm->begin("merge", st) : -1;
+    hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
+    if (tm) tm->end(tok);
+    tok = tm ? tm->begin("fold_emit", st) : -1;
+    hipLaunchKernelGGL(cc::k_fold_emit, dim3(F), dim3(cc::FT), 0, st, a);
+    if (tm) tm->end(tok);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, uint8_t* out, int h, int w,
+                              int ntx) {
+    dim3 grid((unsigned)(((w + 7) / 8 + 255) / 256), (unsigned)h);
+    hipLaunchKernelGGL(cc::k_expand_bits, grid, dim3(256), 0, st, dbits, candf, out, h, w, ntx);
+    return hipGetLastError();
+}
+
+
+
+}  // namespace fm

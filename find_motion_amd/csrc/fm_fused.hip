@@ -515,6 +515,7 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
             if (y0 + ln >= h) o = 0;
             Ob[ln] = o;
             a.dbits[(f * a.ntiles + ti) * 64 + ln] = o;
+            if (__ballot(o != 0) != 0 && ln == 0) a.tflag[f * a.ntiles + ti] = FLAG_ANY;
         }
         lds_barrier();
 
@@ -529,375 +530,6 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
     }
 }
 
-
-// ---------------------------------------------------------------------------
-// Run-length CCL of one dilated 64x64 tile (one wave, lane = tile row).
-// Runs are numbered in raster order; union-find over runs links the larger
-// root under the smaller, so a root is its component's raster-first run.
-// Foreground runs of adjacent rows connect 8-wise (x ranges within 1),
-// background runs 4-wise (x ranges overlap).  Out-of-image pixels are
-// background and, like pixels on the image border, mark their background
-// component "outer" (they play the role of findContours' 1-px zero pad).
-struct CclScratch {
-    int* par;
-    int* amin;  // fg root: min x0; bg root: outer flag
-    int* amax;
-    int* ay;
-    uint8_t *rx0, *rx1, *rf;
-    int* rb;
-};
-
-// returns false (nothing written) if the tile has more than CAP runs
-template <int CAP>
-__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const CclScratch& sc) {
-    int* par = sc.par;
-    int* amin = sc.amin;
-    int* amax = sc.amax;
-    int* ay = sc.ay;
-    uint8_t* rx0 = sc.rx0;
-    uint8_t* rx1 = sc.rx1;
-    uint8_t* rf = sc.rf;
-    int* rb = sc.rb;
-    const size_t F = (size_t)a.T * a.S;
-    const int h = a.h, w = a.w;
-    const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
-    TileRec* TR = a.tiles + f * a.ntiles + ti;
-    NodeRec* NR = a.nodes + f * (size_t)a.nnodes + (size_t)ti * MAXR;
-
-    if (__ballot(m != 0) == 0) {  // empty tile: one background component (run 0)
-        TR->edges[ln] = 0;
-        TR->edges[64 + ln] = 0;
-        TR->edges[128 + ln] = 0;
-        TR->edges[192 + ln] = 0;
-        if (ln == 0) {
-            TR->nroots = 1;
-            TR->roots[0] = 0;
-            const bool outer = x0 == 0 || y0 == 0 || x0 + TS - 1 >= w - 1 || y0 + TS - 1 >= h - 1;
-            NodeRec nrec;
-            nrec.key = 0;
-            nrec.parent = ti * MAXR;
-            nrec.flags = outer ? 2u : 0u;
-            nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
-            NR[0] = nrec;
-        }
-        return true;
-    }
-
-    const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
-    const int nr = __popcll(starts);
-    int incl = nr;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (ln >= o) incl += v;
-    }
-    const int total = __shfl(incl, 63, 64);
-    const int base = incl - nr;
-    if (total > CAP) {
-        if (CAP >= MAXR && ln == 0) {  // impossible for a dilated mask (<= 24 runs per row); host relabels the frame
-            TR->nroots = 0;
-            atomicOr(&a.count[F + f], 1);
-        }
-        return CAP >= MAXR;
-    }
-    rb[ln] = base;
-    if (ln == 63) rb[64] = total;
-    const int gy = y0 + ln;
-    {
-        uint64_t sb = starts;
-        int id = base;
-        while (sb) {
-            const int xs = __builtin_ctzll(sb);
-            sb &= sb - 1;
-            const int xe = sb ? __builtin_ctzll(sb) - 1 : 63;
-            const int fg = (int)((m >> xs) & 1);
-            const int outer = !fg && (x0 + xs == 0 || x0 + xe >= w - 1 || gy == 0 || gy >= h - 1);
-            rx0[id] = (uint8_t)xs;
-            rx1[id] = (uint8_t)xe;
-            rf[id] = (uint8_t)(fg | (outer << 1));
-            par[id] = id;
-            amin[id] = fg ? xs : outer;
-            amax[id] = xe;
-            ay[id] = ln;
-            id++;
-        }
-    }
-    lds_fence();
-    if (ln < 63) {  // union the runs of row ln with those of row ln+1
-        int j = rb[ln + 1];
-        const int jend = rb[ln + 2];
-        for (int i = base; i < base + nr; i++) {
-            const int fgi = rf[i] & 1;
-            const int lo = (int)rx0[i] - fgi, hi2 = (int)rx1[i] + fgi;
-            while (j < jend && (int)rx1[j] < lo) j++;
-            for (int kk = j; kk < jend && (int)rx0[kk] <= hi2; kk++)
-                if ((rf[kk] & 1) == fgi) lunion(par, i, kk);
-        }
-    }
-    lds_fence();
-    for (int i = base; i < base + nr; i++) {  // flatten + fold into roots
-        const int rt = lfind(par, i);
-        if (rt != i) {
-            par[i] = rt;
-            if (rf[i] & 1) {
-                atomicMin(&amin[rt], (int)rx0[i]);
-                atomicMax(&amax[rt], (int)rx1[i]);
-                atomicMax(&ay[rt], ln);
-            } else if (rf[i] & 2) {
-                atomicOr(&amin[rt], 1);
-            }
-        }
-    }
-    lds_fence();
-    int myr = 0;
-    for (int i = base; i < base + nr; i++) myr += (par[i] == i);
-    int rin = myr;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(rin, o, 64);
-        if (ln >= o) rin += v;
-    }
-    if (ln == 63) TR->nroots = rin;
-    int kk = rin - myr;
-    for (int i = base; i < base + nr; i++) {
-        if (par[i] != i) continue;
-        TR->roots[kk++] = (uint16_t)i;
-        const int fg = rf[i] & 1;
-        NodeRec nrec;
-        nrec.parent = ti * MAXR + i;
-        nrec.key = 0;
-        nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
-        if (fg) {
-            const int xs = rx0[i];
-            uint32_t ref;
-            if (x0 + xs == 0) ref = REF_OUTER;
-            else if (xs == 0) ref = REF_EDGE | (uint32_t)ln;
-            else ref = (uint32_t)par[i - 1];  // the background run left of this run, flattened
-            nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
-            nrec.flags = 1u;
-            nrec.minx = x0 + amin[i];
-            nrec.maxx = x0 + amax[i];
-            nrec.maxy = y0 + ay[i];
-        } else {
-            nrec.flags = amin[i] ? 2u : 0u;
-        }
-        NR[i] = nrec;
-    }
-    const uint64_t mask_c = (2ull << ln) - 1;
-    const uint64_t s0 = __shfl(starts, 0, 64), s63 = __shfl(starts, 63, 64);
-    const uint64_t m0 = __shfl(m, 0, 64), m63 = __shfl(m, 63, 64);
-    const int id0 = rb[0] + __popcll(s0 & mask_c) - 1;
-    const int id63 = rb[63] + __popcll(s63 & mask_c) - 1;
-    TR->edges[ln] = (uint16_t)(par[base] | ((rf[base] & 1) << 15));
-    TR->edges[64 + ln] = (uint16_t)(par[base + nr - 1] | ((rf[base + nr - 1] & 1) << 15));
-    TR->edges[128 + ln] = (uint16_t)(par[id0] | (((m0 >> ln) & 1) << 15));
-    TR->edges[192 + ln] = (uint16_t)(par[id63] | (((m63 >> ln) & 1) << 15));
-    return true;
-}
-
-constexpr int LIGHT_RUNS = 256;   // most tiles: empty or a few blobs
-constexpr int CCL_WAVES = 4;
-
-// 5x5 dilation (dilate(thresh, None, iterations=2), fm.py:266) of one tile's
-// threshold bit rows, lane = row: the 68-bit row (2 columns of each side
-// neighbour) is ORed over 5 shifts, then over 5 rows through LDS (2 halo rows
-// from the tiles above and below).  Out-of-image pixels are 0 in the input and
-// cleared in the output.
-__device__ __forceinline__ uint64_t hdil(uint64_t L, uint64_t C, uint64_t R) {
-    const uint64_t lo = (L >> 62) | (C << 2), hi = (C >> 62) | ((R & 3) << 2);
-    return lo | ((lo >> 1) | (hi << 63)) | ((lo >> 2) | (hi << 62)) | ((lo >> 3) | (hi << 61)) | ((lo >> 4) | (hi << 60));
-}
-
-__device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, int ti, int ln, uint64_t* hv) {
-    const int tx = ti % a.ntx, ty = ti / a.ntx;
-    const uint64_t* B = a.bits + f * (size_t)a.ntiles * 64;
-    auto row = [&](int t, int r) -> uint64_t { return B[(size_t)t * 64 + r]; };
-    const bool hl = tx > 0, hr = tx + 1 < a.ntx;
-    hv[ln + 2] = hdil(hl ? row(ti - 1, ln) : 0, row(ti, ln), hr ? row(ti + 1, ln) : 0);
-    if (ln < 4) {  // halo rows -2, -1 (tile above, rows 62, 63) and 64, 65 (tile below, rows 0, 1)
-        const int dy = ln < 2 ? -1 : 1;
-        const int rr = ln < 2 ? 62 + ln : ln - 2;
-        const int tyy = ty + dy;
-        uint64_t v = 0;
-        if (tyy >= 0 && tyy < a.nty) {
-            const int tt = tyy * a.ntx + tx;
-            v = hdil(hl ? row(tt - 1, rr) : 0, row(tt, rr), hr ? row(tt + 1, rr) : 0);
-        }
-        hv[ln < 2 ? ln : 64 + ln] = v;
-    }
-    lds_fence();
-    uint64_t o = hv[ln] | hv[ln + 1] | hv[ln + 2] | hv[ln + 3] | hv[ln + 4];
-    const int x0 = tx * TS, y0 = ty * TS;
-    const int vc = a.w - x0;
-    if (vc < 64) o &= (1ull << vc) - 1;
-    if (y0 + ln >= a.h) o = 0;
-    return o;
-}
-
-// light pass: one wave per tile, 4 tiles per workgroup, small LDS; tiles with
-// more runs are appended to a work list for the heavy pass
-template <bool DILATE>
-__global__ __launch_bounds__(64 * CCL_WAVES) void k_tile_ccl(FusedArgs a) {
-    __shared__ int par[CCL_WAVES][LIGHT_RUNS], amin[CCL_WAVES][LIGHT_RUNS], amax[CCL_WAVES][LIGHT_RUNS],
-        ay[CCL_WAVES][LIGHT_RUNS];
-    __shared__ uint8_t rx0[CCL_WAVES][LIGHT_RUNS], rx1[CCL_WAVES][LIGHT_RUNS], rf[CCL_WAVES][LIGHT_RUNS];
-    __shared__ int rb[CCL_WAVES][66];
-    __shared__ uint64_t hv[CCL_WAVES][68];
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const long long item = (long long)blockIdx.x * CCL_WAVES + wv;
-    const long long nitems = (long long)a.T * a.S * a.ntiles;
-    if (item >= nitems) return;
-    const size_t f = item / a.ntiles;
-    const int ti = (int)(item - (long long)f * a.ntiles);
-    uint64_t m;
-    if (DILATE) {
-        m = dilate_tile(a, f, ti, ln, hv[wv]);
-        a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
-    } else {
-        m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
-    }
-    CclScratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv]};
-    if (!tile_ccl<LIGHT_RUNS>(a, f, ti, ln, m, sc) && ln == 0) {
-        const size_t F = (size_t)a.T * a.S;
-        const int slot = atomicAdd(&a.count[2 * F], 1);
-        a.heavy[slot] = (int)item;
-    }
-}
-
-// heavy pass: persistent workgroups drain the work list with full-size LDS
-__global__ __launch_bounds__(64) void k_tile_ccl_heavy(FusedArgs a) {
-    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
-    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
-    __shared__ int rb[66];
-    const size_t F = (size_t)a.T * a.S;
-    const int n = a.count[2 * F];
-    CclScratch sc{par, amin, amax, ay, rx0, rx1, rf, rb};
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int item = a.heavy[i];
-        const size_t f = item / a.ntiles;
-        const int ti = (int)(item - (long long)f * a.ntiles);
-        tile_ccl<MAXR>(a, f, ti, threadIdx.x, a.dbits[(f * a.ntiles + ti) * 64 + threadIdx.x], sc);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Global merge of tile records
-__device__ __forceinline__ int enode(int tile, uint16_t e) { return tile * MAXR + (e & 0x7FFF); }
-__device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
-
-__global__ __launch_bounds__(64) void k_tile_merge(FusedArgs a) {
-    const size_t f = blockIdx.y;
-    const size_t F = (size_t)a.T * a.S;
-    const int ti = blockIdx.x, ln = threadIdx.x;
-    const int tx = ti % a.ntx, ty = ti / a.ntx;
-    if (a.count[F + f]) return;
-    const TileRec* TR = a.tiles + f * a.ntiles;
-    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
-    if (tx + 1 < a.ntx) {  // vertical boundary with the right tile
-        const int tb = ti + 1;
-        const uint16_t A = TR[ti].edges[64 + ln], B = TR[tb].edges[ln];
-        const int Ap = __shfl_up((int)A, 1, 64), Bp = __shfl_up((int)B, 1, 64);
-        if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(ti, A), enode(tb, B));
-        if (efg(A)) {
-            if (ln > 0) {
-                const uint16_t Bu = TR[tb].edges[ln - 1];
-                if (efg(Bu) && Bu != B) gunion(N, enode(ti, A), enode(tb, Bu));
-            }
-            if (ln < 63) {
-                const uint16_t Bd = TR[tb].edges[ln + 1];
-                if (efg(Bd) && Bd != B) gunion(N, enode(ti, A), enode(tb, Bd));
-            }
-        }
-    }
-    if (ty + 1 < a.nty) {  // horizontal boundary with the tile below
-        const int tb = ti + a.ntx;
-        const uint16_t A = TR[ti].edges[192 + ln], B = TR[tb].edges[128 + ln];
-        const int Ap = __shfl_up((int)A, 1, 64), Bp = __shfl_up((int)B, 1, 64);
-        if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(ti, A), enode(tb, B));
-        if (efg(A)) {
-            if (ln > 0) {
-                const uint16_t Bl = TR[tb].edges[128 + ln - 1];
-                if (efg(Bl) && Bl != B) gunion(N, enode(ti, A), enode(tb, Bl));
-            }
-            if (ln < 63) {
-                const uint16_t Br = TR[tb].edges[128 + ln + 1];
-                if (efg(Br) && Br != B) gunion(N, enode(ti, A), enode(tb, Br));
-            }
-        }
-        if (ln == 0 && tx + 1 < a.ntx) {  // (63,63) <-> (0,0) of the down-right tile
-            const uint16_t P = TR[ti].edges[192 + 63], Q = TR[tb + 1].edges[128];
-            if (efg(P) && efg(Q)) gunion(N, enode(ti, P), enode(tb + 1, Q));
-        }
-        if (ln == 0 && tx > 0) {  // (0,63) <-> (63,0) of the down-left tile
-            const uint16_t P = TR[ti].edges[192], Q = TR[tb - 1].edges[128 + 63];
-            if (efg(P) && efg(Q)) gunion(N, enode(ti, P), enode(tb - 1, Q));
-        }
-    }
-}
-
-// fold every non-root node into its root: bbox / raster-first key (fg), outer flag (bg)
-__global__ __launch_bounds__(64) void k_tile_resolve1(FusedArgs a) {
-    const size_t f = blockIdx.y;
-    const size_t F = (size_t)a.T * a.S;
-    const int ti = blockIdx.x;
-    if (a.count[F + f]) return;
-    const TileRec* TR = a.tiles + f * a.ntiles + ti;
-    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
-    const int nr = TR->nroots;
-    for (int kx = threadIdx.x; kx < nr; kx += 64) {
-        const int n = ti * MAXR + TR->roots[kx];
-        const int rt = gfind(N, n);
-        if (rt == n) continue;
-        N[n].parent = rt;
-        const uint32_t fl = N[n].flags;
-        if (fl & 1) {
-            atomicMin((unsigned long long*)&N[rt].key, (unsigned long long)N[n].key);
-            atomicMin(&N[rt].minx, N[n].minx);
-            atomicMax(&N[rt].maxx, N[n].maxx);
-            atomicMax(&N[rt].maxy, N[n].maxy);
-        } else if (fl & 2) {
-            atomicOr(&N[rt].flags, 2u);
-        }
-    }
-}
-
-// external test at every foreground root; emit contour records
-__global__ __launch_bounds__(64) void k_tile_resolve2(FusedArgs a) {
-    const size_t f = blockIdx.y;
-    const size_t F = (size_t)a.T * a.S;
-    const int ti = blockIdx.x;
-    if (a.count[F + f]) return;
-    const TileRec* TRf = a.tiles + f * a.ntiles;
-    const TileRec* TR = TRf + ti;
-    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
-    const int nr = TR->nroots;
-    for (int kx = threadIdx.x; kx < nr; kx += 64) {
-        const int n = ti * MAXR + TR->roots[kx];
-        const NodeRec nd = N[n];
-        if (nd.parent != n || !(nd.flags & 1)) continue;
-        const uint32_t first = (uint32_t)(nd.key >> 32), ref = (uint32_t)nd.key;
-        const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
-        bool ext;
-        if (ref & REF_OUTER) {
-            ext = true;
-        } else {
-            const int tfirst = (fy / TS) * a.ntx + fx / TS;
-            const int bn = (ref & REF_EDGE) ? enode(tfirst - 1, TRf[tfirst - 1].edges[64 + (ref & 63)])
-                                            : tfirst * MAXR + (int)ref;
-            ext = (N[N[bn].parent].flags & 2) != 0;
-        }
-        if (!ext) continue;
-        const int id = atomicAdd(&a.count[f], 1);
-        if (id < a.cap) {
-            int32_t* rr = a.rec + (f * a.cap + id) * 5;
-            rr[0] = (int32_t)first;
-            rr[1] = nd.minx;
-            rr[2] = fy;
-            rr[3] = nd.maxx;
-            rr[4] = nd.maxy;
-        }
-    }
-}
 
 }  // namespace fz
 
@@ -917,51 +549,6 @@ hipError_t launch_fused(hipStream_t st, const FusedArgs& a, KernelTimer* tm) {
         hipLaunchKernelGGL(fz::k_fused<0>, grid, dim3(fz::NT), bytes, st, a);
     }
     if (tm) tm->end(tok);
-    return hipGetLastError();
-}
-
-hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
-    hipError_t e;
-    dim3 gm(a.ntiles, a.T * a.S);
-    int tok = tm ? tm->begin("tile_ccl", st) : -1;
-    const long long items = (long long)a.T * a.S * a.ntiles;
-    const dim3 gl((unsigned)((items + fz::CCL_WAVES - 1) / fz::CCL_WAVES));
-    if (dilate) hipLaunchKernelGGL(fz::k_tile_ccl<true>, gl, dim3(64 * fz::CCL_WAVES), 0, st, a);
-    else hipLaunchKernelGGL(fz::k_tile_ccl<false>, gl, dim3(64 * fz::CCL_WAVES), 0, st, a);
-    hipLaunchKernelGGL(fz::k_tile_ccl_heavy, dim3(512), dim3(64), 0, st, a);
-    if (tm) tm->end(tok);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_merge", st) : -1;
-    hipLaunchKernelGGL(fz::k_tile_merge, gm, dim3(64), 0, st, a);
-    if (tm) tm->end(tok);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_resolve1", st) : -1;
-    hipLaunchKernelGGL(fz::k_tile_resolve1, gm, dim3(64), 0, st, a);
-    if (tm) tm->end(tok);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    tok = tm ? tm->begin("tile_resolve2", st) : -1;
-    hipLaunchKernelGGL(fz::k_tile_resolve2, gm, dim3(64), 0, st, a);
-    if (tm) tm->end(tok);
-    return hipGetLastError();
-}
-
-// one thread per 8 mask bytes of one frame
-__global__ __launch_bounds__(256) void k_expand_bits(const uint64_t* __restrict__ dbits, uint8_t* __restrict__ out, int h,
-                                                     int w, int ntx) {
-    const int x8 = blockIdx.x * 256 + threadIdx.x;
-    const int y = blockIdx.y;
-    const int xs = 8 * x8;
-    if (xs >= w) return;
-    const int tx = xs >> 6, ty = y >> 6;
-    const uint64_t row = dbits[((size_t)ty * ntx + tx) * 64 + (y & 63)];
-    const uint32_t b = (uint32_t)(row >> (xs & 63)) & 0xFFu;
-    uint8_t* dst = out + (size_t)y * w + xs;
-    for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = ((b >> i) & 1) ? 255 : 0;
-}
-
-hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, uint8_t* out, int h, int w, int ntx, int) {
-    dim3 grid((unsigned)(((w + 7) / 8 + 255) / 256), (unsigned)h);
-    hipLaunchKernelGGL(k_expand_bits, grid, dim3(256), 0, st, dbits, out, h, w, ntx);
     return hipGetLastError();
 }
 

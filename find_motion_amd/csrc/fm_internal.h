@@ -64,9 +64,16 @@ struct NodeRec {
     int32_t minx, maxx, maxy, pad;
 };
 struct TileRec {
-    int32_t nroots, pad[3];
-    uint16_t edges[256];              // 0..63 left col, 64.. right col, 128.. top row, 192.. bottom row; bit15 = fg
-    uint16_t roots[kTileMaxRuns];     // local ids of the tile's components
+    int32_t nroots, pad[3];           // components of the tile (ordinals 0..nroots-1, raster order)
+    uint16_t edges[256];              // 0..63 left col, 64.. right col, 128.. top row, 192.. bottom row:
+                                      // component ordinal | fg << 15
+};
+
+// per-tile threshold-bit flags written by the pixel kernel (decide which tiles the
+// 5x5 dilation can make non-empty: the tile itself or a neighbour's 2-px margin)
+enum : uint32_t {
+    FLAG_ANY = 1u, FLAG_L = 2u, FLAG_R = 4u, FLAG_T = 8u, FLAG_B = 16u,
+    FLAG_TL = 32u, FLAG_TR = 64u, FLAG_BL = 128u, FLAG_BR = 256u,
 };
 
 struct FusedArgs {
@@ -82,6 +89,13 @@ struct FusedArgs {
     uint64_t* dbits;             // [F][ntiles][64] dilated rows (VideoFrame.thresh as bits; == bits when the
                                  // pixel kernel dilates itself, i.e. the generic-k k_fused path)
     TileRec* tiles;              // [F][ntiles]
+    uint32_t* tflag;             // [F][ntiles] FLAG_* bits: where the tile has threshold bits (dilated
+                                 // bits on the k_fused path, which sets FLAG_ANY only)
+    uint8_t* candf;              // [F][ntiles] 1: the tile's dilated mask may be non-empty (labelled)
+    int32_t* clist;              // [F][ntiles] candidate tiles of each frame
+    int32_t* rlist;              // [F][ntiles] representative tile of each empty-tile region
+    int32_t* regrep;             // [F][ntiles] empty tile -> its region's representative tile
+    int32_t* ncr;                // [F][2] candidates, regions
     NodeRec* nodes;              // [F][nnodes]
     int32_t* count;              // [2F+1]: [f] external contours, [F+f] overflow flag, [2F] heavy-tile count
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
@@ -90,6 +104,7 @@ struct FusedArgs {
     int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
+    uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
     double alpha, beta;
     long long acc_vec_end;
     int32_t coef[kMaxK];
@@ -115,8 +130,9 @@ int pix_lds_bytes(int ksize);
 bool pix_supported(int ksize);
 // CCL over tile summaries; dilate = true: a.bits are threshold rows to dilate into a.dbits
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer);
-// dilated bit rows of one frame -> mask bytes (VideoFrame.thresh) [h][w]
-hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, uint8_t* out, int h, int w, int ntx, int ntiles);
+// dilated bit rows of one frame -> mask bytes (VideoFrame.thresh) [h][w]; non-candidate tiles are 0
+hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, uint8_t* out, int h, int w,
+                              int ntx);
 
 // Optional per-kernel event timing (FM_FLAG_PROFILE): events are recorded on
 // the launch stream around each kernel and read back after the stream syncs.

@@ -442,6 +442,20 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
         chain_rows<KC, PLANES, INIT>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf, init0 && t == t0,
                                      mybits);
         if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
+        {   // where the tile has threshold bits (decides the contour pass's candidate tiles)
+            uint32_t fl = 0;
+            if (ln < RPWV && mybits) {
+                const int row = RPWV * wv + ln;
+                const bool l = (mybits & 3ull) != 0, r = (mybits >> 62) != 0;
+                fl = FLAG_ANY | (l ? FLAG_L : 0u) | (r ? FLAG_R : 0u);
+                if (row < 2) fl |= FLAG_T | (l ? FLAG_TL : 0u) | (r ? FLAG_TR : 0u);
+                if (row >= TS - 2) fl |= FLAG_B | (l ? FLAG_BL : 0u) | (r ? FLAG_BR : 0u);
+            }
+            fl |= __shfl_xor(fl, 1, 64);
+            fl |= __shfl_xor(fl, 2, 64);
+            fl |= __shfl_xor(fl, 4, 64);
+            if (ln == 0 && fl) atomicOr(&a.tflag[f * a.ntiles + ti], fl);
+        }
 
         if (t + 1 < t1)
             gray_stage(raw + (b ^ 1) * g.raw_bytes, roff + (b ^ 1) * (g.roff_bytes / 4), Hs + (b ^ 1) * (g.H_bytes / 2),

@@ -93,14 +93,20 @@ int fm_set_mask(fm_ctx* ctx, int stream, const uint8_t* keep_hw);
  * (VideoMotion.ref_frame = None, fm.py:414, 651-652). */
 int fm_reset_stream(fm_ctx* ctx, int stream);
 
+/* Batches that may be in flight at once (fm_submit before fm_wait): the contour
+ * pass of one batch overlaps the pixel kernel of the next ones. */
+int fm_max_inflight(const fm_ctx* ctx);
+
 /* Run the hot path on n_frames consecutive frames of every stream.
  * frames: BGR u8, layout [n_frames][n_streams][src_h][src_w][3], C-contiguous;
  * host memory (on_device = 0, copied with hipMemcpyAsync) or device memory
  * (on_device = 1, read in place).  Asynchronous: host buffers must stay valid
- * until fm_wait returns. */
+ * until fm_wait returns for this batch.  Up to fm_max_inflight() batches may be
+ * submitted before waiting; fm_wait completes them in submission order. */
 int fm_submit(fm_ctx* ctx, const uint8_t* frames, int n_frames, int on_device);
 
-/* Wait for the last submit; makes its results readable. */
+/* Wait for the oldest batch in flight; makes its results readable (device-side
+ * results -- masks, planes -- until that batch's slot is reused by a later submit). */
 int fm_wait(fm_ctx* ctx);
 
 /* External-contour counts of the last batch, layout [n_frames][n_streams]

@@ -264,22 +264,24 @@ def test_batch_split_and_tail_geometries(W, H):
     run_pair(W, H, W, ksize=5, T=5, n_batches=2, keep_planes=False)
 
 
-def test_two_batches_in_flight_match_sequential():
-    """fm_submit of batch i+1 before fm_wait of batch i (the pipelined mode): each wait completes the
-    oldest batch, results and background match the oracle run frame by frame; a third submit is refused."""
+def test_batches_in_flight_match_sequential():
+    """fm_submit of later batches before fm_wait of batch i (the pipelined mode): each wait completes the
+    oldest batch, results and background match the oracle run frame by frame; one submit beyond
+    fm_max_inflight is refused."""
     W, H, S, T = 320, 180, 2, 3
     eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T,
                        keep_planes=True)
     cfg = oracle.OracleConfig(H=H, W=W, box=W, ksize=5)
     orc = [oracle.OracleStream(cfg) for _ in range(S)]
-    batches = [batch(W, H, S, 90 + T * b, T) for b in range(4)]
-    eng.submit(batches[0])
-    for b in range(4):
-        if b + 1 < 4:
-            eng.submit(batches[b + 1])
-            if b == 0:
-                with pytest.raises(Exception):
-                    eng.submit(batches[0])  # two already in flight
+    NB = 6
+    batches = [batch(W, H, S, 90 + T * b, T) for b in range(NB)]
+    depth = eng.max_inflight
+    assert depth >= 2
+    for b in range(depth):
+        eng.submit(batches[b])
+    with pytest.raises(Exception):
+        eng.submit(batches[0])  # all slots in flight
+    for b in range(NB):
         eng.wait()
         counts = eng.counts()
         for t in range(T):
@@ -289,6 +291,8 @@ def test_two_batches_in_flight_match_sequential():
                 assert [c.bbox for c in eng.contours(t, s)] == ref["boxes"]
                 np.testing.assert_array_equal(eng.mask(t, s), ref["mask"])
                 np.testing.assert_array_equal(eng.plane(PLANE_BLUR, t, s), ref["blur"])
+        if b + depth < NB:  # reuses batch b's slot: its device-side results are gone after this
+            eng.submit(batches[b + depth])
     for s in range(S):
         np.testing.assert_array_equal(eng.background(s), orc[s].bg)
     eng.close()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Contour-pass ablations (FM_DEBUG_SKIP bits >= 64; results invalid), serial mode.
+mkdir -p gpurun_out
+for M in 0 64 128 192 256; do
+  FM_SERIAL=1 FM_DEBUG_SKIP=$M timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/abl_$M.log 2>&1 || { tail -3 gpurun_out/abl_$M.log; exit 1; }
+  tail -1 gpurun_out/abl_$M.log | python -c "
+import json,sys
+d=json.loads(sys.stdin.read()); k=d['kernels']
+print('skip=$M', {n: v['avg_us'] for n, v in k.items()})"
+done
