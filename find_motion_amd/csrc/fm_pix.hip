@@ -28,7 +28,10 @@ namespace fm {
 namespace px {
 
 constexpr int TS = 64;          // tile edge
-constexpr int NT = 512;         // threads
+#ifndef FM_PIX_NT
+#define FM_PIX_NT 512
+#endif
+constexpr int NT = FM_PIX_NT;   // threads
 constexpr int NW = NT / 64;     // waves; wave w owns tile rows [8w, 8w + 8)
 constexpr int RPWV = TS / NW;   // rows per wave in the chain stage
 
@@ -38,8 +41,8 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 // columns x0-PC .. x0+63+PC with PC = 4*ceil(r/4) (quad aligned)
 struct Geo {
     int r, PC, GW, NQ, GH, RS, CPR, nchunks, RSH;
-    int o_raw, o_H, o_rowy, o_colx, o_roff, bytes;
-    int raw_bytes, H_bytes, roff_bytes;  // per buffer; raw, H and roff are double buffered
+    int o_raw, o_H, o_rowy, o_colx, bytes;
+    int raw_bytes, H_bytes;  // per buffer; raw and H are double buffered
     __host__ __device__ explicit Geo(int rr) {
         r = rr;
         PC = 4 * ((r + 3) / 4);
@@ -52,13 +55,11 @@ struct Geo {
         RSH = (GH + 3) & ~3;  // transposed H row (u16 per G row), 8-B aligned
         raw_bytes = GH * RS;
         H_bytes = a16(TS * RSH * 2);
-        roff_bytes = a16(GH * 4);
         o_raw = 0;
         o_H = o_raw + 2 * raw_bytes;
         o_rowy = o_H + 2 * H_bytes;
         o_colx = o_rowy + a16(GH * 4);
-        o_roff = o_colx + a16(GW * 4);
-        bytes = o_roff + 2 * roff_bytes;
+        bytes = o_colx + a16(GW * 4);
     }
 };
 
@@ -287,7 +288,6 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + g.o_H);
     int* rowy = reinterpret_cast<int*>(smem + g.o_rowy);
     int* colx = reinterpret_cast<int*>(smem + g.o_colx);
-    int* roff = reinterpret_cast<int*>(smem + g.o_roff);
 
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -301,10 +301,9 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
     const bool init0 = INIT && a.init != nullptr && a.init[s] != 0;
-    // loaded source columns [cx0, cx1); interior tiles need no reflection
+    // loaded source columns [cx0, cx1)
     const int gx0 = x0 - g.PC;
     const int cx0 = max(gx0, 0), cx1 = min(gx0 + g.GW, w);
-    const bool interior = gx0 >= 0 && gx0 + g.GW <= w;
 
     for (int i = tid; i < g.GH; i += NT) rowy[i] = reflect101(y0 - R + i, h);
     for (int i = tid; i < g.GW; i += NT) colx[i] = 3 * (min(max(reflect101(gx0 + i, w), cx0), cx1 - 1) - cx0);
@@ -351,6 +350,11 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     constexpr int NG = (KC + 3) / 4;                   // dot4 groups (last one zero padded)
     constexpr int NQW = (6 + OFF + 4 * (NG - 1)) / 4 + 1;  // quads the 4-byte windows touch
     const int rg = ln / NQc, q = ln - rg * NQc;
+    // this lane's gray quad, columns [qc, qc + 4): the fast path needs it inside the
+    // loaded columns (only the quads over a reflected image edge take the gather path)
+    const int qc = gx0 + 4 * q;
+    const bool qin = qc >= cx0 && qc + 4 <= cx1;
+    const int qoff = 3 * (qc - cx0);
     uint32_t cpk[NG];
 #pragma unroll
     for (int gi = 0; gi < NG; gi++) cpk[gi] = tap4<KC>(gi);
@@ -360,43 +364,71 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     plan_chunks(plan, rowy, g, cx0, w, tid);
     const uint32_t span = 3u * (uint32_t)(cx1 - cx0), fb32 = (uint32_t)fbytes;
     // ---- gray (4 px per lane) + horizontal taps of frame f -> transposed H (u16)
-    auto gray_stage = [&](const uint8_t* rawb, const int* roffb, uint16_t* Hb, size_t f) {
+    // Lane (rg, q) of iteration it owns gray quad q of G row gy(it).  Frame-invariant
+    // per-lane state: the row's byte offset in the frame (its 16-B aligned-down start
+    // is where stage_raw put the row in LDS) and the G row index (clamped for idle lanes).
+    uint32_t rowbyte[NIT];
+    int gyc[NIT];
+    bool act[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; it++) {
+        const int gy = (it * NW + wv) * RPW + rg;
+        act[it] = rg < RPW && gy < GHc;
+        gyc[it] = act[it] ? gy : 0;
+        rowbyte[it] = (uint32_t)(rowy[gyc[it]] * w + cx0) * 3u;
+    }
+    auto gray_stage = [&](const uint8_t* rawb, uint16_t* Hb, size_t f) {
+        const uint32_t flo = (uint32_t)(uintptr_t)(a.src + f * fbytes);
+        uint32_t g4[NIT];
+        bool slow = false;
+        // straight-line over the iterations so their LDS round trips overlap
 #pragma unroll
         for (int it = 0; it < NIT; it++) {
-            const int gy = (it * NW + wv) * RPW + rg;
-            const bool act = rg < RPW && gy < GHc;
-            uint32_t g4 = 0;
-            if (act) {
-                const int ro = roffb[gy];
-                const uint8_t* rowp = rawb + gy * g.RS + ro;
-                if (interior && (ro & 3) == 0) {
-                    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rowp + 12 * q);
-                    g4 = gray4(p32[0], p32[1], p32[2]);
-                } else {  // reflected / unaligned columns
-                    const int c0 = 4 * q;
-                    g4 = gray1(rowp + colx[c0]) | (gray1(rowp + colx[c0 + 1]) << 8) | (gray1(rowp + colx[c0 + 2]) << 16) |
-                         (gray1(rowp + colx[c0 + 3]) << 24);
-                }
-                if (PLANES) {
-                    const int y = y0 - R + gy, xq = gx0 + 4 * q;
-                    if (gy >= R && gy < R + TS && xq >= x0 && xq < x0 + TS && y < h) {
-                        uint8_t* gp = a.planes + f * plane + (size_t)y * w;
+            const uint32_t ro = (flo + rowbyte[it]) & 15u;  // row start inside its first 16-B chunk
+            const uint32_t off = (uint32_t)(gyc[it] * g.RS) + ro + (uint32_t)qoff;
+            const bool fast = qin && (off & 3u) == 0;
+            slow |= !fast && act[it];
+            const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + (off & ~3u));
+            g4[it] = gray4(p32[0], p32[1], p32[2]);
+        }
+        if (__builtin_expect(slow, 0)) {  // reflected image edge or unaligned row: per-pixel gather
 #pragma unroll
-                        for (int b = 0; b < 4; b++)
-                            if (xq + b < w) gp[xq + b] = (uint8_t)(g4 >> (8 * b));
-                    }
+            for (int it = 0; it < NIT; it++) {
+                const uint32_t ro = (flo + rowbyte[it]) & 15u;
+                const uint32_t off = (uint32_t)(gyc[it] * g.RS) + ro + (uint32_t)qoff;
+                if (act[it] && !(qin && (off & 3u) == 0)) {
+                    const uint8_t* rowp = rawb + gyc[it] * g.RS + ro;
+                    const int c0 = 4 * q;
+                    g4[it] = gray1(rowp + colx[c0]) | (gray1(rowp + colx[c0 + 1]) << 8) |
+                             (gray1(rowp + colx[c0 + 2]) << 16) | (gray1(rowp + colx[c0 + 3]) << 24);
                 }
             }
-            uint32_t qv[NQW];
-            qv[0] = g4;
+        }
 #pragma unroll
-            for (int d = 1; d < NQW; d++) qv[d] = d < NQN ? (uint32_t)__shfl_down((int)g4, d, 64) : 0u;  // zero-weight bytes
-            if (act && q < TS / 4) {
+        for (int it = 0; it < NIT; it++) {
+            if (PLANES && act[it]) {
+                const int gy = gyc[it];
+                const int y = y0 - R + gy, xq = gx0 + 4 * q;
+                if (gy >= R && gy < R + TS && xq >= x0 && xq < x0 + TS && y < h) {
+                    uint8_t* gp = a.planes + f * plane + (size_t)y * w;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        if (xq + b < w) gp[xq + b] = (uint8_t)(g4[it] >> (8 * b));
+                }
+            }
+            // neighbour quads q+1, q+2, ... by wavefront shifts (DPP wave_shl:1, lane i <- lane i+1);
+            // across a row group's end they bring the next row's quads, which only feed halo lanes
+            uint32_t qv[NQW];
+            qv[0] = g4[it];
+#pragma unroll
+            for (int d = 1; d < NQW; d++)
+                qv[d] = d < NQN ? (uint32_t)__builtin_amdgcn_mov_dpp((int)qv[d - 1], 0x130, 0xF, 0xF, true) : 0u;
+            if (act[it] && q < TS / 4) {
                 const uint32_t h0 = htap<0, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h1 = htap<1, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h2 = htap<2, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h3 = htap<3, OFF, NG, 0, NQW>(qv, cpk, 0u);
-                uint16_t* hc = Hb + (4 * q) * g.RSH + gy;
+                uint16_t* hc = Hb + (4 * q) * g.RSH + gyc[it];
                 hc[0] = (uint16_t)h0;
                 hc[g.RSH] = (uint16_t)h1;
                 hc[2 * g.RSH] = (uint16_t)h2;
@@ -404,30 +436,26 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
             }
         }
     };
-    auto stage_raw = [&](const Raw<NCH>& Rr, int buf, size_t f) {
-        store_raw(Rr, raw + buf * g.raw_bytes, g, tid);
-        if (tid < g.GH)
-            roff[buf * (g.roff_bytes / 4) + tid] =
-                (int)(((uintptr_t)(a.src + f * fbytes) + ((size_t)rowy[tid] * w + cx0) * 3) & 15);
-    };
+    auto stage_raw = [&](const Raw<NCH>& Rr, int buf) { store_raw(Rr, raw + buf * g.raw_bytes, g, tid); };
 
     // Software pipeline, one barrier per frame: iteration t runs the chain of
     // frame t (H buffer t&1) and the gray/horizontal stage of frame t+1 (raw and
     // H buffers (t+1)&1), while frame t+2's raw tile is in flight into registers.
     const int t0 = a.t_begin, t1 = a.t_end;
+    const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);  // profiling-only ablation (FM_DEBUG_SKIP)
     Raw<NCH> Rw;
     load_raw(Rw, a.src + ((size_t)t0 * S + s) * fbytes, fb32, plan, span);
-    stage_raw(Rw, 0, (size_t)t0 * S + s);
+    stage_raw(Rw, 0);
     if (t0 + 1 < t1) load_raw(Rw, a.src + ((size_t)(t0 + 1) * S + s) * fbytes, fb32, plan, span);
     lds_barrier();
-    gray_stage(raw, roff, Hs, (size_t)t0 * S + s);
+    gray_stage(raw, Hs, (size_t)t0 * S + s);
 
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
         if (t + 1 < t1) {
-            stage_raw(Rw, b ^ 1, f + S);
-            if (t + 2 < t1) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
+            if (!(skip & 8)) stage_raw(Rw, b ^ 1);
+            if (t + 2 < t1 && !(skip & 4)) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
         }
         lds_barrier();
 
@@ -437,10 +465,11 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
         // per-row exec masks out of the frame loop and they spill
         ChainCtx ccf = cc;
         int x0f = x0, y0f = y0, wvf = wv;
-        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+        if constexpr (NT == 512) asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-        chain_rows<KC, PLANES, INIT>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf, init0 && t == t0,
-                                     mybits);
+        if (!(skip & 2))
+            chain_rows<KC, PLANES, INIT>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf, init0 && t == t0,
+                                         mybits);
         if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
         {   // where the tile has threshold bits (decides the contour pass's candidate tiles)
             uint32_t fl = 0;
@@ -457,9 +486,8 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
             if (ln == 0 && fl) atomicOr(&a.tflag[f * a.ntiles + ti], fl);
         }
 
-        if (t + 1 < t1)
-            gray_stage(raw + (b ^ 1) * g.raw_bytes, roff + (b ^ 1) * (g.roff_bytes / 4), Hs + (b ^ 1) * (g.H_bytes / 2),
-                       f + S);
+        if (t + 1 < t1 && !(skip & 1))
+            gray_stage(raw + (b ^ 1) * g.raw_bytes, Hs + (b ^ 1) * (g.H_bytes / 2), f + S);
     }
 
     // background out (ping-pong: neighbours never read this batch's update)
