@@ -93,6 +93,9 @@ def main() -> None:
     ap.add_argument("--cpu-frames", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
+    ap.add_argument("--no-ktimes", action="store_true", help="no HIP event timing at all (no roofline)")
+    ap.add_argument("--all-ktimes", action="store_true",
+                    help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
 
     from find_motion_amd import dist
@@ -130,7 +133,7 @@ def main() -> None:
     frame_bytes = S * H * W * 3
 
     eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
-                       max_batch=T, max_contours=1 << 14, profile=True, device=local)
+                       max_batch=T, max_contours=1 << 14, profile=False if args.no_ktimes else True if args.all_ktimes else "pix", device=local)
     base = ring.data_ptr()
     n_batches = R // T
 

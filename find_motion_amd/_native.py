@@ -16,7 +16,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libfm_hip.so")
 
 FM_OK, FM_EINVAL, FM_EHIP, FM_ENOMEM, FM_ESTATE, FM_ENOTSUP = 0, -1, -2, -3, -4, -5
-FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE = 0x1, 0x2
+FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE, FM_FLAG_PROFILE_PIX = 0x1, 0x2, 0x4
 PLANE_GRAY, PLANE_BLUR, PLANE_DELTA = 0, 1, 2
 
 EXPORTED = (
@@ -131,11 +131,13 @@ class MotionEngine:
 
     def __init__(self, *, n_streams: int, src_w: int, src_h: int, box_size: int, ksize: int,
                  threshold: int, avg: float, max_batch: int = 1, max_contours: int = 4096,
-                 keep_planes: bool = False, profile: bool = False, device: int = 0):
+                 keep_planes: bool = False, profile: bool | str = False, device: int = 0):
+        # profile: True = every kernel timed with HIP events, "pix" = pixel-stream kernels only
         self._L = load()
         p = FMParams(device, n_streams, src_w, src_h, box_size, ksize, int(threshold), float(avg),
                      max_batch, max_contours,
-                     (FM_FLAG_KEEP_PLANES if keep_planes else 0) | (FM_FLAG_PROFILE if profile else 0))
+                     (FM_FLAG_KEEP_PLANES if keep_planes else 0) |
+                     (FM_FLAG_PROFILE_PIX if profile == "pix" else FM_FLAG_PROFILE if profile else 0))
         h = C.c_void_p()
         rc = self._L.fm_create(C.byref(h), C.byref(p))
         if rc != FM_OK:

@@ -36,7 +36,7 @@ enum class ResizeMode { Identity, Fast, General };
 // recurrence), each slot's contour pass on its own stream, so the latency-bound
 // contour passes of consecutive batches overlap each other and the next
 // batches' pixel kernels.
-constexpr int kSlots = 3;
+constexpr int kSlots = 4;
 struct BatchSlot {
     uint8_t* d_in = nullptr;        // host-fed staging [T][S][H][W][3]
     uint8_t* d_work = nullptr;      // resized BGR [T][S][h][w][3] (mode D)
@@ -55,6 +55,8 @@ struct BatchSlot {
     int32_t* d_count = nullptr;     // [2F+1]
     int32_t* h_count = nullptr;     // pinned [F]
     int32_t* h_overflow = nullptr;  // pinned [F]
+    int32_t* dh_count = nullptr;     // device aliases of the two (mapped): the fused path's k_fold_emit writes them
+    int32_t* dh_overflow = nullptr;
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
@@ -75,6 +77,8 @@ struct fm_ctx {
 
     // streams: pixel work (caller-replaceable), contour pass, synchronous reads
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
+    hipStream_t ccl_streams[kSlots] = {};
+    int nccl = 1;
     KernelTimer timer;
 
     // device state shared by all batches
@@ -246,6 +250,7 @@ namespace fm {
 int KernelTimer::begin(const char* name, hipStream_t st) {
     if (!enabled) return -1;
     if (!st) st = stream;
+    if (pixel_only && st != stream) return -1;
     int id = -1;
     for (size_t i = 0; i < names.size(); i++)
         if (names[i] == name || std::strcmp(names[i], name) == 0) id = (int)i;
@@ -349,10 +354,17 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 
     fm_ctx* cp = c.get();
     HIP_TRY(cp, hipSetDevice(p.device));
-    HIP_TRY(cp, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    {   // the pixel stream at high priority: it gets a hardware queue of its own instead of
+        // sharing one (in order) with a contour-pass stream
+        int lo = 0, hi = 0;
+        HIP_TRY(cp, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        if (std::getenv("FM_PIX_PRIO_OFF")) hi = lo;
+        HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
+    }
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
-    c->timer.enabled = (p.flags & FM_FLAG_PROFILE) != 0;
+    c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
+    c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
     c->timer.stream = c->stream;
 
     const size_t S = p.n_streams, T = p.max_batch;
@@ -365,6 +377,11 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
                  std::getenv("FM_NO_PIX") == nullptr;
     c->nslots = c->use_fused ? kSlots : 1;
+    // contour-pass streams shared round-robin by the slots: few streams, because the
+    // runtime multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order,
+    // and a contour kernel queued ahead of a pixel kernel on a shared queue stalls it
+    c->nccl = 2;
+    if (const char* e = std::getenv("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
@@ -395,10 +412,14 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         // (only the records that exist cross PCIe)
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.d_rec, b.h_rec, 0));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t)));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t)));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_count, b.h_count, 0));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_overflow, b.h_overflow, 0));
+        if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * sizeof(uint32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
-        HIP_TRY(cp, hipStreamCreateWithFlags(&b.ccl_stream, hipStreamNonBlocking));
+        if (i < c->nccl) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
+        b.ccl_stream = c->ccl_streams[i % c->nccl];
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
     }
@@ -431,6 +452,9 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         c->ts_sum.assign(16, 0.0);
         c->ts_n.assign(16, 0);
     }
+    // the initialising hipMemset calls run on the null stream, which does not order the
+    // context's non-blocking streams: finish them before the first submit can read the buffers
+    HIP_TRY(cp, hipDeviceSynchronize());
     *out = c.release();
     return FM_OK;
 }
@@ -447,11 +471,13 @@ void fm_destroy(fm_ctx* c) {
     (void)hipSetDevice(c->p.device);
     for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream})
         if (st) (void)hipStreamSynchronize(st);
-    for (auto& b : c->slots) {
-        if (b.ccl_stream) {
-            (void)hipStreamSynchronize(b.ccl_stream);
-            (void)hipStreamDestroy(b.ccl_stream);
+    for (hipStream_t& st : c->ccl_streams)
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+            st = nullptr;
         }
+    for (auto& b : c->slots) {
         dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
         dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
         dfree(b.d_clist); dfree(b.d_rlist); dfree(b.d_regrep); dfree(b.d_ncr);
@@ -551,8 +577,8 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, B.h_init, S, hipMemcpyHostToDevice, ps));
 
     const long long npx = (long long)c->work_plane;
-    HIP_TRY(c, hipMemsetAsync(B.d_count, 0, (2 * F + 1) * sizeof(int32_t), ps));
-    if (B.d_tflag) HIP_TRY(c, hipMemsetAsync(B.d_tflag, 0, F * c->ntiles * sizeof(uint32_t), ps));
+    // fused path: k_regions zeroes the counters, k_fold_emit clears the tile flags
+    if (!c->use_fused) HIP_TRY(c, hipMemsetAsync(B.d_count, 0, (2 * F + 1) * sizeof(int32_t), ps));
     if (c->use_fused) {
         FusedArgs fa{};
         fa.src = work;
@@ -576,6 +602,8 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.count = B.d_count;
         fa.heavy = B.d_heavy;
         fa.rec = B.d_rec;
+        fa.h_count = B.dh_count;
+        fa.h_overflow = B.dh_overflow;
         fa.T = n;
         fa.S = S;
         fa.h = c->h;
@@ -628,9 +656,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         hipStream_t cs = c->serial ? ps : B.ccl_stream;
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
         HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
-        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer));
-        HIP_TRY(c, hipMemcpyAsync(B.h_overflow, B.d_count + F, F * sizeof(int32_t), hipMemcpyDeviceToHost, cs));
-        HIP_TRY(c, hipMemcpyAsync(B.h_count, B.d_count, F * sizeof(int32_t), hipMemcpyDeviceToHost, cs));
+        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer));  // counts land in mapped h_count / h_overflow
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));
     } else {
         PixelArgs a{};

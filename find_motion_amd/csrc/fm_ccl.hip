@@ -421,7 +421,13 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     const int f = blockIdx.x;
     const int nt = a.ntiles, ntx = a.ntx, nty = a.nty;
     const int tid = threadIdx.x;
-    if (tid == 0) s_nc = s_nr = 0;
+    if (tid == 0) {
+        s_nc = s_nr = 0;
+        // this batch's counters (the slot's previous batch was read back before reuse)
+        a.count[f] = 0;
+        a.count[(size_t)a.T * a.S + f] = 0;
+        if (f == 0) a.count[2 * (size_t)a.T * a.S] = 0;
+    }
     __syncthreads();
     for (int t = tid; t < nt; t += RG) {
         const bool c = is_candidate(a, f, t, DILATE);
@@ -634,7 +640,15 @@ constexpr int FT = 256;
 __global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
     const size_t f = blockIdx.x;
     const size_t F = (size_t)a.T * a.S;
-    if (a.count[F + f]) return;
+    // the tile flags were consumed by k_regions: clear them for the slot's next batch
+    for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
+    if (a.count[F + f]) {  // relabelled by the host's pixel-level fallback
+        if (threadIdx.x == 0) {
+            a.h_overflow[f] = 1;
+            a.h_count[f] = 0;
+        }
+        return;
+    }
     NodeRec* N = a.nodes + f * (size_t)a.nnodes;
     const TileRec* TRf = a.tiles + f * a.ntiles;
     const uint8_t* cf = a.candf + f * a.ntiles;
@@ -690,6 +704,11 @@ __global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
             }
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // results straight into mapped host memory: no copy after the kernel
+        a.h_count[f] = __hip_atomic_load(&a.count[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.h_overflow[f] = 0;
+    }
 }
 
 // one thread per 8 mask bytes of one frame; non-candidate tiles are empty
@@ -720,7 +739,7 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     tok = tm ? tm->begin("tile_ccl", st) : -1;
     if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), 0, st, a);
     else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), 0, st, a);
-    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(64), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(8), dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);

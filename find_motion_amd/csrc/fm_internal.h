@@ -100,6 +100,8 @@ struct FusedArgs {
     int32_t* count;              // [2F+1]: [f] external contours, [F+f] overflow flag, [2F] heavy-tile count
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
     int32_t* rec;                // [F][cap][5]
+    int32_t* h_count;            // mapped host [F]: external contours per frame (written by k_fold_emit)
+    int32_t* h_overflow;         // mapped host [F]: frame needs the pixel-level fallback
     int T, S, h, w, ksize, thresh;
     int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
@@ -138,6 +140,7 @@ hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8
 // the launch stream around each kernel and read back after the stream syncs.
 struct KernelTimer {
     bool enabled = false;
+    bool pixel_only = false;  // time only launches on `stream` (the pixel stream): FM_FLAG_PROFILE_PIX
     hipStream_t stream = nullptr;
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;

@@ -77,18 +77,31 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 
-// BGR2GRAY of 4 consecutive pixels packed in 3 dwords (B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3)
+template <int I> struct IntC { static constexpr int value = I; };
+// compile-time unrolled loop: fn(IntC<0>{}), ..., fn(IntC<N-1>{})
+template <int N, int I = 0, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+    if constexpr (I < N) {
+        fn(IntC<I>{});
+        static_for<N, I + 1>(fn);
+    }
+}
+
+// BGR2GRAY of 4 consecutive pixels packed in 3 dwords (B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3):
+// (1868 B + 9617 G + 4899 R + 8192) >> 14 computed with all constants x4, so that
+// gray is byte 2 of the sum (< 2^24) and two v_perm gather the four results.
 __device__ __forceinline__ uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
-    const u16x2_t cbg = __builtin_bit_cast(u16x2_t, 1868u | (9617u << 16));
+    const u16x2_t cbg = __builtin_bit_cast(u16x2_t, (4u * 1868u) | ((4u * 9617u) << 16));
+    constexpr uint32_t CR = 4u * 4899u, RND = 4u * 8192u;
     const uint32_t p0 = __builtin_amdgcn_perm(d0, d0, 0x0C010C00u);
     const uint32_t p1 = __builtin_amdgcn_perm(d1, d0, 0x0C040C03u);
     const uint32_t p2 = __builtin_amdgcn_perm(d1, d1, 0x0C030C02u);
     const uint32_t p3 = __builtin_amdgcn_perm(d2, d2, 0x0C020C01u);
-    const uint32_t g0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p0), cbg, __umul24((d0 >> 16) & 0xFF, 4899u) + 8192u, false) >> 14;
-    const uint32_t g1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p1), cbg, __umul24((d1 >> 8) & 0xFF, 4899u) + 8192u, false) >> 14;
-    const uint32_t g2 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p2), cbg, __umul24(d2 & 0xFF, 4899u) + 8192u, false) >> 14;
-    const uint32_t g3 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p3), cbg, __umul24(d2 >> 24, 4899u) + 8192u, false) >> 14;
-    return g0 | (g1 << 8) | (g2 << 16) | (g3 << 24);
+    const uint32_t g0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p0), cbg, __umul24((d0 >> 16) & 0xFF, CR) + RND, false);
+    const uint32_t g1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p1), cbg, __umul24((d1 >> 8) & 0xFF, CR) + RND, false);
+    const uint32_t g2 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p2), cbg, __umul24(d2 & 0xFF, CR) + RND, false);
+    const uint32_t g3 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, p3), cbg, __umul24(d2 >> 24, CR) + RND, false);
+    return __builtin_amdgcn_perm(g1, g0, 0x0C0C0602u) | __builtin_amdgcn_perm(g3, g2, 0x06020C0Cu);
 }
 
 __device__ __forceinline__ uint32_t gray1(const uint8_t* p) {
@@ -216,8 +229,10 @@ struct ChainCtx {
 
 // One frame's vertical taps + per-pixel chain for the wave's 8 rows.
 // INIT: the launch may hold a stream's first frame (bg := blur before the diff,
-// fm.py:651-652); `init` says whether this frame is one.
-template <int KC, bool PLANES, bool INIT>
+// fm.py:651-652); `init` says whether this frame is one.  KEEP: apply the
+// keep-mask bytes (off when the stream has no mask).  TAIL: the wave's rows reach
+// accumulateWeighted's scalar tail (per-pixel test of the product order).
+template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
 __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const Geo& g, double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
                                            bool init, uint64_t& mybits) {
@@ -243,9 +258,11 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
     }
     const double alpha = a.alpha, beta = a.beta;
     const int thresh = a.thresh;
-#pragma unroll
-    for (int j = 0; j < RPWV; j++) {
-        // acc = sum_t c[t] * H[j + t] + 2^15 over u16 pairs (H[e], H[e+1])
+    int mb_lo = 0, mb_hi = 0;
+    static_for<RPWV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        // acc = sum_t c[t] * H[j + t] + 2^15 over u16 pairs (H[e], H[e+1]); blur = byte 2
+        // (acc < 2^24), bytes 0-1 are the fraction
         uint32_t acc = 32768u;
 #pragma unroll
         for (int t = 0; t < (KC + 1) / 2; t++) {
@@ -253,30 +270,36 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
             const uint32_t pr = (e & 1) ? __builtin_amdgcn_alignbit(P[(e >> 1) + 1], P[e >> 1], 16) : P[e >> 1];
             acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, pr), __builtin_bit_cast(u16x2_t, tap2<KC>(t)), acc, false);
         }
-        // keep bytes are 0xFF (keep) / 0x00 (masked off, fm.py:619-636); all 0xFF without a mask
-        const uint32_t blur = (acc >> 16) & ((j < 4 ? cc.keep_lo >> (8 * j) : cc.keep_hi >> (8 * (j - 4))) & 0xFFu);
+        // keep bytes are 0xFF (keep) / 0x00 (masked off, fm.py:619-636): masked pixels blur to 0
+        if (KEEP)
+            acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
+        const uint32_t blur = acc >> 16;
         double b = bg[j];
         if (INIT && init) b = (double)blur;
-        // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8
-        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 0, 0u);
-        const uint32_t d = __builtin_amdgcn_sad_u8(blur, q, 0u);  // absdiff
+        // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8 -- into byte 2 of a copy
+        // of acc, so that the byte-wise absdiff of the two words is |blur - q|
+        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
+        const uint32_t d = __builtin_amdgcn_sad_u8(acc, q, 0u);  // absdiff
         const uint64_t bits = __builtin_amdgcn_ballot_w64((int)d > thresh);
         const double bl = __dmul_rn((double)blur, alpha);
         double nb = __fma_rn(b, beta, bl);
-        if (!cc.vec) {  // the tile holding accumulateWeighted's scalar tail: two products, one add there
+        if (TAIL) {  // accumulateWeighted's scalar tail: two products, one add there
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
             if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
         }
         const bool rv = (cc.rowvalid >> j) & 1;
         bg[j] = nb;  // out-of-image pixels compute values that are never stored
-        if (ln == j) mybits = rv ? (bits & cc.colmask) : 0;
+        const uint64_t bm = rv ? (bits & cc.colmask) : 0;  // row j's bits -> lane j
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_lo) : "s"((uint32_t)bm), "n"(j));
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_hi) : "s"((uint32_t)(bm >> 32)), "n"(j));
         if (PLANES && rv && ((cc.colmask >> ln) & 1)) {
             const size_t plane = (size_t)a.h * w;
             const size_t li = (size_t)(y0 + RPWV * wv + j) * w + x0 + ln;
             a.planes[(size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)blur;
             a.planes[2 * (size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)d;
         }
-    }
+    });
+    mybits = ((uint64_t)(uint32_t)mb_hi << 32) | (uint32_t)mb_lo;
 }
 
 template <int KC, bool PLANES, bool INIT>
@@ -367,7 +390,7 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     // Lane (rg, q) of iteration it owns gray quad q of G row gy(it).  Frame-invariant
     // per-lane state: the row's byte offset in the frame (its 16-B aligned-down start
     // is where stage_raw put the row in LDS) and the G row index (clamped for idle lanes).
-    uint32_t rowbyte[NIT];
+    uint32_t rowbyte[NIT], loff[NIT];
     int gyc[NIT];
     bool act[NIT];
 #pragma unroll
@@ -376,26 +399,38 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
         act[it] = rg < RPW && gy < GHc;
         gyc[it] = act[it] ? gy : 0;
         rowbyte[it] = (uint32_t)(rowy[gyc[it]] * w + cx0) * 3u;
+        loff[it] = (uint32_t)(gyc[it] * g.RS + qoff);
     }
+    // rows of a 16-B multiple: every row starts at the same offset inside its first chunk
+    const bool rows16 = (w * 3) % 16 == 0;
     auto gray_stage = [&](const uint8_t* rawb, uint16_t* Hb, size_t f) {
         const uint32_t flo = (uint32_t)(uintptr_t)(a.src + f * fbytes);
         uint32_t g4[NIT];
         bool slow = false;
         // straight-line over the iterations so their LDS round trips overlap
+        if (rows16) {
+            const uint32_t ro = (flo + 3u * (uint32_t)cx0) & 15u;  // uniform
+            slow = act[0] && !(qin && ((ro + (uint32_t)qoff) & 3u) == 0);
 #pragma unroll
-        for (int it = 0; it < NIT; it++) {
-            const uint32_t ro = (flo + rowbyte[it]) & 15u;  // row start inside its first 16-B chunk
-            const uint32_t off = (uint32_t)(gyc[it] * g.RS) + ro + (uint32_t)qoff;
-            const bool fast = qin && (off & 3u) == 0;
-            slow |= !fast && act[it];
-            const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + (off & ~3u));
-            g4[it] = gray4(p32[0], p32[1], p32[2]);
+            for (int it = 0; it < NIT; it++) {
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + ((loff[it] + ro) & ~3u));
+                g4[it] = gray4(p32[0], p32[1], p32[2]);
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < NIT; it++) {
+                const uint32_t ro = (flo + rowbyte[it]) & 15u;  // row start inside its first 16-B chunk
+                const uint32_t off = loff[it] + ro;
+                slow |= act[it] && !(qin && (off & 3u) == 0);
+                const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + (off & ~3u));
+                g4[it] = gray4(p32[0], p32[1], p32[2]);
+            }
         }
         if (__builtin_expect(slow, 0)) {  // reflected image edge or unaligned row: per-pixel gather
 #pragma unroll
             for (int it = 0; it < NIT; it++) {
                 const uint32_t ro = (flo + rowbyte[it]) & 15u;
-                const uint32_t off = (uint32_t)(gyc[it] * g.RS) + ro + (uint32_t)qoff;
+                const uint32_t off = loff[it] + ro;
                 if (act[it] && !(qin && (off & 3u) == 0)) {
                     const uint8_t* rowp = rawb + gyc[it] * g.RS + ro;
                     const int c0 = 4 * q;
@@ -467,9 +502,16 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
         int x0f = x0, y0f = y0, wvf = wv;
         if constexpr (NT == 512) asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-        if (!(skip & 2))
-            chain_rows<KC, PLANES, INIT>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf, init0 && t == t0,
-                                         mybits);
+        if (!(skip & 2)) {
+            const uint16_t* Hb = Hs + b * (g.H_bytes / 2);
+            const bool fi = init0 && t == t0;
+            if (!ccf.vec)
+                chain_rows<KC, PLANES, INIT, true, true>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
+            else if (ccf.hk)
+                chain_rows<KC, PLANES, INIT, true, false>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
+            else
+                chain_rows<KC, PLANES, INIT, false, false>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
+        }
         if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
         {   // where the tile has threshold bits (decides the contour pass's candidate tiles)
             uint32_t fl = 0;

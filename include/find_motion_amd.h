@@ -42,6 +42,7 @@ extern "C" {
 /* fm_params.flags */
 #define FM_FLAG_KEEP_PLANES 0x1u /* keep gray/blur/frame_delta per frame (show/debug, fm.py:907-926) */
 #define FM_FLAG_PROFILE 0x2u     /* time every kernel launch with HIP events */
+#define FM_FLAG_PROFILE_PIX 0x4u /* time only the pixel-stream kernels (cheap enough for the bench's timed loop) */
 
 /* planes for fm_read_plane */
 #define FM_PLANE_GRAY 0  /* VideoFrame.gray        (fm.py:493) */

@@ -17,6 +17,13 @@ from find_motion_amd.synthetic import batch
 pytestmark = pytest.mark.gpu
 
 
+def _eq(got, ref, msg):
+    if not np.array_equal(got, ref):
+        bad = np.argwhere(got != ref)
+        raise AssertionError(f"{msg}: {len(bad)} mismatches, first {bad[:16].tolist()} "
+                             f"got {got[tuple(bad[:8].T)].tolist()} ref {ref[tuple(bad[:8].T)].tolist()}")
+
+
 def run_pair(W, H, box, blur_scale=20, ksize=None, S=1, T=3, n_batches=2, thresh=12, alpha=0.1,
              masks=None, keep_planes=True, start=0, frames=None):
     k = ksize if ksize is not None else make_gaussian(box, blur_scale)
@@ -41,9 +48,9 @@ def run_pair(W, H, box, blur_scale=20, ksize=None, S=1, T=3, n_batches=2, thresh
                 ref = orc[s].step(fr[t, s])
                 tag = f"batch {b} frame {t} stream {s}"
                 if keep_planes:
-                    np.testing.assert_array_equal(eng.plane(PLANE_GRAY, t, s), ref["gray"], err_msg="gray " + tag)
-                    np.testing.assert_array_equal(eng.plane(PLANE_BLUR, t, s), ref["blur"], err_msg="blur " + tag)
-                    np.testing.assert_array_equal(eng.plane(PLANE_DELTA, t, s), ref["delta"], err_msg="delta " + tag)
+                    _eq(eng.plane(PLANE_GRAY, t, s), ref["gray"], "gray " + tag)
+                    _eq(eng.plane(PLANE_BLUR, t, s), ref["blur"], "blur " + tag)
+                    _eq(eng.plane(PLANE_DELTA, t, s), ref["delta"], "delta " + tag)
                 np.testing.assert_array_equal(eng.mask(t, s), ref["mask"], err_msg="mask " + tag)
                 assert counts[t, s] == ref["count"], tag
                 got = [c.bbox for c in eng.contours(t, s)]
@@ -51,7 +58,10 @@ def run_pair(W, H, box, blur_scale=20, ksize=None, S=1, T=3, n_batches=2, thresh
                 assert [c.origin for c in eng.contours(t, s)] == ref["origins"], tag
         for s in range(S):
             bg = eng.background(s)
-            np.testing.assert_allclose(bg, orc[s].bg, rtol=0, atol=1e-4)
+            if not np.allclose(bg, orc[s].bg, rtol=0, atol=1e-4):
+                bad = np.argwhere(np.abs(bg - orc[s].bg) > 1e-4)
+                raise AssertionError(f"background batch {b} stream {s}: {len(bad)} bad, first {bad[:8].tolist()} "
+                                     f"got {bg[tuple(bad[:8].T)].tolist()} ref {orc[s].bg[tuple(bad[:8].T)].tolist()}")
             assert np.array_equal(bg, orc[s].bg), "background not bit-identical"
     eng.close()
 

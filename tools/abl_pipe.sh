@@ -1,0 +1,10 @@
+#!/bin/bash
+# Pipelined (default-mode) bench under stage ablations (results invalid): which side bounds the steady state.
+mkdir -p gpurun_out
+for M in ${MASKS:-0 64 15 79}; do
+  FM_DEBUG_SKIP=$M timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 3 "$@" > gpurun_out/ablpipe_$M.log 2>&1 || { tail -3 gpurun_out/ablpipe_$M.log; exit 1; }
+  tail -1 gpurun_out/ablpipe_$M.log | python -c "
+import json,sys
+d=json.loads(sys.stdin.read()); k=d['kernels']
+print('skip=$M', d['value'], {n: v['avg_us'] for n, v in k.items()})"
+done

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Contour-stream count x pixel-stream priority sweep of the default bench.
+for P in "" "FM_PIX_PRIO_OFF=1"; do
+for N in ${NS:-2 3 4}; do
+    env $P FM_CCL_STREAMS=$N timeout -k 10 120 python bench.py --no-cpu-baseline > gpurun_out/q.log 2>&1 || { tail -3 gpurun_out/q.log; exit 1; }
+    echo "$P ccl_streams=$N $(tail -1 gpurun_out/q.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["avg_launch_us"])')"
+done
+done
