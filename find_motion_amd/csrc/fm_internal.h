@@ -140,7 +140,9 @@ hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8
 // the launch stream around each kernel and read back after the stream syncs.
 struct KernelTimer {
     bool enabled = false;
-    bool pixel_only = false;  // time only launches on `stream` (the pixel stream): FM_FLAG_PROFILE_PIX
+    bool pixel_only = false;  // time only launches on `stream` (the pixel stream), one in kSample: FM_FLAG_PROFILE_PIX
+    static constexpr int kSample = 4;
+    std::vector<int64_t> calls;
     hipStream_t stream = nullptr;
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;

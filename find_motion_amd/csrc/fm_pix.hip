@@ -28,6 +28,11 @@ namespace fm {
 namespace px {
 
 constexpr int TS = 64;          // tile edge
+// minimum waves per SIMD the steady-state variants are compiled for (2 workgroups of
+// 8 waves per CU = 4 per SIMD: <= 128 VGPRs)
+#ifndef FM_PIX_WPE
+#define FM_PIX_WPE 4
+#endif
 #ifndef FM_PIX_NT
 #define FM_PIX_NT 512
 #endif
@@ -52,9 +57,9 @@ struct Geo {
         RS = a16(3 * GW + 15);  // aligned-down row start (<= 15 B early) + 3 B per gray column
         CPR = RS / 16;
         nchunks = GH * CPR;
-        RSH = (GH + 3) & ~3;  // transposed H row (u16 per G row), 8-B aligned
+        RSH = TS;  // H is row-major: u16 [GH (+1 pad row)][TS]
         raw_bytes = GH * RS;
-        H_bytes = a16(TS * RSH * 2);
+        H_bytes = a16((GH + 1) * RSH * 2);
         o_raw = 0;
         o_H = o_raw + 2 * raw_bytes;
         o_rowy = o_H + 2 * H_bytes;
@@ -235,30 +240,28 @@ struct ChainCtx {
 template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
 __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const Geo& g, double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
-                                           bool init, uint64_t& mybits) {
+                                           bool init, uint64_t& mybits, uint32_t& flags) {
     constexpr int R = KC >> 1;
     constexpr int NV = RPWV + 2 * R;       // H rows feeding the wave's 8 outputs
     constexpr int NP = (NV + 1) / 2;       // u16 pairs
     const int w = a.w;
-    // transposed H: column ln, rows 8*wv .. 8*wv + NV - 1, read as pairs
+    // column ln of H, rows 8*wv .. 8*wv + NV - 1, as u16 pairs (ds_read_u16_d16 / _d16_hi)
     uint32_t P[NP + 1];
     {
-        const uint32_t* col = reinterpret_cast<const uint32_t*>(Hs + ln * g.RSH + RPWV * wv);
+        const uint16_t* col = Hs + (RPWV * wv) * g.RSH + ln;
 #pragma unroll
-        for (int i = 0; i < NP; i += 2) {
-            if (i + 1 < NP) {
-                const uint2 v = *reinterpret_cast<const uint2*>(col + i);
-                P[i] = v.x;
-                P[i + 1] = v.y;
-            } else {
-                P[i] = col[i];
-            }
+        for (int i = 0; i < NP; i++) {
+            u16x2_t v;
+            v.x = col[(2 * i) * g.RSH];
+            v.y = col[(2 * i + 1) * g.RSH];
+            P[i] = __builtin_bit_cast(uint32_t, v);
         }
         P[NP] = 0;
     }
     const double alpha = a.alpha, beta = a.beta;
     const int thresh = a.thresh;
     int mb_lo = 0, mb_hi = 0;
+    uint64_t orr = 0, top = 0, bot = 0;  // wave-uniform ORs of the row ballots (SGPRs)
     static_for<RPWV>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         // acc = sum_t c[t] * H[j + t] + 2^15 over u16 pairs (H[e], H[e+1]); blur = byte 2
@@ -290,6 +293,9 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         const bool rv = (cc.rowvalid >> j) & 1;
         bg[j] = nb;  // out-of-image pixels compute values that are never stored
         const uint64_t bm = rv ? (bits & cc.colmask) : 0;  // row j's bits -> lane j
+        orr |= bm;
+        if (j < 2) top |= bm;
+        if (j >= RPWV - 2) bot |= bm;
         asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_lo) : "s"((uint32_t)bm), "n"(j));
         asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_hi) : "s"((uint32_t)(bm >> 32)), "n"(j));
         if (PLANES && rv && ((cc.colmask >> ln) & 1)) {
@@ -300,10 +306,17 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         }
     });
     mybits = ((uint64_t)(uint32_t)mb_hi << 32) | (uint32_t)mb_lo;
+    // where the tile has threshold bits (decides the contour pass's candidate tiles):
+    // any, within 2 px of the left / right edge, and for the tile's first / last two rows
+    uint32_t fl = 0;
+    if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
+    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    flags = fl;
 }
 
 template <int KC, bool PLANES, bool INIT>
-__global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && !PLANES && !INIT) ? FM_PIX_WPE : 1))) void k_pix(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = KC >> 1;
     const Geo g(R);
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
         cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
         cc.rowvalid = 0;
         cc.keep_lo = cc.keep_hi = 0;
-        cc.hk = hk;
+        cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;  // wave-uniform (chooses the loop variant)
 #pragma unroll
         for (int j = 0; j < RPWV; j++) {
             const int y = y0 + RPWV * wv + j;
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     }
     // rows of a 16-B multiple: every row starts at the same offset inside its first chunk
     const bool rows16 = (w * 3) % 16 == 0;
-    auto gray_stage = [&](const uint8_t* rawb, uint16_t* Hb, size_t f) {
+    auto gray_stage = [&](const uint8_t* rawb, uint16_t* Hb, size_t f) __attribute__((always_inline)) {
         const uint32_t flo = (uint32_t)(uintptr_t)(a.src + f * fbytes);
         uint32_t g4[NIT];
         bool slow = false;
@@ -463,21 +476,21 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
                 const uint32_t h1 = htap<1, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h2 = htap<2, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h3 = htap<3, OFF, NG, 0, NQW>(qv, cpk, 0u);
-                uint16_t* hc = Hb + (4 * q) * g.RSH + gyc[it];
-                hc[0] = (uint16_t)h0;
-                hc[g.RSH] = (uint16_t)h1;
-                hc[2 * g.RSH] = (uint16_t)h2;
-                hc[3 * g.RSH] = (uint16_t)h3;
+                // row-major: one conflict-free 8-B store of the quad's four taps
+                *reinterpret_cast<uint2*>(Hb + gyc[it] * g.RSH + 4 * q) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
             }
         }
     };
-    auto stage_raw = [&](const Raw<NCH>& Rr, int buf) { store_raw(Rr, raw + buf * g.raw_bytes, g, tid); };
+    auto stage_raw = [&](const Raw<NCH>& Rr, int buf) __attribute__((always_inline)) { store_raw(Rr, raw + buf * g.raw_bytes, g, tid); };
 
     // Software pipeline, one barrier per frame: iteration t runs the chain of
     // frame t (H buffer t&1) and the gray/horizontal stage of frame t+1 (raw and
     // H buffers (t+1)&1), while frame t+2's raw tile is in flight into registers.
     const int t0 = a.t_begin, t1 = a.t_end;
-    const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);  // profiling-only ablation (FM_DEBUG_SKIP)
+    // profiling-only stage ablation (FM_DEBUG_SKIP bits; results invalid), 0 in normal use.
+    // Kept as a runtime test on purpose: its branches bound the scheduler's live ranges
+    // (117 VGPRs, measured 3 % faster than the branch-free build capped at 128)
+    const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
     Raw<NCH> Rw;
     load_raw(Rw, a.src + ((size_t)t0 * S + s) * fbytes, fb32, plan, span);
     stage_raw(Rw, 0);
@@ -485,52 +498,41 @@ __global__ __launch_bounds__(NT) void k_pix(FusedArgs a) {
     lds_barrier();
     gray_stage(raw, Hs, (size_t)t0 * S + s);
 
-    for (int t = t0; t < t1; t++) {
-        const int b = (t - t0) & 1;
-        const size_t f = (size_t)t * S + s;
-        if (t + 1 < t1) {
-            if (!(skip & 8)) stage_raw(Rw, b ^ 1);
-            if (t + 2 < t1 && !(skip & 4)) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
-        }
-        lds_barrier();
-
-        // ---- vertical taps + chain for the wave's 8 rows; threshold bits by ballot
-        uint64_t mybits = 0;
-        // launder the per-tile uniforms each frame: otherwise LICM hoists dozens of
-        // per-row exec masks out of the frame loop and they spill
-        ChainCtx ccf = cc;
-        int x0f = x0, y0f = y0, wvf = wv;
-        if constexpr (NT == 512) asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-        asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-        if (!(skip & 2)) {
-            const uint16_t* Hb = Hs + b * (g.H_bytes / 2);
-            const bool fi = init0 && t == t0;
-            if (!ccf.vec)
-                chain_rows<KC, PLANES, INIT, true, true>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
-            else if (ccf.hk)
-                chain_rows<KC, PLANES, INIT, true, false>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
-            else
-                chain_rows<KC, PLANES, INIT, false, false>(a, Hb, g, bg, wvf, ln, x0f, y0f, f, ccf, fi, mybits);
-        }
-        if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
-        {   // where the tile has threshold bits (decides the contour pass's candidate tiles)
-            uint32_t fl = 0;
-            if (ln < RPWV && mybits) {
-                const int row = RPWV * wv + ln;
-                const bool l = (mybits & 3ull) != 0, r = (mybits >> 62) != 0;
-                fl = FLAG_ANY | (l ? FLAG_L : 0u) | (r ? FLAG_R : 0u);
-                if (row < 2) fl |= FLAG_T | (l ? FLAG_TL : 0u) | (r ? FLAG_TR : 0u);
-                if (row >= TS - 2) fl |= FLAG_B | (l ? FLAG_BL : 0u) | (r ? FLAG_BR : 0u);
+    // the chain variant is fixed per wave for the whole launch: one loop instance each
+    auto frame_loop = [&](auto keepc, auto tailc, const ChainCtx ccv) __attribute__((always_inline)) {
+        constexpr bool KEEP = decltype(keepc)::value != 0, TAIL = decltype(tailc)::value != 0;
+        for (int t = t0; t < t1; t++) {
+            const int b = (t - t0) & 1;
+            const size_t f = (size_t)t * S + s;
+            if (t + 1 < t1) {
+                if (!(skip & 8)) stage_raw(Rw, b ^ 1);
+                if (t + 2 < t1 && !(skip & 4)) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
             }
-            fl |= __shfl_xor(fl, 1, 64);
-            fl |= __shfl_xor(fl, 2, 64);
-            fl |= __shfl_xor(fl, 4, 64);
-            if (ln == 0 && fl) atomicOr(&a.tflag[f * a.ntiles + ti], fl);
-        }
+            if (!(skip & 16)) lds_barrier();
 
-        if (t + 1 < t1 && !(skip & 1))
-            gray_stage(raw + (b ^ 1) * g.raw_bytes, Hs + (b ^ 1) * (g.H_bytes / 2), f + S);
-    }
+            // ---- vertical taps + chain for the wave's 8 rows; threshold bits by ballot
+            uint64_t mybits = 0;
+            uint32_t fl = 0;
+            // launder the per-tile uniforms each frame: otherwise LICM hoists dozens of
+            // per-row exec masks out of the frame loop and they spill
+            ChainCtx ccf = ccv;
+            ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+            int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv;
+            if constexpr (NT == 512) asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+            if (!(skip & 2))
+                chain_rows<KC, PLANES, INIT, KEEP, TAIL>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf,
+                                                         init0 && t == t0, mybits, fl);
+            if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
+            if (ln == 0 && fl) atomicOr(&a.tflag[f * a.ntiles + ti], fl);
+
+            if (t + 1 < t1 && !(skip & 1))
+                gray_stage(raw + (b ^ 1) * g.raw_bytes, Hs + (b ^ 1) * (g.H_bytes / 2), f + S);
+        }
+    };
+    if (!cc.vec) frame_loop(IntC<1>{}, IntC<1>{}, cc);
+    else if (cc.hk) frame_loop(IntC<1>{}, IntC<0>{}, cc);
+    else frame_loop(IntC<0>{}, IntC<0>{}, cc);
 
     // background out (ping-pong: neighbours never read this batch's update)
     double* bgo = a.bg_out + (size_t)s * plane;

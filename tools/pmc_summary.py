@@ -9,7 +9,7 @@ from collections import defaultdict
 
 def main(d):
     acc = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"].split("(")[0]
