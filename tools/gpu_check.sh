@@ -2,7 +2,7 @@
 # Parity tests + bench summary on the GPU box.  Usage: tools/gpu_check.sh <tag> [bench args...]
 TAG=${1:-chk}; shift
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/parity_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/parity_$TAG.log 2>&1
 RC=$?
 tail -3 gpurun_out/parity_$TAG.log
 [ $RC -ne 0 ] && { grep -E "Error|assert|FAILED|error" gpurun_out/parity_$TAG.log | head -30; exit $RC; }

@@ -5,7 +5,7 @@ set -o pipefail
 TAG=${1:-run}; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/parity_$TAG.log 2>&1 || { tail -40 gpurun_out/parity_$TAG.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/parity_$TAG.log 2>&1 || { tail -40 gpurun_out/parity_$TAG.log; exit 1; }
 tail -3 gpurun_out/parity_$TAG.log
 timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_$TAG.log; exit 1; }
 tail -1 gpurun_out/bench_$TAG.log
