@@ -49,6 +49,19 @@ def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
     return None
 
 
+def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None]:
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/traffic.json,
+    written by tools/traffic.py from FETCH_SIZE / WRITE_SIZE passes of this same workload), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("workload") != cfg["workload"] or kernel not in t.get("kernels", {}):
+        return None, None
+    return int(t["kernels"][kernel]["traffic_bytes"]), t.get("source")
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -90,7 +103,7 @@ def main() -> None:
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
     ap.add_argument("--batch", type=int, default=32, help="frames per stream per step")
     ap.add_argument("--ring", type=int, default=64, help="device-resident frames per stream")
-    ap.add_argument("--cpu-frames", type=int, default=8)
+    ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
     ap.add_argument("--no-ktimes", action="store_true", help="no HIP event timing at all (no roofline)")
@@ -182,9 +195,12 @@ def main() -> None:
         nbytes = algorithmic_bytes(dom, cfg)
         if nbytes is not None and avg_s > 0:
             ach = nbytes / avg_s / 1e9
+            traffic, tsrc = pmc_traffic(dom, cfg)
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3)}
+            if traffic is not None:
+                roof["traffic_source"] = f"{tsrc}: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 16-B read correction)"
 
     # measured device copy peak (for reference beside the spec)
     try:

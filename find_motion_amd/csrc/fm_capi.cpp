@@ -112,6 +112,7 @@ struct fm_ctx {
     std::vector<uint8_t> bg_init, has_keep;
     std::string err;
     uint64_t* d_ts = nullptr;     // FM_TS: contour-pass phase stamps (profiling)
+    uint64_t* d_pts = nullptr;    // FM_PTS=<file>: k_pix workgroup stamps of the last launch (profiling)
     std::vector<double> ts_sum;   // summed phase deltas (cycles)
     std::vector<int64_t> ts_n;
     bool serial = false;  // FM_SERIAL: contour pass on the pixel stream (profiling: no overlap)
@@ -452,6 +453,10 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->has_keep.assign(S, 0);
     if (const char* e = std::getenv("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
     c->serial = std::getenv("FM_SERIAL") != nullptr;
+    if (std::getenv("FM_PTS") && c->use_pix) {
+        if ((rc = dalloc(cp, &c->d_pts, (size_t)S * c->ntiles * 4))) return rc;
+        HIP_TRY(cp, hipMemset(c->d_pts, 0, (size_t)S * c->ntiles * 4 * sizeof(uint64_t)));
+    }
     if (std::getenv("FM_TS") && c->use_fused) {
         if ((rc = dalloc(cp, &c->d_ts, frames * c->ntiles * 16))) return rc;
         c->ts_sum.assign(16, 0.0);
@@ -466,6 +471,18 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 
 void fm_destroy(fm_ctx* c) {
     if (!c) return;
+    if (c->d_pts) {  // profiling: per-workgroup (hw_id, xcc_id, realtime start/end, memtime start/end) of the last k_pix
+        const size_t n = (size_t)c->p.n_streams * c->ntiles * 4;
+        std::vector<uint64_t> v(n);
+        if (hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(v.data(), c->d_pts, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess) {
+            if (FILE* fh = std::fopen(std::getenv("FM_PTS"), "wb")) {
+                std::fwrite(v.data(), sizeof(uint64_t), n, fh);
+                std::fclose(fh);
+            }
+        }
+        dfree(c->d_pts);
+    }
     if (c->d_ts) {
         std::fprintf(stderr, "[fm] contour-pass phase cycles (mean per labelled tile):");
         for (int k = 2; k < 16; k++)
@@ -626,6 +643,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.acc_vec_end = npx - npx % 16;
         fa.dbg_skip = c->dbg_skip;
         fa.dbg_ts = c->d_ts;
+        fa.dbg_pts = c->d_pts;
         if (c->d_ts) HIP_TRY(c, hipMemsetAsync(c->d_ts, 0, F * c->ntiles * 16 * sizeof(uint64_t), ps));
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
         fa.t_begin = 0;

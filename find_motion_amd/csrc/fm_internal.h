@@ -107,6 +107,7 @@ struct FusedArgs {
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
+    uint64_t* dbg_pts;           // profiling-only k_pix workgroup stamps [S][ntiles][4] (FM_PTS); nullptr in normal use
     double alpha, beta;
     long long acc_vec_end;
     int32_t coef[kMaxK];

@@ -329,6 +329,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
     const int ti = swizzle_tile(blockIdx.x, a.ntiles);
+    // profiling only (FM_PTS): [hw_id | xcc_id << 32, realtime start, realtime end, memtime cycles]
+    uint64_t* pts = (a.dbg_pts && tid == 0) ? a.dbg_pts + ((size_t)s * a.ntiles + ti) * 4 : nullptr;
+    uint64_t rt0 = 0, mt0 = 0;
+    if (pts) {
+        pts[0] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        mt0 = __builtin_amdgcn_s_memtime();
+    }
     const int h = a.h, w = a.w, S = a.S;
     const int tx = ti % a.ntx, ty = ti / a.ntx;
     const int x0 = tx * TS, y0 = ty * TS;
@@ -390,7 +398,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
     // loaded columns (only the quads over a reflected image edge take the gather path)
     const int qc = gx0 + 4 * q;
     const bool qin = qc >= cx0 && qc + 4 <= cx1;
-    const int qoff = 3 * (qc - cx0);
+    // Quads over a reflected image edge (R <= 4, w % 4 == 0, w >= 8): the one quad just
+    // outside the image on each side is rebuilt from the two mirrored inside quads by
+    // lane shuffles (reflq 1 = left, 2 = right); quads further out feed only columns past
+    // the image and keep whatever they read.  Those lanes read a clamped in-row quad.
+    // Other geometries take the per-pixel gather below.
+    const bool shfix = PCc == 4 && (w & 3) == 0 && w >= 8;
+    const int reflq = !shfix ? 0 : qc == -4 ? 1 : qc == w ? 2 : 0;
+    const bool qok = qin || (shfix && (reflq != 0 || qc >= w + 4));
+    const int qoff = 3 * ((qin || !qok ? qc : qc < 0 ? cx0 : cx1 - 4) - cx0);
+    const bool has_refl = shfix && (x0 == 0 || gx0 + g.GW > w);  // workgroup-uniform
     uint32_t cpk[NG];
 #pragma unroll
     for (int gi = 0; gi < NG; gi++) cpk[gi] = tap4<KC>(gi);
@@ -423,7 +440,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
         // straight-line over the iterations so their LDS round trips overlap
         if (rows16) {
             const uint32_t ro = (flo + 3u * (uint32_t)cx0) & 15u;  // uniform
-            slow = act[0] && !(qin && ((ro + (uint32_t)qoff) & 3u) == 0);
+            slow = act[0] && !(qok && ((ro + (uint32_t)qoff) & 3u) == 0);
 #pragma unroll
             for (int it = 0; it < NIT; it++) {
                 const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + ((loff[it] + ro) & ~3u));
@@ -434,7 +451,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
             for (int it = 0; it < NIT; it++) {
                 const uint32_t ro = (flo + rowbyte[it]) & 15u;  // row start inside its first 16-B chunk
                 const uint32_t off = loff[it] + ro;
-                slow |= act[it] && !(qin && (off & 3u) == 0);
+                slow |= act[it] && !(qok && (off & 3u) == 0);
                 const uint32_t* p32 = reinterpret_cast<const uint32_t*>(rawb + (off & ~3u));
                 g4[it] = gray4(p32[0], p32[1], p32[2]);
             }
@@ -444,12 +461,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
             for (int it = 0; it < NIT; it++) {
                 const uint32_t ro = (flo + rowbyte[it]) & 15u;
                 const uint32_t off = loff[it] + ro;
-                if (act[it] && !(qin && (off & 3u) == 0)) {
+                if (act[it] && !(qok && (off & 3u) == 0)) {
                     const uint8_t* rowp = rawb + gyc[it] * g.RS + ro;
                     const int c0 = 4 * q;
                     g4[it] = gray1(rowp + colx[c0]) | (gray1(rowp + colx[c0 + 1]) << 8) |
                              (gray1(rowp + colx[c0 + 2]) << 16) | (gray1(rowp + colx[c0 + 3]) << 24);
                 }
+            }
+        }
+        if (has_refl) {  // reflected edge quads from the mirrored inside quads (see reflq)
+            const int d = reflq == 1 ? 1 : reflq == 2 ? -1 : 0;
+            const uint32_t sel = reflq == 1 ? 0x01020304u : 0x07000102u;
+#pragma unroll
+            for (int it = 0; it < NIT; it++) {
+                const uint32_t A = (uint32_t)__builtin_amdgcn_ds_bpermute((ln + d) << 2, (int)g4[it]);
+                const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute((ln + 2 * d) << 2, (int)g4[it]);
+                if (reflq) g4[it] = __builtin_amdgcn_perm(B, A, sel);
             }
         }
 #pragma unroll
@@ -541,6 +568,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
     for (int j = 0; j < RPWV; j++) {
         const int y = y0 + RPWV * wv + j;
         if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+    }
+    if (pts) {
+        const uint64_t rt = __builtin_amdgcn_s_memrealtime(), mt = __builtin_amdgcn_s_memtime();
+        pts[1] = rt0;
+        pts[2] = rt;
+        pts[3] = mt - mt0;
     }
 }
 

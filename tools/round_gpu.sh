@@ -12,3 +12,4 @@ tail -1 gpurun_out/bench_$TAG.log
 tools/profile.sh $TAG "$@" || exit 1
 python tools/pmc_summary.py gpurun_out/prof_$TAG > gpurun_out/pmc_$TAG.txt 2>&1
 cat gpurun_out/pmc_$TAG.txt
+python tools/traffic.py gpurun_out/prof_$TAG gpurun_out/bench_$TAG.log $TAG > /dev/null || echo "traffic extraction failed"

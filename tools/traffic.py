@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of each kernel from rocprofv3 PMC passes -> profiles/traffic.json.
+
+Usage: tools/traffic.py <prof_dir> <bench_log> <tag>
+  prof_dir  : tools/profile.sh output (pmc*/ passes with FETCH_SIZE and WRITE_SIZE)
+  bench_log : the bench.py JSON line of the same workload (its config.workload keys the entry)
+
+Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the
+bytes of a 16-B-per-lane streaming read; the pixel kernel's dominant reads are
+global_load_dwordx4 BGR chunks, so traffic = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).
+bench.py reports this as roofline.traffic when its workload matches.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+SHORT = {"k_pix": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit",
+         "k_regions": "regions", "k_resize_area": "resize_area", "k_pixel": "pixel"}
+
+
+def short(name):
+    base = name.split("(")[0]
+    for k, v in SHORT.items():
+        if base.split("<")[0].endswith(k):
+            return v
+    return None
+
+
+def main(prof, bench_log, tag):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(prof, "**", "*counter_collection.csv"), recursive=True)):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row["Kernel_Name"]
+                if "k_pix<" in k and ", true>" in k:  # the init-frame variant is a one-off
+                    continue
+                s = short(k)
+                if s and row["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+                    acc[s][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    line = [l for l in open(bench_log).read().splitlines() if l.startswith("{")][-1]
+    workload = json.loads(line)["config"]["workload"]
+    out = {"tag": tag, "workload": workload, "source": f"profiles/{tag}_pmc.txt", "kernels": {}}
+    for k, cs in acc.items():
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024
+        write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
+        out["kernels"][k] = {"fetch_size_bytes": round(fetch), "write_size_bytes": round(write),
+                             "traffic_bytes": round(2 * fetch + write), "dispatches": len(cs["FETCH_SIZE"])}
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
