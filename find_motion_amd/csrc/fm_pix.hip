@@ -36,6 +36,9 @@ constexpr int TS = 64;          // tile edge
 #ifndef FM_PIX_NT
 #define FM_PIX_NT 512
 #endif
+#ifndef FM_PIX_PRIO
+#define FM_PIX_PRIO 0
+#endif
 constexpr int NT = FM_PIX_NT;   // threads
 constexpr int NW = NT / 64;     // waves; wave w owns tile rows [8w, 8w + 8)
 constexpr int RPWV = TS / NW;   // rows per wave in the chain stage
@@ -531,6 +534,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
         for (int t = t0; t < t1; t++) {
             const int b = (t - t0) & 1;
             const size_t f = (size_t)t * S + s;
+#if FM_PIX_PRIO
+            // two workgroups share each CU; by age the first-dispatched one wins issue and the
+            // second finishes alone at one wave per SIMD.  Priority falling with progress keeps
+            // the pair within a quarter batch of each other.
+            {
+                const int q4 = ((t - t0) * 4) / (t1 - t0);
+                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
+                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
+                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
             if (t + 1 < t1) {
                 if (!(skip & 8)) stage_raw(Rw, b ^ 1);
                 if (t + 2 < t1 && !(skip & 4)) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
