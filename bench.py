@@ -101,7 +101,7 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
-    ap.add_argument("--batch", type=int, default=32, help="frames per stream per step")
+    ap.add_argument("--batch", type=int, default=64, help="frames per stream per step (one pixel-kernel launch)")
     ap.add_argument("--ring", type=int, default=64, help="device-resident frames per stream")
     ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -84,6 +84,11 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+// v_writelane_b32 through the LLVM intrinsic (HIP has no builtin).  Not inline asm: the
+// source SGPR is often VCC just written by the compare, and only a compiler-visible
+// operand gets the VALU-writes-SGPR -> VALU-reads-it wait states (inline asm here read a
+// stale VCC whenever no SALU op happened to sit between the two)
+__device__ int fm_writelane(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 template <int I> struct IntC { static constexpr int value = I; };
 // compile-time unrolled loop: fn(IntC<0>{}), ..., fn(IntC<N-1>{})
@@ -299,8 +304,8 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         orr |= bm;
         if (j < 2) top |= bm;
         if (j >= RPWV - 2) bot |= bm;
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_lo) : "s"((uint32_t)bm), "n"(j));
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(mb_hi) : "s"((uint32_t)(bm >> 32)), "n"(j));
+        mb_lo = fm_writelane((int)(uint32_t)bm, j, mb_lo);
+        mb_hi = fm_writelane((int)(uint32_t)(bm >> 32), j, mb_hi);
         if (PLANES && rv && ((cc.colmask >> ln) & 1)) {
             const size_t plane = (size_t)a.h * w;
             const size_t li = (size_t)(y0 + RPWV * wv + j) * w + x0 + ln;
@@ -606,7 +611,10 @@ static bool taps_match(const FusedArgs& a) {
 }
 
 hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init) {
-    const int bytes = px::Geo(a.ksize >> 1).bytes;
+#ifndef FM_PIX_LDS_PAD
+#define FM_PIX_LDS_PAD 0  // diagnostics only: extra LDS per workgroup (limits workgroups per CU)
+#endif
+    const int bytes = px::Geo(a.ksize >> 1).bytes + FM_PIX_LDS_PAD;
     const bool ok = a.ksize == 3 ? taps_match<3>(a) : a.ksize == 5 ? taps_match<5>(a) : a.ksize == 7 ? taps_match<7>(a)
                   : a.ksize == 21 ? taps_match<21>(a) : false;
     if (!ok) return hipErrorInvalidValue;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Each abvar/ variant: serial pixel-kernel time, then three pipelined bench values (noise check).
+set -o pipefail
+mkdir -p gpurun_out
+for D in abvar/*/; do
+  N=$(basename $D)
+  FM_HIP_LIB=$PWD/$D/libfm_hip.so FM_SERIAL=1 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 --warmup 2 "$@" > gpurun_out/ab_$N.log 2>&1 || { tail -3 gpurun_out/ab_$N.log; exit 1; }
+  L="$N serial_pix $(tail -1 gpurun_out/ab_$N.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["kernels"]["pix"]["avg_us"])') pipelined"
+  for i in 1 2 3; do
+    FM_HIP_LIB=$PWD/$D/libfm_hip.so timeout -k 10 120 python bench.py --no-cpu-baseline --steps 40 --warmup 3 "$@" > gpurun_out/abp_$N.log 2>&1 || { tail -3 gpurun_out/abp_$N.log; exit 1; }
+    L="$L $(tail -1 gpurun_out/abp_$N.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1000,1))')k"
+  done
+  echo "$L"
+done

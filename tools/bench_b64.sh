@@ -1,0 +1,10 @@
+#!/bin/bash
+# Batch 64 from the same 64-frame ring as the default bench (pipelined and serial).
+set -o pipefail
+mkdir -p gpurun_out
+for B in 32 64; do for MODE in pipe serial; do
+  E=""; [ $MODE = serial ] && E="FM_SERIAL=1"
+  env $E timeout -k 10 120 python bench.py --no-cpu-baseline --batch $B --ring 64 --steps $((640/B)) --warmup 2 "$@" > gpurun_out/b64_${MODE}_$B.log 2>&1 || { tail -5 gpurun_out/b64_${MODE}_$B.log; exit 1; }
+  tail -1 gpurun_out/b64_${MODE}_$B.log | python -c "
+import json,sys; d=json.loads(sys.stdin.read()); print('batch $B $MODE', d['value'], d['kernels']['pix'])"
+done; done
