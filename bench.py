@@ -100,6 +100,8 @@ def main() -> None:
                     help="F: -B 1920 -b 384 (full-resolution fused kernel); D: reference default -B 100 -b 20")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--blur-scale", type=int, default=None,
+                    help="-b override (config 5: --width 3840 --height 2160 --blur-scale 183 -> k 21)")
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
     ap.add_argument("--batch", type=int, default=64, help="frames per stream per step (one pixel-kernel launch)")
     ap.add_argument("--ring", type=int, default=64, help="device-resident frames per stream")
@@ -128,6 +130,8 @@ def main() -> None:
     box, blur_scale = (W, W // 5) if args.mode == "F" else (100, 20)
     if args.mode == "F" and W == 1920:
         blur_scale = 384
+    if args.blur_scale is not None:
+        blur_scale = args.blur_scale
     k = make_gaussian(box, blur_scale)
     S, T = args.streams, args.batch
     R = max(args.ring - args.ring % T, T)

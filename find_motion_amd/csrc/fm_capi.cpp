@@ -60,7 +60,7 @@ struct BatchSlot {
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
-    hipEvent_t ev_pix = nullptr, ev_done = nullptr;
+    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr;
     hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
     uint64_t gen = 0;               // submits into this slot
@@ -77,6 +77,7 @@ struct fm_ctx {
 
     // streams: pixel work (caller-replaceable), contour pass, synchronous reads
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
+    hipStream_t rs_stream = nullptr;  // modes with a resize: input copy + resize, ahead of the pixel stream
     hipStream_t ccl_streams[kSlots] = {};
     int nccl = 1;
     KernelTimer timer;
@@ -368,6 +369,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
     }
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    if (c->rmode != ResizeMode::Identity && !std::getenv("FM_RESIZE_INLINE"))
+        HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
@@ -428,6 +431,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         b.ccl_stream = c->ccl_streams[i % c->nccl];
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
+        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_rs, hipEventDisableTiming));
     }
     // pixel-level CCL: the whole batch on the v1 path, one frame for the fused path's overflow fallback
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
@@ -491,7 +495,7 @@ void fm_destroy(fm_ctx* c) {
         dfree(c->d_ts);
     }
     (void)hipSetDevice(c->p.device);
-    for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream})
+    for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamSynchronize(st);
     for (hipStream_t& st : c->ccl_streams)
         if (st) {
@@ -507,11 +511,12 @@ void fm_destroy(fm_ctx* c) {
             if (hp) (void)hipHostFree(hp);
         if (b.ev_pix) (void)hipEventDestroy(b.ev_pix);
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
+        if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
-    for (hipStream_t st : {c->own_stream, c->aux_stream})
+    for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamDestroy(st);
     delete c;
 }
@@ -567,29 +572,37 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     BatchSlot& B = c->slots[si];
     const int S = c->p.n_streams;
     const size_t F = (size_t)n * S;
-    hipStream_t ps = c->stream;  // pixel stream: input, resize, pixel kernel (bg recurrence is ordered here)
+    hipStream_t ps = c->stream;  // pixel stream: pixel kernel (bg recurrence is ordered here)
+    // input copy and resize: on their own stream when there is a resize, so batch i+1's
+    // resize (many workgroups, HBM-bound) overlaps batch i's pixel kernel (few, when the
+    // work image is small); the pixel stream waits for it below
+    hipStream_t rs = c->rs_stream ? c->rs_stream : ps;
     const uint8_t* src = frames;
     if (!on_device) {
         if (!B.d_in) {
             int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
             if (rc) return rc;
         }
-        HIP_TRY(c, hipMemcpyAsync(B.d_in, frames, F * c->src_frame_bytes, hipMemcpyHostToDevice, ps));
+        HIP_TRY(c, hipMemcpyAsync(B.d_in, frames, F * c->src_frame_bytes, hipMemcpyHostToDevice, rs));
         src = B.d_in;
     }
     const uint8_t* work = src;
     if (c->rmode == ResizeMode::General) {
-        int tok = c->timer.begin("resize_area", ps);
-        HIP_TRY(c, launch_resize_area(ps, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->d_xofs, c->d_xcnt,
+        int tok = c->timer.begin("resize_area", rs);
+        HIP_TRY(c, launch_resize_area(rs, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->d_xofs, c->d_xcnt,
                                       c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt, c->d_ywt, c->ay.max_taps));
         c->timer.end(tok);
         work = B.d_work;
     } else if (c->rmode == ResizeMode::Fast) {
-        int tok = c->timer.begin("resize_area_fast", ps);
-        HIP_TRY(c, launch_resize_area_fast(ps, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->fast_sx,
+        int tok = c->timer.begin("resize_area_fast", rs);
+        HIP_TRY(c, launch_resize_area_fast(rs, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->fast_sx,
                                            c->fast_sy));
         c->timer.end(tok);
         work = B.d_work;
+    }
+    if (rs != ps) {
+        HIP_TRY(c, hipEventRecord(B.ev_rs, rs));
+        HIP_TRY(c, hipStreamWaitEvent(ps, B.ev_rs, 0));
     }
     bool any_init = false;
     for (int s = 0; s < S; s++) {

@@ -67,6 +67,97 @@ __global__ __launch_bounds__(256) void k_resize_area(const uint8_t* __restrict__
     }
 }
 
+// INTER_AREA, general path, staged: one workgroup per (destination row, frame) walks
+// that row's source rows in ytab order.  Each source row (3*W bytes) is read once with
+// coalesced 16-B loads into LDS (double buffered: row j+1 is in flight into registers
+// while row j is summed), the x weights sit in LDS for the whole walk, and thread e keeps
+// the running sums of its destination elements (dx, c) = (e / 3, e % 3) in registers.
+// The float chain per element is k_resize_area's, in the same order, so the bytes are
+// identical.  Limits (else k_resize_area): 3*W % 16 == 0, 16-B aligned frames,
+// 3*W <= RS_MAXROW, w*3 <= 256 * RS_EPT, w * xtaps floats <= RS_MAXWT.
+constexpr int RS_T = 256, RS_EPT = 8, RS_CPT = 4;
+constexpr int RS_MAXROW = RS_T * RS_CPT * 16;
+constexpr int RS_MAXWT = 8192;
+__global__ __launch_bounds__(RS_T) void k_resize_area_rows(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                           int H, int W, int h, int w, const int32_t* __restrict__ xofs,
+                                                           const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
+                                                           int xtaps, const int32_t* __restrict__ yofs,
+                                                           const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
+                                                           int ytaps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int rowb = 3 * W;                        // multiple of 16
+    uint8_t* rows = lds;                           // [2][rowb]
+    float* wt = reinterpret_cast<float*>(lds + 2 * rowb);  // [w][xtaps]
+    const int dy = blockIdx.x;
+    const size_t f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const uint8_t* S0 = src + f * (size_t)H * rowb;
+    for (int i = tid; i < w * xtaps; i += RS_T) wt[i] = xwt[i];
+    const int sy0 = yofs[dy], ny = ycnt[dy];
+    const int nch = rowb / 16;
+    uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;  // row prefetch (RS_CPT = 4 chunks)
+    static_assert(RS_CPT == 4, "prefetch registers");
+#define RS_LOAD_ROW(J)                                                                          \
+    do {                                                                                        \
+        const uint4* R_ = reinterpret_cast<const uint4*>(S0 + (size_t)(sy0 + (J)) * rowb);     \
+        if (tid < nch) p0 = R_[tid];                                                            \
+        if (tid + RS_T < nch) p1 = R_[tid + RS_T];                                              \
+        if (tid + 2 * RS_T < nch) p2 = R_[tid + 2 * RS_T];                                      \
+        if (tid + 3 * RS_T < nch) p3 = R_[tid + 3 * RS_T];                                      \
+    } while (0)
+#define RS_STORE_ROW(B)                                                                         \
+    do {                                                                                        \
+        uint4* L_ = reinterpret_cast<uint4*>(rows + (B) * rowb);                                \
+        if (tid < nch) L_[tid] = p0;                                                            \
+        if (tid + RS_T < nch) L_[tid + RS_T] = p1;                                              \
+        if (tid + 2 * RS_T < nch) L_[tid + 2 * RS_T] = p2;                                      \
+        if (tid + 3 * RS_T < nch) L_[tid + 3 * RS_T] = p3;                                      \
+    } while (0)
+    const int ne = w * 3;
+    int sx0[RS_EPT], nx[RS_EPT], c3[RS_EPT];
+    float sum[RS_EPT];
+#pragma unroll
+    for (int k = 0; k < RS_EPT; k++) {
+        const int e = tid + RS_T * k;
+        const int dx = e < ne ? e / 3 : 0;
+        sx0[k] = xofs[dx];
+        nx[k] = e < ne ? xcnt[dx] : 0;
+        c3[k] = dx * xtaps;                   // weight row
+        sum[k] = 0.f;
+        sx0[k] = sx0[k] * 3 + (e < ne ? e - dx * 3 : 0);  // byte of tap 0 in the row
+    }
+    const float* wy = ywt + (size_t)dy * ytaps;
+    RS_LOAD_ROW(0);
+    for (int j = 0; j < ny; j++) {
+        const int b = j & 1;
+        __syncthreads();  // buffer b is free (row j-2 summed) and the weights are in
+        RS_STORE_ROW(b);
+        if (j + 1 < ny) RS_LOAD_ROW(j + 1);
+        __syncthreads();
+        const uint8_t* L = rows + b * rowb;
+        const float wyj = wy[j];
+#pragma unroll
+        for (int k = 0; k < RS_EPT; k++) {
+            if (RS_T * k < ne) {  // wave-uniform
+                float buf = 0.f;
+                const uint8_t* Lp = L + sx0[k];
+                const float* wp = wt + c3[k];
+                for (int t = 0; t < nx[k]; t++) buf = __fadd_rn(buf, __fmul_rn((float)Lp[3 * t], wp[t]));
+                const float term = __fmul_rn(wyj, buf);
+                sum[k] = (j == 0) ? term : __fadd_rn(sum[k], term);
+            }
+        }
+    }
+    uint8_t* D = dst + (f * h + dy) * (size_t)ne;
+#pragma unroll
+    for (int k = 0; k < RS_EPT; k++) {
+        const int e = tid + RS_T * k;
+        if (e < ne) D[e] = sat_u8(__float2int_rn(sum[k]));
+    }
+#undef RS_LOAD_ROW
+#undef RS_STORE_ROW
+}
+
 // INTER_AREA integer-scale path (resizeAreaFast): 2x2 => (sum+2)>>2,
 // otherwise cvRound(sum * (1.f/area)).
 __global__ __launch_bounds__(256) void k_resize_area_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -88,8 +179,17 @@ hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, 
                               const int32_t* xofs, const int32_t* xcnt, const float* xwt, int xtaps,
                               const int32_t* yofs, const int32_t* ycnt, const float* ywt, int ytaps) {
     dim3 grid(h, F);
-    hipLaunchKernelGGL(k_resize_area, grid, dim3(256), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs,
-                       ycnt, ywt, ytaps);
+    const int rowb = 3 * W;
+    if (rowb % 16 == 0 && ((uintptr_t)src & 15) == 0 && rowb <= RS_MAXROW && w * 3 <= RS_T * RS_EPT &&
+        w * xtaps <= RS_MAXWT) {
+        const int bytes = 2 * rowb + w * xtaps * 4;
+        (void)hipFuncSetAttribute((const void*)k_resize_area_rows, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(k_resize_area_rows, grid, dim3(RS_T), bytes, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps,
+                           yofs, ycnt, ywt, ytaps);
+    } else {
+        hipLaunchKernelGGL(k_resize_area, grid, dim3(256), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs,
+                           ycnt, ywt, ytaps);
+    }
     return hipGetLastError();
 }
 
