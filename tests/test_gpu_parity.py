@@ -78,6 +78,14 @@ def test_mode_d_1080p():
     run_pair(1920, 1080, 100, T=4, n_batches=2)
 
 
+def test_mode_d_resize_paths():
+    # staged INTER_AREA (3*W % 16 == 0) with a ragged last tap, the plain kernel (3*W % 16 != 0),
+    # two streams through the resize stream
+    run_pair(336, 200, 100, T=3, n_batches=2)
+    run_pair(642, 481, 100, T=2, n_batches=2)
+    run_pair(640, 480, 100, S=2, T=2, n_batches=2)
+
+
 def test_mode_f_1080p_k5():
     run_pair(1920, 1080, 1920, blur_scale=384, T=2, n_batches=2)
 
