@@ -409,7 +409,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
         if (c->use_fused) {
             if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
-                (rc = dalloc(cp, &b.d_tflag, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_candf, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_tflag, frames * c->ntiles * 8)) || (rc = dalloc(cp, &b.d_candf, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_clist, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_rlist, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_regrep, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_ncr, frames * 2)) ||
                 (rc = dalloc(cp, &b.d_dbits, frames * c->ntiles * 64)) ||
@@ -425,7 +425,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_count, b.h_count, 0));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_overflow, b.h_overflow, 0));
-        if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * sizeof(uint32_t)));
+        if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * 8 * sizeof(uint32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
         if (i < c->nccl) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
         b.ccl_stream = c->ccl_streams[i % c->nccl];
@@ -628,6 +628,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.dbits = B.d_dbits;
         fa.tiles = B.d_tiles;
         fa.tflag = B.d_tflag;
+        fa.tflag_waves = c->use_pix ? 8 : 1;
         fa.candf = B.d_candf;
         fa.clist = B.d_clist;
         fa.rlist = B.d_rlist;

@@ -115,36 +115,71 @@ __device__ __forceinline__ bool tile_on_border(const FusedArgs& a, int ti) {
 }
 
 // ---------------------------------------------------------------------------
-// dilate(thresh, None, iterations=2) = 5x5 max (fm.py:266) on bit rows, lane = row
-__device__ __forceinline__ uint64_t hdil(uint64_t L, uint64_t C, uint64_t R) {
-    const uint64_t lo = (L >> 62) | (C << 2), hi = (C >> 62) | ((R & 3) << 2);
-    return lo | ((lo >> 1) | (hi << 63)) | ((lo >> 2) | (hi << 62)) | ((lo >> 3) | (hi << 61)) | ((lo >> 4) | (hi << 60));
+// dilate(thresh, None, iterations=2) = 5x5 max (fm.py:266).  The pixel kernel writes each
+// tile's threshold bits column-major (word c = column c, bit r = row r), so the vertical
+// half of the separable dilation is shifts inside a word (the tiles above and below give
+// rows -2, -1 and 64, 65), the horizontal half is lane shuffles (lane = column; the left
+// and right tiles give columns -2, -1 and 64, 65), and one 64x64 bit transpose turns the
+// dilated tile into the row words (lane = row) the run-length labelling walks.
+__device__ __forceinline__ uint64_t vdil(const uint64_t* B, const FusedArgs& a, int t, int ty, int c) {
+    const uint64_t x = B[(size_t)t * 64 + c];
+    uint64_t v = x | (x << 1) | (x << 2) | (x >> 1) | (x >> 2);
+    if (ty > 0) {  // rows -1 (bit 63) and -2 (bit 62) of the tile above
+        const uint64_t u = B[(size_t)(t - a.ntx) * 64 + c];
+        v |= ((u >> 63) ? 3ull : 0ull) | ((u >> 62) & 1ull);
+    }
+    if (ty + 1 < a.nty) {  // rows 64 (bit 0) and 65 (bit 1) of the tile below
+        const uint64_t d = B[(size_t)(t + a.ntx) * 64 + c];
+        v |= ((d & 1ull) ? (3ull << 62) : 0ull) | (((d >> 1) & 1ull) << 63);
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const int lo = __shfl((int)(uint32_t)v, src, 64), hi = __shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// 64x64 bit transpose across the wave: lane k holds word k; afterwards lane r holds the
+// word whose bit c is bit r of the old word c
+__device__ __forceinline__ uint64_t transpose64(uint64_t w, int ln) {
+    const uint64_t masks[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                               0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+    for (int s = 0; s < 6; s++) {
+        const int j = 32 >> s;
+        const uint64_t p = shfl64(w, ln ^ j);
+        if (ln & j) w ^= ((p >> j) ^ w) & masks[s];
+        else w ^= (((w >> j) ^ p) & masks[s]) << j;
+    }
+    return w;
 }
 
 __device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, int ti, int ln, uint64_t* hv) {
+    (void)hv;
     const int tx = ti % a.ntx, ty = ti / a.ntx;
     const uint64_t* B = a.bits + f * (size_t)a.ntiles * 64;
-    auto row = [&](int t, int r) -> uint64_t { return B[(size_t)t * 64 + r]; };
     const bool hl = tx > 0, hr = tx + 1 < a.ntx;
-    hv[ln + 2] = hdil(hl ? row(ti - 1, ln) : 0, row(ti, ln), hr ? row(ti + 1, ln) : 0);
-    if (ln < 4) {  // halo rows -2, -1 (tile above, rows 62, 63) and 64, 65 (tile below, rows 0, 1)
-        const int dy = ln < 2 ? -1 : 1;
-        const int rr = ln < 2 ? 62 + ln : ln - 2;
-        const int tyy = ty + dy;
-        uint64_t v = 0;
-        if (tyy >= 0 && tyy < a.nty) {
-            const int tt = tyy * a.ntx + tx;
-            v = hdil(hl ? row(tt - 1, rr) : 0, row(tt, rr), hr ? row(tt + 1, rr) : 0);
-        }
-        hv[ln < 2 ? ln : 64 + ln] = v;
-    }
-    lds_fence();
-    uint64_t o = hv[ln] | hv[ln + 1] | hv[ln + 2] | hv[ln + 3] | hv[ln + 4];
+    const uint64_t v = vdil(B, a, ti, ty, ln);
+    // columns of the neighbours: lanes 62, 63 hold the left tile's columns 62, 63,
+    // lanes 0, 1 the right tile's columns 0, 1
+    uint64_t e = 0;
+    if (ln >= 62 && hl) e = vdil(B, a, ti - 1, ty, ln);
+    if (ln <= 1 && hr) e = vdil(B, a, ti + 1, ty, ln);
+    const uint64_t vm1 = shfl64(v, (ln + 63) & 63), vm2 = shfl64(v, (ln + 62) & 63);
+    const uint64_t vp1 = shfl64(v, (ln + 1) & 63), vp2 = shfl64(v, (ln + 2) & 63);
+    const uint64_t e62 = shfl64(e, 62), e63 = shfl64(e, 63), e0 = shfl64(e, 0), e1 = shfl64(e, 1);
+    uint64_t o = v;
+    o |= ln >= 1 ? vm1 : e63;
+    o |= ln >= 2 ? vm2 : (ln == 1 ? e63 : e62);
+    o |= ln <= 62 ? vp1 : e0;
+    o |= ln <= 61 ? vp2 : (ln == 62 ? e0 : e1);
+    // columns / rows outside the image are background
     const int x0 = tx * TS, y0 = ty * TS;
-    const int vc = a.w - x0;
-    if (vc < 64) o &= (1ull << vc) - 1;
-    if (y0 + ln >= a.h) o = 0;
-    return o;
+    if (x0 + ln >= a.w) o = 0;
+    const int vr = a.h - y0;
+    if (vr < 64) o &= (1ull << vr) - 1;
+    return transpose64(o, ln);
 }
 
 // ---------------------------------------------------------------------------
@@ -394,21 +429,29 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
 // candidate: the tile's dilated mask can be non-empty.  With threshold bits
 // (dilate) that is: its own bits, or a neighbour's bits within 2 px of the
 // shared edge or corner; with already dilated bits, its own bits.
+// the tile's FLAG_* bits: one word per tile (k_fused), or one per wave of the pixel
+// kernel's workgroup (k_pix writes them with plain stores, no atomics), ORed here
+__device__ __forceinline__ uint32_t tile_flags(const FusedArgs& a, size_t f, int ti) {
+    if (a.tflag_waves == 1) return a.tflag[f * a.ntiles + ti];
+    const uint4* q = reinterpret_cast<const uint4*>(a.tflag + (f * a.ntiles + ti) * 8);
+    const uint4 x = q[0], y = q[1];
+    return x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w;
+}
+
 __device__ __forceinline__ bool is_candidate(const FusedArgs& a, size_t f, int ti, bool dilate) {
-    const uint32_t* fl = a.tflag + f * a.ntiles;
-    if (fl[ti]) return true;
+    if (tile_flags(a, f, ti)) return true;
     if (!dilate) return false;
     const int ntx = a.ntx, tx = ti % ntx, ty = ti / ntx;
     const bool l = tx > 0, r = tx + 1 < ntx, u = ty > 0, d = ty + 1 < a.nty;
     uint32_t m = 0;
-    if (l) m |= fl[ti - 1] & FLAG_R;
-    if (r) m |= fl[ti + 1] & FLAG_L;
-    if (u) m |= fl[ti - ntx] & FLAG_B;
-    if (d) m |= fl[ti + ntx] & FLAG_T;
-    if (u && l) m |= fl[ti - ntx - 1] & FLAG_BR;
-    if (u && r) m |= fl[ti - ntx + 1] & FLAG_BL;
-    if (d && l) m |= fl[ti + ntx - 1] & FLAG_TR;
-    if (d && r) m |= fl[ti + ntx + 1] & FLAG_TL;
+    if (l) m |= tile_flags(a, f, ti - 1) & FLAG_R;
+    if (r) m |= tile_flags(a, f, ti + 1) & FLAG_L;
+    if (u) m |= tile_flags(a, f, ti - ntx) & FLAG_B;
+    if (d) m |= tile_flags(a, f, ti + ntx) & FLAG_T;
+    if (u && l) m |= tile_flags(a, f, ti - ntx - 1) & FLAG_BR;
+    if (u && r) m |= tile_flags(a, f, ti - ntx + 1) & FLAG_BL;
+    if (d && l) m |= tile_flags(a, f, ti + ntx - 1) & FLAG_TR;
+    if (d && r) m |= tile_flags(a, f, ti + ntx + 1) & FLAG_TL;
     return m != 0;
 }
 
@@ -641,7 +684,9 @@ __global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
     const size_t f = blockIdx.x;
     const size_t F = (size_t)a.T * a.S;
     // the tile flags were consumed by k_regions: clear them for the slot's next batch
-    for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
+    // (k_pix rewrites its per-wave flag words every frame: nothing to clear there)
+    if (a.tflag_waves == 1)
+        for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
     if (a.count[F + f]) {  // relabelled by the host's pixel-level fallback
         if (threadIdx.x == 0) {
             a.h_overflow[f] = 1;

@@ -89,7 +89,7 @@ struct FusedArgs {
     uint64_t* dbits;             // [F][ntiles][64] dilated rows (VideoFrame.thresh as bits; == bits when the
                                  // pixel kernel dilates itself, i.e. the generic-k k_fused path)
     TileRec* tiles;              // [F][ntiles]
-    uint32_t* tflag;             // [F][ntiles] FLAG_* bits: where the tile has threshold bits (dilated
+    uint32_t* tflag;             // [F][ntiles][tflag_waves] FLAG_* bits: where the tile has threshold bits (dilated
                                  // bits on the k_fused path, which sets FLAG_ANY only)
     uint8_t* candf;              // [F][ntiles] 1: the tile's dilated mask may be non-empty (labelled)
     int32_t* clist;              // [F][ntiles] candidate tiles of each frame
@@ -105,6 +105,7 @@ struct FusedArgs {
     int T, S, h, w, ksize, thresh;
     int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
+    int tflag_waves;             // words per tile-frame in tflag: 1 (k_fused, atomicOr) or 8 (k_pix, one per wave)
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
     uint64_t* dbg_pts;           // profiling-only k_pix workgroup stamps [S][ntiles][4] (FM_PTS); nullptr in normal use

@@ -39,9 +39,13 @@ constexpr int TS = 64;          // tile edge
 #ifndef FM_PIX_PRIO
 #define FM_PIX_PRIO 0
 #endif
+#ifndef FM_PIX_ABL
+#define FM_PIX_ABL 0  // timing ablations of the chain (results invalid): 1 f64 update, 2 absdiff, 4 ballot
+#endif
 constexpr int NT = FM_PIX_NT;   // threads
 constexpr int NW = NT / 64;     // waves; wave w owns tile rows [8w, 8w + 8)
 constexpr int RPWV = TS / NW;   // rows per wave in the chain stage
+static_assert(NW == 8, "tflag holds 8 words per tile (FusedArgs::tflag_waves)");
 
 __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 
@@ -84,11 +88,6 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
-// v_writelane_b32 through the LLVM intrinsic (HIP has no builtin).  Not inline asm: the
-// source SGPR is often VCC just written by the compare, and only a compiler-visible
-// operand gets the VALU-writes-SGPR -> VALU-reads-it wait states (inline asm here read a
-// stale VCC whenever no SALU op happened to sit between the two)
-__device__ int fm_writelane(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 template <int I> struct IntC { static constexpr int value = I; };
 // compile-time unrolled loop: fn(IntC<0>{}), ..., fn(IntC<N-1>{})
@@ -238,6 +237,7 @@ struct ChainCtx {
     uint32_t keep_lo, keep_hi;  // keep-mask bytes of the wave's 8 rows for this lane's column (1 = keep)
     bool hk;            // stream has a keep-mask
     uint32_t vec;       // every pixel of the wave's rows lies in accumulateWeighted's vector body
+    uint32_t tbmask;    // this lane's column inside the image ? rowvalid : 0
 };
 
 // One frame's vertical taps + per-pixel chain for the wave's 8 rows.
@@ -248,7 +248,7 @@ struct ChainCtx {
 template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
 __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const Geo& g, double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
-                                           bool init, uint64_t& mybits, uint32_t& flags) {
+                                           bool init, uint32_t& colbits, uint32_t& flags) {
     constexpr int R = KC >> 1;
     constexpr int NV = RPWV + 2 * R;       // H rows feeding the wave's 8 outputs
     constexpr int NP = (NV + 1) / 2;       // u16 pairs
@@ -267,9 +267,10 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         P[NP] = 0;
     }
     const double alpha = a.alpha, beta = a.beta;
-    const int thresh = a.thresh;
-    int mb_lo = 0, mb_hi = 0;
-    uint64_t orr = 0, top = 0, bot = 0;  // wave-uniform ORs of the row ballots (SGPRs)
+    // d in [0, 255]: clamping the threshold to [-1, 255] keeps d > t, and makes the sign of
+    // t - d that test
+    const int thr = min(max(a.thresh, -1), 255);
+    uint32_t tb = 0;  // bit j: row 8*wv + j of this lane's column is over the threshold
     static_for<RPWV>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         // acc = sum_t c[t] * H[j + t] + 2^15 over u16 pairs (H[e], H[e+1]); blur = byte 2
@@ -289,23 +290,29 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         if (INIT && init) b = (double)blur;
         // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8 -- into byte 2 of a copy
         // of acc, so that the byte-wise absdiff of the two words is |blur - q|
+#if FM_PIX_ABL & 2  // timing ablation only (results invalid): no convertScaleAbs / absdiff
+        const uint32_t d = acc >> 16;
+#else
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
         const uint32_t d = __builtin_amdgcn_sad_u8(acc, q, 0u);  // absdiff
-        const uint64_t bits = __builtin_amdgcn_ballot_w64((int)d > thresh);
+#endif
+#if !(FM_PIX_ABL & 4)  // timing ablation only: no threshold bits
+        tb |= ((uint32_t)(thr - (int)d) >> 31) << j;
+#endif
+#if FM_PIX_ABL & 1  // timing ablation only: no f64 background update
+        double nb = b + 0.0;
+        const double bl = 0.0;
+        (void)alpha; (void)beta;
+#else
         const double bl = __dmul_rn((double)blur, alpha);
         double nb = __fma_rn(b, beta, bl);
+#endif
         if (TAIL) {  // accumulateWeighted's scalar tail: two products, one add there
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
             if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
         }
         const bool rv = (cc.rowvalid >> j) & 1;
         bg[j] = nb;  // out-of-image pixels compute values that are never stored
-        const uint64_t bm = rv ? (bits & cc.colmask) : 0;  // row j's bits -> lane j
-        orr |= bm;
-        if (j < 2) top |= bm;
-        if (j >= RPWV - 2) bot |= bm;
-        mb_lo = fm_writelane((int)(uint32_t)bm, j, mb_lo);
-        mb_hi = fm_writelane((int)(uint32_t)(bm >> 32), j, mb_hi);
         if (PLANES && rv && ((cc.colmask >> ln) & 1)) {
             const size_t plane = (size_t)a.h * w;
             const size_t li = (size_t)(y0 + RPWV * wv + j) * w + x0 + ln;
@@ -313,9 +320,14 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
             a.planes[2 * (size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)d;
         }
     });
-    mybits = ((uint64_t)(uint32_t)mb_hi << 32) | (uint32_t)mb_lo;
+    // out-of-image pixels are background for the contour pass
+    tb &= cc.tbmask;
+    colbits = tb;
     // where the tile has threshold bits (decides the contour pass's candidate tiles):
     // any, within 2 px of the left / right edge, and for the tile's first / last two rows
+    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
+    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
     uint32_t fl = 0;
     if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
     if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
@@ -383,6 +395,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
         }
         const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
         cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
+        cc.tbmask = x < w ? cc.rowvalid : 0u;
     }
     // consume those loads here (the asm is a use, so the compiler waits before it):
     // inside the frame loop only the raw prefetch is then in flight and the chain
@@ -558,7 +571,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
             if (!(skip & 16)) lds_barrier();
 
             // ---- vertical taps + chain for the wave's 8 rows; threshold bits by ballot
-            uint64_t mybits = 0;
+            uint32_t colbits = 0;
             uint32_t fl = 0;
             // launder the per-tile uniforms each frame: otherwise LICM hoists dozens of
             // per-row exec masks out of the frame loop and they spill
@@ -569,9 +582,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
             asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
             if (!(skip & 2))
                 chain_rows<KC, PLANES, INIT, KEEP, TAIL>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf,
-                                                         init0 && t == t0, mybits, fl);
-            if (ln < RPWV) a.bits[(f * a.ntiles + ti) * TS + RPWV * wv + ln] = mybits;
-            if (ln == 0 && fl) atomicOr(&a.tflag[f * a.ntiles + ti], fl);
+                                                         init0 && t == t0, colbits, fl);
+            // column-major bit tile: word c of the tile = column c, bit r = row r; this wave
+            // owns byte wv of every column word
+            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+            // this wave's flag word, a plain store every frame (an atomic would sit in vmcnt
+            // until the next frame's wait for the raw prefetch)
+            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
 
             if (t + 1 < t1 && !(skip & 1))
                 gray_stage(raw + (b ^ 1) * g.raw_bytes, Hs + (b ^ 1) * (g.H_bytes / 2), f + S);
