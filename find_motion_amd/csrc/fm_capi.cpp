@@ -55,7 +55,7 @@ struct BatchSlot {
     int32_t* d_count = nullptr;     // [2F+1]
     int32_t* h_count = nullptr;     // pinned [F]
     int32_t* h_overflow = nullptr;  // pinned [F]
-    int32_t* dh_count = nullptr;     // device aliases of the two (mapped): the fused path's k_fold_emit writes them
+    int32_t* dh_count = nullptr;     // device aliases of the two (mapped): the fused path's k_counts writes them
     int32_t* dh_overflow = nullptr;
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
@@ -612,7 +612,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     if (any_init) HIP_TRY(c, hipMemcpyAsync(c->d_init, B.h_init, S, hipMemcpyHostToDevice, ps));
 
     const long long npx = (long long)c->work_plane;
-    // fused path: k_regions zeroes the counters, k_fold_emit clears the tile flags
+    // fused path: counters zeroed by k_pix (k_regions on the k_fused path), tile flags cleared by k_counts
     if (!c->use_fused) HIP_TRY(c, hipMemsetAsync(B.d_count, 0, (2 * F + 1) * sizeof(int32_t), ps));
     if (c->use_fused) {
         FusedArgs fa{};

@@ -22,10 +22,12 @@
 //                dilated masks: <= 24 runs per 64-px row; kept for safety).
 //   k_merge      one wave per candidate: unions along its edges with candidate
 //                neighbours (right / below) and empty regions (all sides).
-//   k_fold_emit  one workgroup per frame: path compression with outer flags,
-//                bboxes and raster-first pixels folded into the roots (one thread
-//                per candidate or region), then the external test at each
+//   k_fold       one wave per candidate tile (lanes = its components) or region:
+//                path compression with outer flags, bboxes and raster-first
+//                pixels folded into the roots.
+//   k_emit       one wave per candidate tile: the external test at each
 //                foreground root and the contour records (mapped host memory).
+//   k_counts     per frame: counts / overflow flags into mapped host memory.
 // A frame with a tile beyond even the heavy pass is flagged (count[F+f]); the
 // host relabels it with the pixel-level CCL of fm_kernels.hip.
 #include "fm_internal.h"
@@ -679,47 +681,46 @@ __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
 // pixels folded into the roots, one thread per candidate tile (all its nodes) or
 // enclosed empty region; (2) after a workgroup barrier, the external test at every
 // foreground root and the contour records.
-constexpr int FT = 256;
-__global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
-    const size_t f = blockIdx.x;
+// one wave per candidate tile (lanes = its components) or per empty-tile region: path
+// compression with outer flags, bboxes and raster-first pixels folded into the roots
+__global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
-    // the tile flags were consumed by k_regions: clear them for the slot's next batch
-    // (k_pix rewrites its per-wave flag words every frame: nothing to clear there)
-    if (a.tflag_waves == 1)
-        for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
-    if (a.count[F + f]) {  // relabelled by the host's pixel-level fallback
-        if (threadIdx.x == 0) {
-            a.h_overflow[f] = 1;
-            a.h_count[f] = 0;
-        }
-        return;
-    }
+    if (a.count[F + f]) return;  // relabelled by the host's pixel-level fallback
     NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    const TileRec* TRf = a.tiles + f * a.ntiles;
+    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
+    for (int k = blockIdx.x * CW + wv; k < nc + nr; k += gridDim.x * CW) {
+        if (k < nc) {
+            const int t = a.clist[f * a.ntiles + k];
+            const int k1 = TRf[t].nroots;
+            for (int i = ln; i < k1; i += 64) fold_node(N, t * MAXR + i);
+        } else if (ln == 0) {
+            fold_node(N, a.rlist[f * a.ntiles + (k - nc)] * MAXR);
+        }
+    }
+}
+
+// one wave per candidate tile, lanes = its components: the external test at every
+// foreground root and its contour record (after k_fold: every node points at its root)
+__global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.count[F + f]) return;
+    const NodeRec* N = a.nodes + f * (size_t)a.nnodes;
     const TileRec* TRf = a.tiles + f * a.ntiles;
     const uint8_t* cf = a.candf + f * a.ntiles;
     const int32_t* rr = a.regrep + f * a.ntiles;
-    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
-    for (int i = threadIdx.x; i < nc + nr; i += FT) {
-        if (i < nc) {
-            const int t = a.clist[f * a.ntiles + i];
-            const int k1 = TRf[t].nroots;
-            for (int k = 0; k < k1; k++) fold_node(N, t * MAXR + k);
-        } else {
-            fold_node(N, a.rlist[f * a.ntiles + (i - nc)] * MAXR);
-        }
-    }
-    __threadfence();
-    __syncthreads();
-    for (int i = threadIdx.x; i < nc; i += FT) {
-        const int t = a.clist[f * a.ntiles + i];
+    const int nc = a.ncr[2 * f];
+    for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
+        const int t = a.clist[f * a.ntiles + k];
         const int k1 = TRf[t].nroots;
-        for (int k = 0; k < k1; k++) {
-            const int n = t * MAXR + k;
-            // fields other workgroups' threads folded into are read past the L1
-            const int par = __hip_atomic_load(&N[n].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t fl = __hip_atomic_load(&N[n].flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (par != n || !(fl & 1)) continue;
-            const uint64_t key = __hip_atomic_load((unsigned long long*)&N[n].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = ln; i < k1; i += 64) {
+            const int n = t * MAXR + i;
+            if (N[n].parent != n || !(N[n].flags & 1)) continue;
+            const uint64_t key = N[n].key;
             const uint32_t first = (uint32_t)(key >> 32), ref = (uint32_t)key;
             const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
             bool ext;
@@ -734,25 +735,35 @@ __global__ __launch_bounds__(FT) void k_fold_emit(FusedArgs a) {
                 } else {
                     bn = tf * MAXR + (int)ref;
                 }
-                const int br = __hip_atomic_load(&N[bn].parent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ext = (__hip_atomic_load(&N[br].flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) != 0;
+                ext = (N[N[bn].parent].flags & 2) != 0;
             }
             if (!ext) continue;
             const int id = atomicAdd(&a.count[f], 1);
             if (id < a.cap) {
                 int32_t* rec = a.rec + (f * a.cap + id) * 5;
                 rec[0] = (int32_t)first;
-                rec[1] = __hip_atomic_load(&N[n].minx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rec[1] = N[n].minx;
                 rec[2] = fy;
-                rec[3] = __hip_atomic_load(&N[n].maxx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                rec[4] = __hip_atomic_load(&N[n].maxy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                rec[3] = N[n].maxx;
+                rec[4] = N[n].maxy;
             }
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // results straight into mapped host memory: no copy after the kernel
-        a.h_count[f] = __hip_atomic_load(&a.count[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.h_overflow[f] = 0;
+}
+
+// one workgroup per frame: counts and overflow flags straight into mapped host memory
+// (no copy after the kernel); the k_fused path's tile flags cleared for the slot's next
+// batch (k_pix rewrites its per-wave flag words every frame)
+constexpr int FT = 256;
+__global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
+    const size_t f = blockIdx.x;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.tflag_waves == 1)
+        for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
+    if (threadIdx.x == 0) {
+        const bool ovf = a.count[F + f] != 0;
+        a.h_count[f] = ovf ? 0 : a.count[f];
+        a.h_overflow[f] = ovf ? 1 : 0;
     }
 }
 
@@ -790,7 +801,9 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("fold_emit", st) : -1;
-    hipLaunchKernelGGL(cc::k_fold_emit, dim3(F), dim3(cc::FT), 0, st, a);
+    hipLaunchKernelGGL(cc::k_fold, gf, dim3(64 * cc::CW), 0, st, a);
+    hipLaunchKernelGGL(cc::k_emit, gf, dim3(64 * cc::CW), 0, st, a);
+    hipLaunchKernelGGL(cc::k_counts, dim3(F), dim3(cc::FT), 0, st, a);
     if (tm) tm->end(tok);
     return hipGetLastError();
 }
