@@ -142,6 +142,17 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane), hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
 // 64x64 bit transpose across the wave: lane k holds word k; afterwards lane r holds the
 // word whose bit c is bit r of the old word c
 __device__ __forceinline__ uint64_t transpose64(uint64_t w, int ln) {
@@ -168,9 +179,11 @@ __device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, in
     uint64_t e = 0;
     if (ln >= 62 && hl) e = vdil(B, a, ti - 1, ty, ln);
     if (ln <= 1 && hr) e = vdil(B, a, ti + 1, ty, ln);
-    const uint64_t vm1 = shfl64(v, (ln + 63) & 63), vm2 = shfl64(v, (ln + 62) & 63);
-    const uint64_t vp1 = shfl64(v, (ln + 1) & 63), vp2 = shfl64(v, (ln + 2) & 63);
-    const uint64_t e62 = shfl64(e, 62), e63 = shfl64(e, 63), e0 = shfl64(e, 0), e1 = shfl64(e, 1);
+    // neighbour columns by DPP wave shifts (wave_shr:1: lane i <- i-1; wave_shl:1: lane i <- i+1),
+    // the four neighbour-tile columns by readlane
+    const uint64_t vm1 = dpp64<0x138>(v), vm2 = dpp64<0x138>(vm1);
+    const uint64_t vp1 = dpp64<0x130>(v), vp2 = dpp64<0x130>(vp1);
+    const uint64_t e62 = rdl64(e, 62), e63 = rdl64(e, 63), e0 = rdl64(e, 0), e1 = rdl64(e, 1);
     uint64_t o = v;
     o |= ln >= 1 ? vm1 : e63;
     o |= ln >= 2 ? vm2 : (ln == 1 ? e63 : e62);
