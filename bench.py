@@ -105,6 +105,8 @@ def main() -> None:
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
     ap.add_argument("--batch", type=int, default=64, help="frames per stream per step (one pixel-kernel launch)")
     ap.add_argument("--ring", type=int, default=64, help="device-resident frames per stream")
+    ap.add_argument("--ring-period", type=int, default=64,
+                    help="synthetic frames in the ring's cycle: ring slot t holds frame t %% period")
     ap.add_argument("--cpu-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
@@ -136,7 +138,8 @@ def main() -> None:
     S, T = args.streams, args.batch
     R = max(args.ring - args.ring % T, T)
     cfg = {"workload": f"configs[1]: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
-                       f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring",
+                       f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
+                       + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
            "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
 
@@ -144,6 +147,9 @@ def main() -> None:
     vids = [SyntheticVideo(W, H, stream=g) for g in dist.rank_streams(pl, S)]
     host = np.empty((R, S, H, W, 3), np.uint8)
     for t in range(R):
+        if t >= args.ring_period:  # the ring cycles the first ring_period synthetic frames
+            host[t] = host[t % args.ring_period]
+            continue
         for s in range(S):
             host[t, s] = vids[s].frame(t)
     ring = torch.from_numpy(host).to(f"cuda:{local}")
