@@ -122,8 +122,13 @@ def main() -> None:
 
     import torch
 
+    # rehearsal only (one GPU box): FM_BENCH_DEVICE pins every rank to one device and
+    # FM_BENCH_BACKEND=gloo replaces RCCL (which refuses two ranks on one device)
+    if os.environ.get("FM_BENCH_DEVICE") is not None:
+        local = int(os.environ["FM_BENCH_DEVICE"])
+    backend = os.environ.get("FM_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
-    active = dist.init(pl, "nccl", torch.device("cuda", local))
+    active = dist.init(pl, backend, torch.device("cuda", local))
 
     from find_motion_amd import MotionEngine, make_gaussian, work_height
     from find_motion_amd.synthetic import SyntheticVideo
@@ -187,7 +192,7 @@ def main() -> None:
     run(args.warmup, args.steps)
     torch.cuda.synchronize()
     dist.barrier(active)
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, active, device=f"cuda:{local}")
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0, active, device=f"cuda:{local}" if backend == "nccl" else "cpu")
 
     ktimes = eng.kernel_times()
     total_frames = world * S * T * args.steps
