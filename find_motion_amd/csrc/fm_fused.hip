@@ -36,11 +36,8 @@ constexpr int NW = NT / 64;              // waves
 constexpr int EW = TS + 4;               // threshold region (tile + dilation halo)
 constexpr int NCJ = (EW + NW - 1) / NW;  // center rows per thread (9)
 constexpr int NHALO = EW * 4;            // 4 halo columns x 68 rows
-constexpr int MAXR = kTileMaxRuns;
 constexpr int NCH = 6;                   // max 16-B raw chunks per thread for the generic-k kernel
 constexpr int KMAX_FUSED = 49;
-constexpr uint32_t REF_OUTER = 0x80000000u;
-constexpr uint32_t REF_EDGE = 0x40000000u;
 
 __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 __host__ __device__ constexpr int gw_for(int r) { return TS + 4 + 2 * r; }
@@ -298,7 +295,6 @@ __global__ __launch_bounds__(NT) void k_fused(FusedArgs a) {
         }
     }
     __syncthreads();
-    const int cxa = colx[ln];  // this lane's column offset in the raw rows (column ln of the G region)
 
     // ---- background of the owned E pixels -> registers.  Wave w owns the
     //      contiguous E rows [rs, rs + cnt) (9 rows for waves 0-3, 8 for 4-7).
