@@ -65,7 +65,9 @@ struct Geo {
         CPR = RS / 16;
         nchunks = GH * CPR;
         RSH = TS;  // H is row-major: u16 [GH (+1 pad row)][TS]
-        raw_bytes = GH * RS;
+        // every thread's chunk slots (NT per 16-B column of chunks), so the staging stores
+        // need no per-lane predicate: slots past the G region only take garbage
+        raw_bytes = ((nchunks + NT - 1) / NT) * NT * 16;
         H_bytes = a16((GH + 1) * RSH * 2);
         o_raw = 0;
         o_H = o_raw + 2 * raw_bytes;
@@ -177,13 +179,14 @@ __device__ __forceinline__ void load_raw(Raw<NCH>& R, const uint8_t* fsrc, uint3
     for (int i = 0; i < NCH; i++) {
         const uint32_t mis = (flo + P.rel0[i]) & 15u;
         const int rel = (int)P.rel0[i] - (int)mis;
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (P.k16[i] < span + mis) {  // chunk starts before the row segment's last byte
-            if (__builtin_expect(rel >= 0 && (uint32_t)rel + 16u <= fbytes, 1))
-                val = *reinterpret_cast<const uint4*>(fsrc + rel);
-            else
-                val = load_partial(fsrc + rel, fsrc, fsrc + fbytes);
-        }
+        // one unconditional aligned 16-B load per slot from inside the frame: slots the gray
+        // stage does not read (past the row segment's last byte, or past the G region) take
+        // any in-frame window; a needed chunk hanging over either end of the frame (frame
+        // not 16-B aligned) is gathered bytewise instead
+        const bool full = rel >= 0 && (uint32_t)rel + 16u <= fbytes;
+        const int relc = full ? rel : rel < 0 ? rel + 16 : rel - 16;
+        uint4 val = *reinterpret_cast<const uint4*>(fsrc + relc);
+        if (__builtin_expect(!full && P.k16[i] < span + mis, 0)) val = load_partial(fsrc + rel, fsrc, fsrc + fbytes);
         R.v[i] = val;
     }
 }
@@ -192,11 +195,8 @@ template <int NCH>
 __device__ __forceinline__ void store_raw(const Raw<NCH>& R, uint8_t* raw, const Geo& g, int tid) {
 #pragma unroll
     for (int i = 0; i < NCH; i++) {
-        const int c = tid + NT * i;
-        if (c < g.nchunks) {
-            const int gy = c / g.CPR, k = c - gy * g.CPR;
-            *reinterpret_cast<uint4*>(raw + gy * g.RS + 16 * k) = R.v[i];
-        }
+        // chunk c = row c / CPR, 16 B at 16 * (c % CPR) of that row: byte 16 * c (RS = 16 * CPR)
+        *reinterpret_cast<uint4*>(raw + 16 * (tid + NT * i)) = R.v[i];
     }
 }
 
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
     // Lane (rg, q) of iteration it owns gray quad q of G row gy(it).  Frame-invariant
     // per-lane state: the row's byte offset in the frame (its 16-B aligned-down start
     // is where stage_raw put the row in LDS) and the G row index (clamped for idle lanes).
-    uint32_t rowbyte[NIT], loff[NIT];
+    uint32_t rowbyte[NIT], loff[NIT], hoff[NIT];
     int gyc[NIT];
     bool act[NIT];
 #pragma unroll
@@ -451,6 +451,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
         gyc[it] = act[it] ? gy : 0;
         rowbyte[it] = (uint32_t)(rowy[gyc[it]] * w + cx0) * 3u;
         loff[it] = (uint32_t)(gyc[it] * g.RS + qoff);
+        // H store target: lanes without an H quad (idle, or halo quads q >= 16) write the
+        // pad row GH, which the vertical taps never read -- the store needs no predicate
+        hoff[it] = (uint32_t)((act[it] && q < TS / 4 ? gyc[it] : GHc) * g.RSH + 4 * (q & (TS / 4 - 1)));
     }
     // rows of a 16-B multiple: every row starts at the same offset inside its first chunk
     const bool rows16 = (w * 3) % 16 == 0;
@@ -519,13 +522,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && 
 #pragma unroll
             for (int d = 1; d < NQW; d++)
                 qv[d] = d < NQN ? (uint32_t)__builtin_amdgcn_mov_dpp((int)qv[d - 1], 0x130, 0xF, 0xF, true) : 0u;
-            if (act[it] && q < TS / 4) {
+            {
                 const uint32_t h0 = htap<0, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h1 = htap<1, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h2 = htap<2, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 const uint32_t h3 = htap<3, OFF, NG, 0, NQW>(qv, cpk, 0u);
                 // row-major: one conflict-free 8-B store of the quad's four taps
-                *reinterpret_cast<uint2*>(Hb + gyc[it] * g.RSH + 4 * q) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+                *reinterpret_cast<uint2*>(Hb + hoff[it]) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
             }
         }
     };
