@@ -26,6 +26,7 @@ EXPORTED = (
     "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
     "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
+    "fm_host_alloc", "fm_host_free",
 )
 
 
@@ -84,6 +85,8 @@ def load() -> C.CDLL:
     L.fm_write_background.argtypes = [vp, i32, vp]
     L.fm_set_hip_stream.argtypes = [vp, vp]
     L.fm_kernel_times.argtypes = [vp, vp, vp, vp, i32]
+    L.fm_host_alloc.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
+    L.fm_host_free.argtypes = [vp, vp]
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
     L.fm_max_inflight.argtypes = [vp]
@@ -168,8 +171,25 @@ class MotionEngine:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            for buf in getattr(self, "_host_bufs", []):
+                self._L.fm_host_free(self._h, buf)
+            self._host_bufs = []
             self._L.fm_destroy(self._h)
             self._h = None
+
+    def host_buffer(self, n_frames: int) -> np.ndarray:
+        """Page-locked uint8 [n_frames][n_streams][H][W][3] array for frame batches: submit()
+        of it is an asynchronous DMA on the engine's input stream, overlapped with the
+        previous batches' kernels.  Freed by close(); keep it unchanged until wait() returns
+        for a batch submitted from it."""
+        shape = (n_frames, self.n_streams) + self.src_shape
+        nbytes = int(np.prod(shape))
+        p = C.c_void_p()
+        self._check(self._L.fm_host_alloc(self._h, nbytes, C.byref(p)))
+        if not hasattr(self, "_host_bufs"):
+            self._host_bufs = []
+        self._host_bufs.append(p)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(nbytes,)).reshape(shape)
 
     def __del__(self):
         try:

@@ -77,7 +77,7 @@ struct fm_ctx {
 
     // streams: pixel work (caller-replaceable), contour pass, synchronous reads
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
-    hipStream_t rs_stream = nullptr;  // modes with a resize: input copy + resize, ahead of the pixel stream
+    hipStream_t rs_stream = nullptr;  // input stream: host copies + resize, ahead of the pixel stream
     hipStream_t ccl_streams[kSlots] = {};
     int nccl = 1;
     KernelTimer timer;
@@ -369,8 +369,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
     }
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-    if (c->rmode != ResizeMode::Identity && !std::getenv("FM_RESIZE_INLINE"))
-        HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
+    // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
+    if (!std::getenv("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
@@ -521,6 +521,20 @@ void fm_destroy(fm_ctx* c) {
     delete c;
 }
 
+int fm_host_alloc(fm_ctx* c, size_t bytes, void** out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    *out = nullptr;
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    HIP_TRY(c, hipHostMalloc(out, bytes, hipHostMallocPortable));
+    return FM_OK;
+}
+
+int fm_host_free(fm_ctx* c, void* ptr) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (ptr) HIP_TRY(c, hipHostFree(ptr));
+    return FM_OK;
+}
+
 int fm_max_inflight(const fm_ctx* c) { return c ? c->nslots : fail(nullptr, FM_EINVAL, "null context"); }
 
 int fm_work_size(const fm_ctx* c, int* h, int* w) {
@@ -600,7 +614,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         c->timer.end(tok);
         work = B.d_work;
     }
-    if (rs != ps) {
+    if (rs != ps && (!on_device || c->rmode != ResizeMode::Identity)) {  // something ran on the input stream
         HIP_TRY(c, hipEventRecord(B.ev_rs, rs));
         HIP_TRY(c, hipStreamWaitEvent(ps, B.ev_rs, 0));
     }

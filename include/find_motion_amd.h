@@ -106,6 +106,14 @@ int fm_max_inflight(const fm_ctx* ctx);
  * submitted before waiting; fm_wait completes them in submission order. */
 int fm_submit(fm_ctx* ctx, const uint8_t* frames, int n_frames, int on_device);
 
+/* Page-locked host memory for frame batches (a decoder writes frames here): fm_submit
+ * of such a buffer is a true asynchronous DMA (hipMemcpyAsync) on the context's input
+ * stream, overlapped with the previous batch's kernels (north_star: "frame batches
+ * pinned and hipMemcpyAsync-overlapped with compute").  Replaces nothing in the
+ * reference (cap.read() returns pageable numpy frames, fm.py:501); optional. */
+int fm_host_alloc(fm_ctx* ctx, size_t bytes, void** out);
+int fm_host_free(fm_ctx* ctx, void* ptr);
+
 /* Wait for the oldest batch in flight; makes its results readable (device-side
  * results -- masks, planes -- until that batch's slot is reused by a later submit). */
 int fm_wait(fm_ctx* ctx);

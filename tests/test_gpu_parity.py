@@ -314,3 +314,32 @@ def test_batches_in_flight_match_sequential():
     for s in range(S):
         np.testing.assert_array_equal(eng.background(s), orc[s].bg)
     eng.close()
+
+
+def test_pinned_host_buffers_match_pageable():
+    # page-locked batches (fm_host_alloc, DMA on the input stream) give the same results
+    # as pageable numpy batches, with batches in flight
+    W, H = 320, 240
+    fr = batch(W, H, 2, 0, 6)
+    results = []
+    for pinned in (False, True):
+        eng = MotionEngine(n_streams=2, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=3)
+        bufs = []
+        for b in range(2):
+            if pinned:
+                pb = eng.host_buffer(3)
+                pb[:] = fr[3 * b:3 * b + 3]
+                bufs.append(pb)
+            else:
+                bufs.append(np.ascontiguousarray(fr[3 * b:3 * b + 3]))
+        out = []
+        for b in range(2):
+            eng.submit(bufs[b])
+        for b in range(2):
+            eng.wait()
+            out.append((eng.counts().copy(), [eng.mask(t, s).copy() for t in range(3) for s in range(2)]))
+        results.append(out)
+        eng.close()
+    for (ca, ma), (cb, mb) in zip(results[0], results[1]):
+        assert np.array_equal(ca, cb)
+        assert all(np.array_equal(x, y) for x, y in zip(ma, mb))
