@@ -94,8 +94,8 @@ def cpu_baseline(cfg: dict, frames_host: np.ndarray, n_frames: int) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["F", "D"], default="F",
                     help="F: -B 1920 -b 384 (full-resolution fused kernel); D: reference default -B 100 -b 20")
     ap.add_argument("--width", type=int, default=1920)
