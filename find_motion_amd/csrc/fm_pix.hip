@@ -33,6 +33,9 @@ constexpr int TS = 64;          // tile edge
 #ifndef FM_PIX_WPE
 #define FM_PIX_WPE 4
 #endif
+#ifndef FM_PIX_WPE_LARGE
+#define FM_PIX_WPE_LARGE 1  // k = 21: no register cap (178 VGPRs, one workgroup per CU)
+#endif
 #ifndef FM_PIX_NT
 #define FM_PIX_NT 512
 #endif
@@ -336,7 +339,7 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
 }
 
 template <int KC, bool PLANES, bool INIT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((KC <= 7 && !PLANES && !INIT) ? FM_PIX_WPE : 1))) void k_pix(FusedArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && !INIT) ? (KC <= 7 ? FM_PIX_WPE : FM_PIX_WPE_LARGE) : 1))) void k_pix(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = KC >> 1;
     const Geo g(R);
