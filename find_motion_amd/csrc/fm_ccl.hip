@@ -504,18 +504,27 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     for (int t = tid; t < nt; t += RG)
         if (uf[t] >= 0) uf[t] = lfind(uf, t);
     __syncthreads();
-    // region representative = its smallest tile; "outer" if any tile is on the grid border
+    // region representative = its smallest tile; "outer" if any tile is on the grid border.
+    // The representative's node is (re)initialised first: the slot's nodes still hold an
+    // earlier batch's records, where this tile may have been a candidate
     for (int t = tid; t < nt; t += RG) {
         const int r = uf[t];
         if (r < 0) continue;
         a.regrep[(size_t)f * nt + t] = r;
-        const int tx = t % ntx, ty = t / ntx;
-        NodeRec* rep = a.nodes + (size_t)f * a.nnodes + (size_t)r * MAXR;
         if (t == r) {
+            NodeRec* rep = a.nodes + (size_t)f * a.nnodes + (size_t)r * MAXR;
             rep->parent = r * MAXR;
+            rep->flags = 0u;
             a.rlist[(size_t)f * nt + atomicAdd(&s_nr, 1)] = r;
         }
-        if (tx == 0 || ty == 0 || tx == ntx - 1 || ty == nty - 1) atomicOr(&rep->flags, 2u);
+    }
+    __syncthreads();
+    for (int t = tid; t < nt; t += RG) {
+        const int r = uf[t];
+        if (r < 0) continue;
+        const int tx = t % ntx, ty = t / ntx;
+        if (tx == 0 || ty == 0 || tx == ntx - 1 || ty == nty - 1)
+            atomicOr(&a.nodes[(size_t)f * a.nnodes + (size_t)r * MAXR].flags, 2u);
     }
     __syncthreads();
     if (tid == 0) {
