@@ -343,3 +343,35 @@ def test_pinned_host_buffers_match_pageable():
     for (ca, ma), (cb, mb) in zip(results[0], results[1]):
         assert np.array_equal(ca, cb)
         assert all(np.array_equal(x, y) for x, y in zip(ma, mb))
+
+
+def test_batch128_matches_oracle():
+    # the bench default batch: 128 frames per pixel-kernel launch, two batches, against the oracle
+    run_pair(320, 180, 320, ksize=5, S=2, T=128, n_batches=2, keep_planes=False)
+
+
+def test_batch_size_invariance_1080p():
+    # full-size size-independent property: one 128-frame launch == two 64-frame launches
+    # (counts, contours, masks of sampled frames, background bit-identical)
+    W, H, N = 1920, 1080, 128
+    fr = batch(W, H, 1, 0, N)
+    out = []
+    for T in (128, 64):
+        eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+        counts, boxes, masks = [], [], []
+        for b in range(N // T):
+            eng.submit(fr[b * T:(b + 1) * T])
+            eng.wait()
+            c = eng.counts()
+            for t in range(T):
+                counts.append(int(c[t, 0]))
+                boxes.append([x.bbox for x in eng.contours(t, 0)])
+                if (b * T + t) % 17 == 0:
+                    masks.append(eng.mask(t, 0).copy())
+        out.append((counts, boxes, masks, eng.background(0).copy()))
+        eng.close()
+    (ca, ba, ma, ga), (cb, bb, mb, gb) = out
+    assert ca == cb and ba == bb
+    assert all(np.array_equal(x, y) for x, y in zip(ma, mb))
+    assert np.array_equal(ga, gb)
+    assert sum(ca) > 0
