@@ -9,6 +9,7 @@ through the C ABI in include/find_motion_amd.h; there is no CPU fallback.
 __version__ = "0.1.0"
 
 from ._native import (  # noqa: F401
+    CascadeClassifier,
     Contour,
     FMError,
     MotionEngine,

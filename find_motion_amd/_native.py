@@ -27,6 +27,8 @@ EXPORTED = (
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
     "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
     "fm_host_alloc", "fm_host_free",
+    "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
+    "fm_haar_candidates", "fm_haar_last_ms",
 )
 
 
@@ -44,6 +46,15 @@ class FMParams(C.Structure):
     _fields_ = [("device", C.c_int), ("n_streams", C.c_int), ("src_w", C.c_int), ("src_h", C.c_int),
                 ("box_size", C.c_int), ("ksize", C.c_int), ("threshold", C.c_int), ("avg", C.c_double),
                 ("max_batch", C.c_int), ("max_contours", C.c_int), ("flags", C.c_uint)]
+
+
+class FMHaarDesc(C.Structure):
+    _fields_ = [("win_w", C.c_int32), ("win_h", C.c_int32), ("n_stages", C.c_int32), ("n_trees", C.c_int32),
+                ("n_nodes", C.c_int32), ("n_leaves", C.c_int32), ("n_features", C.c_int32),
+                ("stage_ntrees", C.c_void_p), ("stage_threshold", C.c_void_p), ("tree_nodes", C.c_void_p),
+                ("node_left", C.c_void_p), ("node_right", C.c_void_p), ("node_feature", C.c_void_p),
+                ("node_threshold", C.c_void_p), ("leaves", C.c_void_p), ("feat_rects", C.c_void_p),
+                ("feat_weights", C.c_void_p), ("feat_tilted", C.c_void_p)]
 
 
 class FMContour(C.Structure):
@@ -90,8 +101,19 @@ def load() -> C.CDLL:
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
     L.fm_max_inflight.argtypes = [vp]
+    L.fm_haar_create.argtypes = [i32, C.POINTER(FMHaarDesc), C.POINTER(vp)]
+    L.fm_haar_destroy.argtypes = [vp]
+    L.fm_haar_destroy.restype = None
+    L.fm_haar_last_error.argtypes = [vp]
+    L.fm_haar_last_error.restype = C.c_char_p
+    L.fm_haar_window.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
+    L.fm_haar_detect.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, i32, i32, i32, i32, vp, i32, vp]
+    L.fm_haar_candidates.argtypes = [vp, vp, i32]
+    L.fm_haar_last_ms.argtypes = [vp]
+    L.fm_haar_last_ms.restype = C.c_double
     for name in EXPORTED:
-        if name not in ("fm_destroy", "fm_last_error", "fm_abi_version"):
+        if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
+                        "fm_haar_last_ms"):
             getattr(L, name).restype = i32
     _lib = L
     return L
@@ -293,3 +315,81 @@ class MotionEngine:
 
     def reset_kernel_times(self) -> None:
         self._check(self._L.fm_reset_kernel_times(self._h))
+
+
+class CascadeClassifier:
+    """cv2.CascadeClassifier for HAAR cascades on the GPU (find_motion.py:396, :722-731).
+
+    `CascadeClassifier(path)` reads the XML (find_motion_amd.cascade); `detectMultiScale`
+    keeps OpenCV's signature and returns an (N, 4) int32 array of (x, y, w, h), or an
+    empty tuple when nothing is found, as cv2 does.  `detect_batch` runs many images of
+    one size in one call (the ROI frames of many streams)."""
+
+    def __init__(self, path_or_cascade, device: int = 0):
+        from .cascade import Cascade, parse
+        cs = path_or_cascade if isinstance(path_or_cascade, Cascade) else parse(path_or_cascade)
+        self.cascade = cs
+        L = load()
+        self._keep = [np.ascontiguousarray(a) for a in (
+            cs.stage_ntrees, cs.stage_threshold, cs.tree_nodes, cs.node_left, cs.node_right, cs.node_feature,
+            cs.node_threshold, cs.leaves, cs.feat_rects, cs.feat_weights, cs.feat_tilted)]
+        k = self._keep
+        d = FMHaarDesc(cs.win_w, cs.win_h, len(cs.stage_ntrees), len(cs.tree_nodes), len(cs.node_left),
+                       len(cs.leaves), len(cs.feat_tilted), *[_ptr(a) for a in k])
+        h = C.c_void_p()
+        rc = L.fm_haar_create(int(device), C.byref(d), C.byref(h))
+        self._h = h
+        if rc != FM_OK:
+            msg = L.fm_haar_last_error(h).decode() if h else ""
+            L.fm_haar_destroy(h)
+            self._h = None
+            raise FMError(rc, f"fm_haar_create: {msg}")
+
+    def empty(self) -> bool:
+        return self._h is None
+
+    def detect_batch(self, images: np.ndarray, scaleFactor=1.1, minNeighbors=5, minSize=(0, 0), maxSize=(0, 0),
+                     cap: int = 256):
+        """images: [n, H, W, 3] BGR or [n, H, W] gray u8 -> list of (k, 4) int32 arrays."""
+        L = load()
+        imgs = np.ascontiguousarray(images, np.uint8)
+        ch = 3 if imgs.ndim == 4 else 1
+        n, H, W = imgs.shape[:3]
+        while True:
+            rects = np.zeros((n, cap, 4), np.int32)
+            counts = np.zeros(n, np.int32)
+            rc = L.fm_haar_detect(self._h, _ptr(imgs), n, H, W, ch, 0, float(scaleFactor), int(minNeighbors),
+                                  int(minSize[0]), int(minSize[1]), int(maxSize[0]), int(maxSize[1]),
+                                  _ptr(rects), cap, _ptr(counts))
+            if rc != FM_OK:
+                raise FMError(rc, f"fm_haar_detect: {L.fm_haar_last_error(self._h).decode()}")
+            if counts.max(initial=0) <= cap:
+                return [rects[i, :counts[i]].copy() for i in range(n)]
+            cap = int(counts.max())
+
+    def detectMultiScale(self, image, scaleFactor=1.1, minNeighbors=5, flags=0, minSize=(0, 0), maxSize=(0, 0)):
+        r = self.detect_batch(np.asarray(image)[None], scaleFactor, minNeighbors, minSize or (0, 0),
+                              maxSize or (0, 0))[0]
+        return r if len(r) else ()
+
+    def candidates(self) -> np.ndarray:
+        """Ungrouped candidates of image 0 of the last call (parity tests)."""
+        L = load()
+        n = L.fm_haar_candidates(self._h, None, 0)
+        out = np.zeros((max(n, 1), 4), np.int32)
+        L.fm_haar_candidates(self._h, _ptr(out), n)
+        return out[:n]
+
+    def last_ms(self) -> float:
+        return float(load().fm_haar_last_ms(self._h))
+
+    def close(self):
+        if self._h:
+            load().fm_haar_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

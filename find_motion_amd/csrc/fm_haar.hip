@@ -1,0 +1,650 @@
+// Object-ROI stage: cv::CascadeClassifier::detectMultiScale
+// for HAAR cascades, as find_motion.py:722-731 calls it on the 300-px-wide
+// resized frame every 15th frame.  Batched: n images of one size per call.
+//
+// Device side, per call (one HIP stream, all images and scales in each launch):
+//   k_hgray    BGR -> gray (cvtColor fixed point, as the motion path)
+//   k_hresize  every scale's INTER_LINEAR_EXACT image (resize.cpp
+//              resize_bitExact: 8-bit taps, 16-bit horizontal values,
+//              (v + 2^15) >> 16; borders = tap 0 on the clamped edge)
+//   k_hrows    integral rows: sum and squared sum, int32 wrapping (CV_32S)
+//   k_hcols    integral columns
+//   k_htilt    tilted sum T(X,Y) = sum_{y<Y, |x-X+1| <= Y-y-1} I(x,y) (only for
+//              cascades with tilted features)
+//   k_heval    one thread per window of the ystep grid: HaarEvaluator::setWindow
+//              variance normalisation, then the stages (stumps or trees) with
+//              float32 feature sums without FMA and double leaf sums
+// Host side: the x-skip of rows whose window was rejected by stage 0 and
+// groupRectangles (partition + class means + nested-rect filter), both
+// sequential by definition and tiny next to the window sweep.
+//
+// Algorithmic bytes per image (bench): the BGR image once, plus each scale's
+// resized image, integrals (8 or 12 B/px) and the window results.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/find_motion_amd.h"
+
+namespace fm {
+namespace haar {
+
+constexpr int MAXSC = 64;  // scales per call (1.1^64 > 400: far beyond any frame)
+
+struct Node { int left, right, feat; float thr; };
+struct Feat { int r[3][4]; float w[3]; int tilted; };
+
+struct Geo {  // per scale, copied to the device as kernel arguments
+    int n;                    // scales
+    int sw[MAXSC], sh[MAXSC];  // resized size
+    int step[MAXSC];           // ystep
+    int gw[MAXSC], gh[MAXSC];  // window grid (columns, rows) on the ystep grid
+    int poff[MAXSC];           // resized-image offset (pixels) within one image
+    int ioff[MAXSC];           // integral offset (elements) within one image
+    int woff[MAXSC];           // window offset within one image
+    int xtab[MAXSC], ytab[MAXSC];  // offsets into the tap table
+    int P, I, NW;              // per image totals
+};
+
+__device__ __forceinline__ int find_scale(const int* off, int n, int r) {
+    int s = 0;
+    while (s + 1 < n && off[s + 1] <= r) ++s;
+    return s;
+}
+
+__global__ void k_hgray(const uint8_t* __restrict__ src, uint8_t* __restrict__ gray, long long npx, int channels) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npx) return;
+    if (channels == 1) { gray[i] = src[i]; return; }
+    const uint8_t* p = src + i * channels;
+    gray[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14);
+}
+
+// taps: int2 (source offset, 8-bit weight of offset+1); borders carry weight 0
+__global__ void k_hresize(const uint8_t* __restrict__ gray, uint8_t* __restrict__ rimg, const int2* __restrict__ taps,
+                          Geo g, int W, int H, int nimg) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)nimg * g.P) return;
+    const int img = (int)(i / g.P), r = (int)(i - (long long)img * g.P);
+    const int s = find_scale(g.poff, g.n, r);
+    const int q = r - g.poff[s], y = q / g.sw[s], x = q - y * g.sw[s];
+    const int2 tx = taps[g.xtab[s] + x], ty = taps[g.ytab[s] + y];
+    const uint8_t* src = gray + (size_t)img * W * H;
+    const int x1 = min(tx.x + 1, W - 1), y1 = min(ty.x + 1, H - 1);
+    const uint8_t* r0 = src + (size_t)ty.x * W;
+    const uint8_t* r1 = src + (size_t)y1 * W;
+    const uint32_t h0 = r0[tx.x] * (256 - tx.y) + r0[x1] * tx.y;
+    const uint32_t h1 = r1[tx.x] * (256 - tx.y) + r1[x1] * tx.y;
+    const uint32_t v = (h0 * (256 - ty.y) + h1 * ty.y + (1u << 15)) >> 16;
+    rimg[(size_t)img * g.P + r] = (uint8_t)min(v, 255u);
+}
+
+// integral rows: S[y+1][x+1] = sum_{x'<=x} I(x', y) (row prefix; columns follow)
+__global__ void k_hrows(const uint8_t* __restrict__ rimg, uint32_t* __restrict__ S, uint32_t* __restrict__ Q, Geo g,
+                        int nimg, int maxh) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = blockIdx.y, img = blockIdx.z;
+    if (row >= g.sh[s]) return;
+    const int sw = g.sw[s];
+    const uint8_t* p = rimg + (size_t)img * g.P + g.poff[s] + (size_t)row * sw;
+    uint32_t* ps = S + (size_t)img * g.I + g.ioff[s] + (size_t)(row + 1) * (sw + 1);
+    uint32_t* pq = Q + (size_t)img * g.I + g.ioff[s] + (size_t)(row + 1) * (sw + 1);
+    uint32_t a = 0, b = 0;
+    ps[0] = 0;
+    pq[0] = 0;
+    for (int x = 0; x < sw; ++x) {
+        const uint32_t v = p[x];
+        a += v;
+        b += v * v;
+        ps[x + 1] = a;
+        pq[x + 1] = b;
+    }
+}
+
+__global__ void k_hcols(uint32_t* __restrict__ S, uint32_t* __restrict__ Q, Geo g, int nimg) {
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = blockIdx.y, img = blockIdx.z;
+    const int sw = g.sw[s], sh = g.sh[s];
+    if (col > sw) return;
+    uint32_t* ps = S + (size_t)img * g.I + g.ioff[s] + col;
+    uint32_t* pq = Q + (size_t)img * g.I + g.ioff[s] + col;
+    ps[0] = 0;
+    pq[0] = 0;
+    uint32_t a = 0, b = 0;
+    for (int y = 1; y <= sh; ++y) {
+        a += ps[(size_t)y * (sw + 1)];
+        b += pq[(size_t)y * (sw + 1)];
+        ps[(size_t)y * (sw + 1)] = a;
+        pq[(size_t)y * (sw + 1)] = b;
+    }
+}
+
+// tilted: T(X,Y) = sum_{y<Y} P(y, min(w, X+Y-1-y)) - P(y, max(0, X-Y+y)), P = row prefix
+__global__ void k_htilt(const uint32_t* __restrict__ S, uint32_t* __restrict__ T, Geo g, int nimg) {
+    const int s = blockIdx.y, img = blockIdx.z;
+    const int sw = g.sw[s], sh = g.sh[s], st = sw + 1;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= st * (sh + 1)) return;
+    const int Y = e / st, X = e - Y * st;
+    const uint32_t* ps = S + (size_t)img * g.I + g.ioff[s];
+    uint32_t acc = 0;
+    for (int y = 0; y < Y; ++y) {
+        const int hi = min(sw, max(0, X + Y - 1 - y)), lo = min(sw, max(0, X - Y + y));
+        if (hi > lo) {
+            const uint32_t* r1 = ps + (size_t)(y + 1) * st;
+            const uint32_t* r0 = ps + (size_t)y * st;
+            acc += (r1[hi] - r0[hi]) - (r1[lo] - r0[lo]);
+        }
+    }
+    T[(size_t)img * g.I + g.ioff[s] + e] = acc;
+}
+
+struct CascadeDev {
+    int win_w, win_h, n_stages, has_tilted;
+    const int* stage_first;    // first tree of each stage
+    const int* stage_ntrees;
+    const float* stage_thr;
+    const int* tree_node_ofs;  // first node of each tree
+    const int* tree_leaf_ofs;  // first leaf of each tree
+    const Node* nodes;
+    const float* leaves;
+    const Feat* feats;
+};
+
+__device__ __forceinline__ int32_t rsum(const uint32_t* I, int st, int x, int y, const int* r, bool tilted) {
+    uint32_t p0, p1, p2, p3;
+    if (!tilted) {
+        p0 = I[(y + r[1]) * st + x + r[0]];
+        p1 = I[(y + r[1]) * st + x + r[0] + r[2]];
+        p2 = I[(y + r[1] + r[3]) * st + x + r[0]];
+        p3 = I[(y + r[1] + r[3]) * st + x + r[0] + r[2]];
+    } else {
+        p0 = I[(y + r[1]) * st + x + r[0]];
+        p1 = I[(y + r[1] + r[3]) * st + x + r[0] - r[3]];
+        p2 = I[(y + r[1] + r[2]) * st + x + r[0] + r[2]];
+        p3 = I[(y + r[1] + r[2] + r[3]) * st + x + r[0] + r[2] - r[3]];
+    }
+    return (int32_t)(p0 - p1 - p2 + p3);
+}
+
+// one thread per window; res: 1 accepted, 0 rejected by stage 0, -1 rejected later or flat
+__global__ __launch_bounds__(256) void k_heval(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
+                                               const uint32_t* __restrict__ T, int8_t* __restrict__ res,
+                                               CascadeDev c, Geo g, int nimg) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)nimg * g.NW) return;
+    const int img = (int)(i / g.NW), r = (int)(i - (long long)img * g.NW);
+    const int s = find_scale(g.woff, g.n, r);
+    const int q = r - g.woff[s], gy = q / g.gw[s], gx = q - gy * g.gw[s];
+    const int x = gx * g.step[s], y = gy * g.step[s];
+    const int st = g.sw[s] + 1;
+    const size_t base = (size_t)img * g.I + g.ioff[s];
+    const uint32_t* Si = S + base;
+    const uint32_t* Qi = Q + base;
+    const uint32_t* Ti = c.has_tilted ? T + base : nullptr;
+
+    const int nr[4] = {1, 1, c.win_w - 2, c.win_h - 2};
+    const int32_t valsum = rsum(Si, st, x, y, nr, false);
+    const uint32_t valsq = (uint32_t)rsum(Qi, st, x, y, nr, false);
+    const double area = (double)((c.win_w - 2) * (c.win_h - 2));
+    double nf = area * (double)valsq - (double)valsum * (double)valsum;
+    int8_t out = -1;
+    if (nf > 0.) {
+        nf = sqrt(nf);
+        const float vnf = (float)(1. / nf);
+        if (area * (double)vnf < 1e-1) {
+            out = 1;
+            for (int si = 0; si < c.n_stages; ++si) {
+                const int t0 = c.stage_first[si], nt = c.stage_ntrees[si];
+                double sum = 0.;
+                for (int t = t0; t < t0 + nt; ++t) {
+                    const Node* nd = c.nodes + c.tree_node_ofs[t];
+                    int idx = 0;
+                    do {
+                        const Node n = nd[idx];
+                        const Feat& f = c.feats[n.feat];
+                        const uint32_t* I = f.tilted ? Ti : Si;
+                        float v = __fmul_rn(f.w[0], (float)rsum(I, st, x, y, f.r[0], f.tilted));
+                        v = __fadd_rn(v, __fmul_rn(f.w[1], (float)rsum(I, st, x, y, f.r[1], f.tilted)));
+                        if (f.w[2] != 0.f) v = __fadd_rn(v, __fmul_rn(f.w[2], (float)rsum(I, st, x, y, f.r[2], f.tilted)));
+                        v = __fmul_rn(v, vnf);
+                        idx = v < n.thr ? n.left : n.right;
+                    } while (idx > 0);
+                    sum += (double)c.leaves[c.tree_leaf_ofs[t] - idx];
+                }
+                if (sum < (double)c.stage_thr[si]) {
+                    out = si == 0 ? 0 : -1;
+                    break;
+                }
+            }
+        }
+    }
+    res[i] = out;
+}
+
+}  // namespace haar
+}  // namespace fm
+
+using namespace fm::haar;
+
+struct fm_haar {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int win_w = 0, win_h = 0, n_stages = 0, has_tilted = 0;
+    // device cascade
+    void* d_blob = nullptr;
+    CascadeDev cd{};
+    // grow-only work buffers
+    uint8_t *d_src = nullptr, *d_gray = nullptr, *d_rimg = nullptr;
+    uint32_t *d_S = nullptr, *d_Q = nullptr, *d_T = nullptr;
+    int8_t* d_res = nullptr;
+    int2* d_taps = nullptr;
+    size_t cap_src = 0, cap_gray = 0, cap_rimg = 0, cap_S = 0, cap_Q = 0, cap_T = 0, cap_res = 0, cap_taps = 0;
+    std::vector<int8_t> h_res;
+    std::vector<int32_t> cand;  // last call's candidates of image 0 (x, y, w, h)
+    double last_ms = 0.;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+static int hfail(fm_haar* h, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf;
+    return code;
+}
+#define HH(h, x)                                                                       \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) return hfail(h, FM_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+static int grow(fm_haar* h, T** p, size_t& cap, size_t count) {
+    if (count <= cap && *p) return 0;
+    if (*p) HH(h, hipFree(*p));
+    *p = nullptr;
+    cap = 0;
+    HH(h, hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)));
+    cap = count;
+    return 0;
+}
+
+static inline int rne_d(double v) { return (int)std::nearbyint(v); }
+static inline int rne_f(float v) { return (int)std::nearbyintf(v); }
+
+// interpolationLinear<uint8_t>::getCoeffs (resize.cpp), borders folded to weight 0 on the edge
+static void linear_exact_taps(int ssize, int dsize, std::vector<int2>& out) {
+    const double inv = (double)dsize / ssize;
+    const double scale = 1.0 / inv;
+    for (int d = 0; d < dsize; ++d) {
+        const double f = scale * ((double)d + 0.5) - 0.5;
+        const int i = (int)std::floor(f);
+        int2 t;
+        if (i >= 0 && ssize > 1) {
+            if (i < ssize - 1) {
+                t.x = i;
+                t.y = rne_d((f - i) * 256.0);
+            } else {
+                t.x = ssize - 1;
+                t.y = 0;
+            }
+        } else {
+            t.x = 0;
+            t.y = 0;
+        }
+        out.push_back(t);
+    }
+}
+
+extern "C" {
+
+int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
+    if (!out) return FM_EINVAL;
+    *out = nullptr;
+    auto* h = new fm_haar();
+    *out = h;
+    if (!d || d->win_w < 3 || d->win_h < 3 || d->n_stages < 1 || d->n_trees < 1 || d->n_nodes < 1 ||
+        d->n_features < 1 || d->n_leaves != d->n_trees + d->n_nodes)
+        return hfail(h, FM_EINVAL, "bad cascade description (window >= 3x3, stages/trees/nodes/features >= 1, "
+                                   "leaves == trees + nodes)");
+    int tsum = 0;
+    for (int s = 0; s < d->n_stages; ++s) {
+        if (d->stage_ntrees[s] < 1) return hfail(h, FM_EINVAL, "stage %d has no trees", s);
+        tsum += d->stage_ntrees[s];
+    }
+    if (tsum != d->n_trees) return hfail(h, FM_EINVAL, "stage tree counts sum to %d, not n_trees %d", tsum, d->n_trees);
+    int nsum = 0;
+    for (int t = 0; t < d->n_trees; ++t) {
+        if (d->tree_nodes[t] < 1) return hfail(h, FM_EINVAL, "tree %d has no nodes", t);
+        nsum += d->tree_nodes[t];
+    }
+    if (nsum != d->n_nodes) return hfail(h, FM_EINVAL, "tree node counts sum to %d, not n_nodes %d", nsum, d->n_nodes);
+    // node links stay inside their tree; features inside the window
+    for (int t = 0, o = 0; t < d->n_trees; o += d->tree_nodes[t], ++t)
+        for (int k = 0; k < d->tree_nodes[t]; ++k) {
+            const int l = d->node_left[o + k], r = d->node_right[o + k], f = d->node_feature[o + k];
+            if (l >= d->tree_nodes[t] || r >= d->tree_nodes[t] || l < -d->tree_nodes[t] || r < -d->tree_nodes[t] ||
+                f < 0 || f >= d->n_features)
+                return hfail(h, FM_EINVAL, "tree %d node %d: link or feature out of range", t, k);
+            if ((l > 0 && l <= k) || (r > 0 && r <= k))
+                return hfail(h, FM_EINVAL, "tree %d node %d: links must point forward", t, k);
+        }
+    int tilted = 0;
+    for (int i = 0; i < d->n_features; ++i) {
+        const int* r = d->feat_rects + 12 * i;
+        const bool tl = d->feat_tilted && d->feat_tilted[i];
+        tilted |= tl;
+        for (int j = 0; j < 3; ++j) {
+            const int x = r[4 * j], y = r[4 * j + 1], w = r[4 * j + 2], hh = r[4 * j + 3];
+            if (j > 0 && d->feat_weights[3 * i + j] == 0.f) continue;
+            const bool ok = !tl ? (x >= 0 && y >= 0 && w >= 0 && hh >= 0 && x + w <= d->win_w && y + hh <= d->win_h)
+                                : (w >= 0 && hh >= 0 && x - hh >= 0 && x + w <= d->win_w && y >= 0 &&
+                                   y + w + hh <= d->win_h);
+            if (!ok) return hfail(h, FM_EINVAL, "feature %d rect %d outside the %dx%d window", i, j, d->win_w, d->win_h);
+        }
+    }
+    h->device = device;
+    HH(h, hipSetDevice(device));
+    HH(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HH(h, hipEventCreate(&h->e0));
+    HH(h, hipEventCreate(&h->e1));
+    h->win_w = d->win_w;
+    h->win_h = d->win_h;
+    h->n_stages = d->n_stages;
+    h->has_tilted = tilted;
+
+    std::vector<int> sfirst(d->n_stages), tno(d->n_trees), tlo(d->n_trees);
+    for (int s = 0, t = 0; s < d->n_stages; t += d->stage_ntrees[s], ++s) sfirst[s] = t;
+    for (int t = 0, no = 0, lo = 0; t < d->n_trees; ++t) {
+        tno[t] = no;
+        tlo[t] = lo;
+        no += d->tree_nodes[t];
+        lo += d->tree_nodes[t] + 1;
+    }
+    std::vector<Node> nodes(d->n_nodes);
+    for (int k = 0; k < d->n_nodes; ++k)
+        nodes[k] = Node{d->node_left[k], d->node_right[k], d->node_feature[k], d->node_threshold[k]};
+    std::vector<Feat> feats(d->n_features);
+    for (int i = 0; i < d->n_features; ++i) {
+        Feat f{};
+        for (int j = 0; j < 3; ++j) {
+            for (int k = 0; k < 4; ++k) f.r[j][k] = d->feat_rects[12 * i + 4 * j + k];
+            f.w[j] = d->feat_weights[3 * i + j];
+        }
+        f.tilted = d->feat_tilted && d->feat_tilted[i] ? 1 : 0;
+        feats[i] = f;
+    }
+    // one blob: [stage_first][stage_ntrees][stage_thr][tree_node_ofs][tree_leaf_ofs][nodes][leaves][feats]
+    auto al = [](size_t v) { return (v + 63) & ~(size_t)63; };
+    size_t off[8], tot = 0;
+    const size_t sz[8] = {sizeof(int) * d->n_stages, sizeof(int) * d->n_stages, sizeof(float) * d->n_stages,
+                          sizeof(int) * d->n_trees, sizeof(int) * d->n_trees, sizeof(Node) * d->n_nodes,
+                          sizeof(float) * d->n_leaves, sizeof(Feat) * d->n_features};
+    for (int k = 0; k < 8; ++k) {
+        off[k] = tot;
+        tot += al(sz[k]);
+    }
+    std::vector<uint8_t> blob(tot, 0);
+    std::memcpy(&blob[off[0]], sfirst.data(), sz[0]);
+    std::memcpy(&blob[off[1]], d->stage_ntrees, sz[1]);
+    std::memcpy(&blob[off[2]], d->stage_threshold, sz[2]);
+    std::memcpy(&blob[off[3]], tno.data(), sz[3]);
+    std::memcpy(&blob[off[4]], tlo.data(), sz[4]);
+    std::memcpy(&blob[off[5]], nodes.data(), sz[5]);
+    std::memcpy(&blob[off[6]], d->leaves, sz[6]);
+    std::memcpy(&blob[off[7]], feats.data(), sz[7]);
+    HH(h, hipMalloc(&h->d_blob, tot));
+    HH(h, hipMemcpy(h->d_blob, blob.data(), tot, hipMemcpyHostToDevice));
+    auto* b = (uint8_t*)h->d_blob;
+    h->cd = CascadeDev{d->win_w, d->win_h, d->n_stages, tilted,
+                       (const int*)(b + off[0]), (const int*)(b + off[1]), (const float*)(b + off[2]),
+                       (const int*)(b + off[3]), (const int*)(b + off[4]), (const Node*)(b + off[5]),
+                       (const float*)(b + off[6]), (const Feat*)(b + off[7])};
+    return FM_OK;
+}
+
+void fm_haar_destroy(fm_haar* h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (void* p : {(void*)h->d_blob, (void*)h->d_src, (void*)h->d_gray, (void*)h->d_rimg, (void*)h->d_S,
+                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps})
+        if (p) (void)hipFree(p);
+    if (h->e0) (void)hipEventDestroy(h->e0);
+    if (h->e1) (void)hipEventDestroy(h->e1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char* fm_haar_last_error(const fm_haar* h) { return h ? h->err.c_str() : "null detector"; }
+
+int fm_haar_window(const fm_haar* h, int* w, int* hh) {
+    if (!h || !w || !hh) return FM_EINVAL;
+    *w = h->win_w;
+    *hh = h->win_h;
+    return FM_OK;
+}
+
+int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int channels, int on_device,
+                   double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h,
+                   int32_t* rects, int cap, int32_t* counts) {
+    if (!h || !h->d_blob) return FM_EINVAL;
+    if (!images || n < 1 || H < 1 || W < 1 || (channels != 1 && channels != 3) || !(scale_factor > 1.0) ||
+        cap < 0 || !counts || (cap > 0 && !rects))
+        return hfail(h, FM_EINVAL, "bad arguments (n >= 1, 1 or 3 channels, scale_factor > 1, counts[n])");
+    HH(h, hipSetDevice(h->device));
+    for (int i = 0; i < n; ++i) counts[i] = 0;
+    h->cand.clear();
+    // scales (detectMultiScaleNoGrouping)
+    if (max_w == 0 || max_h == 0) {
+        max_w = W;
+        max_h = H;
+    }
+    if (H < h->win_h || W < h->win_w) return FM_OK;
+    std::vector<float> all, sc;
+    for (double f = 1;; f *= scale_factor) {
+        if (rne_d(h->win_w * f) > W || rne_d(h->win_h * f) > H) break;
+        all.push_back((float)f);
+        if ((int)all.size() > 4096) break;
+    }
+    for (float s : all) {
+        const int ww = rne_f((float)h->win_w * s), wh = rne_f((float)h->win_h * s);
+        if (ww > max_w || wh > max_h) break;
+        if (ww < min_w || wh < min_h) continue;
+        sc.push_back(s);
+    }
+    if (sc.empty()) return FM_OK;
+    if ((int)sc.size() > MAXSC) return hfail(h, FM_ENOTSUP, "%zu scales (max %d)", sc.size(), MAXSC);
+    Geo g{};
+    g.n = (int)sc.size();
+    int ww0 = 0;
+    std::vector<int> ylim(g.n);
+    std::vector<int2> taps;
+    for (int s = 0; s < g.n; ++s) {
+        g.sw[s] = rne_f((float)W / sc[s]);
+        g.sh[s] = rne_f((float)H / sc[s]);
+        g.step[s] = sc[s] >= 2.f ? 1 : 2;
+        const int ww = std::max(g.sw[s] + 1 - h->win_w, 0), wh = std::max(g.sh[s] + 1 - h->win_h, 0);
+        if (s == 0) ww0 = ww;
+        g.gw[s] = (ww + g.step[s] - 1) / g.step[s];
+        ylim[s] = wh;
+    }
+    const int nstripes = (ww0 + 31) / 32;
+    for (int s = 0; s < g.n; ++s) {
+        const int wh = std::max(g.sh[s] + 1 - h->win_h, 0);
+        const int stripe = nstripes ? std::max((wh / g.step[s] + nstripes - 1) / nstripes, 1) * g.step[s] : 0;
+        ylim[s] = std::min(nstripes * stripe, wh);
+        g.gh[s] = (ylim[s] + g.step[s] - 1) / g.step[s];
+        if (g.gw[s] == 0) g.gh[s] = 0;
+    }
+    g.P = g.I = g.NW = 0;
+    for (int s = 0; s < g.n; ++s) {
+        g.poff[s] = g.P;
+        g.ioff[s] = g.I;
+        g.woff[s] = g.NW;
+        g.P += g.sw[s] * g.sh[s];
+        g.I += (g.sw[s] + 1) * (g.sh[s] + 1);
+        g.NW += g.gw[s] * g.gh[s];
+        g.xtab[s] = (int)taps.size();
+        linear_exact_taps(W, g.sw[s], taps);
+        g.ytab[s] = (int)taps.size();
+        linear_exact_taps(H, g.sh[s], taps);
+    }
+    const size_t npx = (size_t)n * H * W;
+    int rc;
+    if ((rc = grow(h, &h->d_gray, h->cap_gray, npx)) || (rc = grow(h, &h->d_rimg, h->cap_rimg, (size_t)n * g.P)) ||
+        (rc = grow(h, &h->d_taps, h->cap_taps, taps.size())) || (rc = grow(h, &h->d_res, h->cap_res, (size_t)n * g.NW)))
+        return rc;
+    if ((rc = grow(h, &h->d_S, h->cap_S, (size_t)n * g.I)) || (rc = grow(h, &h->d_Q, h->cap_Q, (size_t)n * g.I)) ||
+        (h->has_tilted && (rc = grow(h, &h->d_T, h->cap_T, (size_t)n * g.I))))
+        return rc;
+    const uint8_t* src = images;
+    if (!on_device) {
+        if ((rc = grow(h, &h->d_src, h->cap_src, npx * channels))) return rc;
+        HH(h, hipMemcpyAsync(h->d_src, images, npx * channels, hipMemcpyHostToDevice, h->stream));
+        src = h->d_src;
+    }
+    HH(h, hipMemcpyAsync(h->d_taps, taps.data(), taps.size() * sizeof(int2), hipMemcpyHostToDevice, h->stream));
+    HH(h, hipEventRecord(h->e0, h->stream));
+    k_hgray<<<(unsigned)((npx + 255) / 256), 256, 0, h->stream>>>(src, h->d_gray, (long long)npx, channels);
+    const long long np = (long long)n * g.P;
+    k_hresize<<<(unsigned)((np + 255) / 256), 256, 0, h->stream>>>(h->d_gray, h->d_rimg, h->d_taps, g, W, H, n);
+    int maxh = 0, maxw = 0;
+    for (int s = 0; s < g.n; ++s) {
+        maxh = std::max(maxh, g.sh[s]);
+        maxw = std::max(maxw, g.sw[s]);
+    }
+    k_hrows<<<dim3((maxh + 63) / 64, g.n, n), 64, 0, h->stream>>>(h->d_rimg, h->d_S, h->d_Q, g, n, maxh);
+    k_hcols<<<dim3((maxw + 1 + 63) / 64, g.n, n), 64, 0, h->stream>>>(h->d_S, h->d_Q, g, n);
+    if (h->has_tilted)
+        k_htilt<<<dim3((unsigned)(((maxw + 1) * (maxh + 1) + 255) / 256), g.n, n), 256, 0, h->stream>>>(h->d_S, h->d_T,
+                                                                                                    g, n);
+    const long long nw = (long long)n * g.NW;
+    if (nw > 0)
+        k_heval<<<(unsigned)((nw + 255) / 256), 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->cd, g, n);
+    HH(h, hipGetLastError());
+    HH(h, hipEventRecord(h->e1, h->stream));
+    h->h_res.resize((size_t)nw);
+    if (nw > 0) HH(h, hipMemcpyAsync(h->h_res.data(), h->d_res, (size_t)nw, hipMemcpyDeviceToHost, h->stream));
+    HH(h, hipStreamSynchronize(h->stream));
+    float ms = 0.f;
+    HH(h, hipEventElapsedTime(&ms, h->e0, h->e1));
+    h->last_ms = ms;
+
+    // per image: the row scan with the stage-0 skip, then groupRectangles (eps 0.2)
+    const double eps = 0.2;
+    for (int img = 0; img < n; ++img) {
+        std::vector<int32_t> c;
+        const int8_t* R = h->h_res.data() + (size_t)img * g.NW;
+        for (int s = 0; s < g.n; ++s) {
+            const float f = sc[s];
+            const int wsw = rne_f((float)h->win_w * f), wsh = rne_f((float)h->win_h * f);
+            for (int gy = 0; gy < g.gh[s]; ++gy)
+                for (int gx = 0; gx < g.gw[s];) {
+                    const int8_t v = R[g.woff[s] + gy * g.gw[s] + gx];
+                    if (v > 0) {
+                        const int x = gx * g.step[s], y = gy * g.step[s];
+                        c.insert(c.end(), {rne_f((float)x * f), rne_f((float)y * f), wsw, wsh});
+                    }
+                    gx += v == 0 ? 2 : 1;
+                }
+        }
+        if (img == 0) h->cand = c;
+        const int nc = (int)c.size() / 4;
+        std::vector<int32_t> outr;
+        if (min_neighbors <= 0) {
+            outr = c;
+        } else if (nc > 0) {
+            auto similar = [&](int a, int b) {
+                const int32_t* r1 = &c[4 * a];
+                const int32_t* r2 = &c[4 * b];
+                const double delta = eps * (std::min(r1[2], r2[2]) + std::min(r1[3], r2[3])) * 0.5;
+                return std::abs(r1[0] - r2[0]) <= delta && std::abs(r1[1] - r2[1]) <= delta &&
+                       std::abs(r1[0] + r1[2] - r2[0] - r2[2]) <= delta && std::abs(r1[1] + r1[3] - r2[1] - r2[3]) <= delta;
+            };
+            // cv::partition
+            std::vector<int> par(nc, -1), rk(nc, 0);
+            auto root = [&](int i) {
+                while (par[i] >= 0) i = par[i];
+                return i;
+            };
+            for (int i = 0; i < nc; ++i) {
+                int r = root(i);
+                for (int j = 0; j < nc; ++j) {
+                    if (i == j || !similar(i, j)) continue;
+                    int r2 = root(j);
+                    if (r2 == r) continue;
+                    if (rk[r] > rk[r2]) {
+                        par[r2] = r;
+                    } else {
+                        par[r] = r2;
+                        rk[r2] += rk[r] == rk[r2];
+                        r = r2;
+                    }
+                    for (int k = j, p; (p = par[k]) >= 0; k = p) par[k] = r;
+                    for (int k = i, p; (p = par[k]) >= 0; k = p) par[k] = r;
+                }
+            }
+            std::vector<int> lab(nc), cls_of_root(nc, -1);
+            int ncls = 0;
+            for (int i = 0; i < nc; ++i) {
+                const int r = root(i);
+                if (cls_of_root[r] < 0) cls_of_root[r] = ncls++;
+                lab[i] = cls_of_root[r];
+            }
+            std::vector<long long> acc(4 * (size_t)ncls, 0);
+            std::vector<int> cnt(ncls, 0);
+            for (int i = 0; i < nc; ++i) {
+                for (int k = 0; k < 4; ++k) acc[4 * lab[i] + k] += c[4 * i + k];
+                cnt[lab[i]]++;
+            }
+            std::vector<int32_t> avg(4 * (size_t)ncls);
+            for (int l = 0; l < ncls; ++l) {
+                const float sinv = 1.f / (float)cnt[l];
+                for (int k = 0; k < 4; ++k) avg[4 * l + k] = rne_f((float)(int)acc[4 * l + k] * sinv);
+            }
+            for (int i = 0; i < ncls; ++i) {
+                const int32_t* r1 = &avg[4 * i];
+                const int n1 = cnt[i];
+                if (n1 <= min_neighbors) continue;
+                int j = 0;
+                for (; j < ncls; ++j) {
+                    const int n2 = cnt[j];
+                    if (j == i || n2 <= min_neighbors) continue;
+                    const int32_t* r2 = &avg[4 * j];
+                    const int dx = rne_d(r2[2] * eps), dy = rne_d(r2[3] * eps);
+                    if (r1[0] >= r2[0] - dx && r1[1] >= r2[1] - dy && r1[0] + r1[2] <= r2[0] + r2[2] + dx &&
+                        r1[1] + r1[3] <= r2[1] + r2[3] + dy && (n2 > std::max(3, n1) || n1 < 3))
+                        break;
+                }
+                if (j == ncls) outr.insert(outr.end(), r1, r1 + 4);
+            }
+        }
+        const int no = (int)outr.size() / 4;
+        counts[img] = no;
+        const int keep = std::min(no, cap);
+        if (keep > 0) std::memcpy(rects + (size_t)img * cap * 4, outr.data(), sizeof(int32_t) * 4 * keep);
+    }
+    return FM_OK;
+}
+
+int fm_haar_candidates(const fm_haar* h, int32_t* rects, int cap) {
+    if (!h || cap < 0 || (cap > 0 && !rects)) return FM_EINVAL;
+    const int nc = (int)h->cand.size() / 4;
+    const int k = std::min(nc, cap);
+    if (k > 0) std::memcpy(rects, h->cand.data(), sizeof(int32_t) * 4 * k);
+    return nc;
+}
+
+double fm_haar_last_ms(const fm_haar* h) { return h ? h->last_ms : 0.; }
+
+}  // extern "C"

@@ -153,6 +153,49 @@ int fm_reset_kernel_times(fm_ctx* ctx);
 int fm_rasterize_masks(int h, int w, double scale, const int32_t* xy, const int32_t* npts,
                        int n_polys, uint8_t* keep);
 
+/* ---- Object-ROI stage ----------------------------------
+ * Replaces cv2.CascadeClassifier(path) + detectMultiScale(frame.resized,
+ * scaleFactor=1.1, minNeighbors=5) at find_motion.py:396 and :722-731 for HAAR
+ * cascades (find_motion_amd/cascade.py reads the XML into this description).
+ * Independent of fm_ctx: one detector per cascade and device. */
+typedef struct fm_haar fm_haar;
+typedef struct fm_haar_desc {
+    int win_w, win_h;                /* <width>, <height> */
+    int n_stages, n_trees, n_nodes, n_leaves, n_features;
+    const int32_t* stage_ntrees;     /* [n_stages] weak classifiers per stage */
+    const float* stage_threshold;    /* [n_stages] (float)value - 1e-5f, as Data::read */
+    const int32_t* tree_nodes;       /* [n_trees] internal nodes per tree */
+    const int32_t* node_left;        /* [n_nodes] > 0: node of the same tree, <= 0: leaf -v */
+    const int32_t* node_right;       /* [n_nodes] */
+    const int32_t* node_feature;     /* [n_nodes] feature index */
+    const float* node_threshold;     /* [n_nodes] */
+    const float* leaves;             /* [n_leaves] = tree nodes + 1 per tree */
+    const int32_t* feat_rects;       /* [n_features][3][4] x y w h */
+    const float* feat_weights;       /* [n_features][3], 0 = unused third rect */
+    const uint8_t* feat_tilted;      /* [n_features] or NULL */
+} fm_haar_desc;
+
+/* Validate and upload a cascade (FM_EINVAL before any HIP call when the
+ * description is inconsistent).  *out is set even on failure so that
+ * fm_haar_last_error can say why; release it with fm_haar_destroy. */
+int fm_haar_create(int device, const fm_haar_desc* desc, fm_haar** out);
+void fm_haar_destroy(fm_haar* det);
+const char* fm_haar_last_error(const fm_haar* det);
+int fm_haar_window(const fm_haar* det, int* w, int* h);
+
+/* detectMultiScale over n images of one size ([n][H][W][channels] u8, BGR or
+ * gray; host memory, or device memory when on_device).  max_w/max_h 0 = the
+ * image size.  rects: [n][cap][4] (x, y, w, h), counts[n] = detections per
+ * image (may exceed cap; only cap are written).  Synchronous. */
+int fm_haar_detect(fm_haar* det, const uint8_t* images, int n, int H, int W, int channels, int on_device,
+                   double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h,
+                   int32_t* rects, int cap, int32_t* counts);
+/* The ungrouped candidates of image 0 of the last fm_haar_detect (parity
+ * tests); returns their number. */
+int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);
+/* Device time of the last fm_haar_detect's kernels (HIP events), ms. */
+double fm_haar_last_ms(const fm_haar* det);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,69 @@
+"""GPU parity of the object-ROI stage (fm_haar_*) against
+oracle/haar.py: the ungrouped candidate rects of detectMultiScaleNoGrouping and
+the grouped detections must be identical (integer rects, same order).
+Cascades and images are synthetic (tests/haar_cases.py); the reference's
+cascade files are not on the GPU box.  Parity vs OpenCV itself: unpinned.
+"""
+import numpy as np
+import pytest
+
+from find_motion_amd import CascadeClassifier
+from haar_cases import make_cascade, make_image
+from oracle import haar
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    (1, 0.41, dict(depth=2)),                 # stumps + depth-2 trees, ~120 candidates
+    (1, 0.38, dict(depth=2, tilted=True)),    # tilted features, ~2k candidates
+    (3, 0.44, dict()),                        # stumps, ~9k candidates
+    (3, 0.41, dict(tilted=True)),             # tilted stumps, ~12k candidates
+    (1, 0.38, dict(stages=6, trees=6)),       # deeper cascade
+    (1, 0.50, dict()),                        # rejects everything
+]
+
+
+@pytest.mark.parametrize("seed,tight,kw", CASES)
+def test_candidates_and_groups_match_oracle(seed, tight, kw):
+    cs = make_cascade(seed, tight=tight, **kw)
+    img = make_image(2)
+    det = CascadeClassifier(cs)
+    got = det.detectMultiScale(img, scaleFactor=1.1, minNeighbors=5)
+    cand = det.candidates()
+    ref_c = haar.detect_candidates(cs, img, 1.1)
+    assert [tuple(r) for r in cand.tolist()] == ref_c
+    ref = haar.group_rectangles(ref_c, 5)
+    assert [tuple(r) for r in np.asarray(got).reshape(-1, 4).tolist()] == ref
+    det.close()
+
+
+def test_batch_of_images_and_gray_input():
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    imgs = np.stack([make_image(s) for s in range(5)])
+    det = CascadeClassifier(cs)
+    got = det.detect_batch(imgs, 1.1, 3)
+    for i in range(len(imgs)):
+        ref = haar.detect_multiscale(cs, imgs[i], 1.1, 3)
+        assert [tuple(r) for r in got[i].tolist()] == ref, i
+    g = haar.bgr2gray(imgs[0])
+    got1 = det.detect_batch(g[None], 1.1, 3)[0]
+    assert [tuple(r) for r in got1.tolist()] == haar.detect_multiscale(cs, g, 1.1, 3)
+    det.close()
+
+
+@pytest.mark.parametrize("size,sf,mn,mins,maxs", [
+    ((300, 169), 1.2, 2, (30, 30), (0, 0)),
+    ((300, 169), 1.05, 5, (0, 0), (90, 90)),
+    ((173, 97), 1.1, 0, (0, 0), (0, 0)),      # minNeighbors 0: raw candidates
+    ((21, 20), 1.1, 1, (0, 0), (0, 0)),       # one window position
+    ((19, 40), 1.1, 1, (0, 0), (0, 0)),       # narrower than the window: nothing
+])
+def test_sizes_scale_factors_and_limits(size, sf, mn, mins, maxs):
+    cs = make_cascade(1, tight=0.41, depth=2)
+    w, h = size
+    img = make_image(7, w=max(w, 40), h=max(h, 40))[:h, :w]
+    det = CascadeClassifier(cs)
+    got = det.detectMultiScale(np.ascontiguousarray(img), scaleFactor=sf, minNeighbors=mn, minSize=mins, maxSize=maxs)
+    ref = haar.detect_multiscale(cs, img, sf, mn, mins, maxs)
+    assert [tuple(r) for r in np.asarray(got).reshape(-1, 4).tolist()] == ref
+    det.close()

@@ -1,0 +1,257 @@
+"""Object-ROI stage on the CPU: the cascade reader, the
+detectMultiScale restatement (oracle/haar.py) against brute force and known
+answers, and the C ABI's cascade validation (no device calls).
+
+Parity unpinned: OpenCV is absent and the reference holds no detection
+fixtures; the restatement is pinned by the known-answer and brute-force checks
+here, the GPU path by tests/test_gpu_haar.py against it.
+"""
+import ctypes as C
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from find_motion_amd import _native
+from find_motion_amd.cascade import CASCADE_LOOKUP, THRESHOLD_EPS, parse, to_xml
+from haar_cases import make_cascade, make_image
+from oracle import haar
+
+REF_CASCADES = "/root/reference/find_motion/haarcascades"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASCADES), reason="reference cascades not present")
+def test_reference_cascades_parse():
+    # every cascade the reference can load (CASCADE_LOOKUP, find_motion.py:104-122) reads into
+    # consistent arrays; the one old-format file is refused
+    for name in CASCADE_LOOKUP:
+        cs = parse(os.path.join(REF_CASCADES, f"haarcascade_{name}.xml"))
+        assert cs.n_stages > 0 and cs.stage_ntrees.sum() == len(cs.tree_nodes)
+        assert cs.tree_nodes.sum() == len(cs.node_left) == len(cs.node_threshold)
+        assert len(cs.leaves) == len(cs.tree_nodes) + len(cs.node_left)
+        assert cs.node_feature.max() < len(cs.feat_tilted)
+        assert cs.has_tilted == (name in ("frontalcatface_extended", "fullbody", "lowerbody")), name
+    d = parse(os.path.join(REF_CASCADES, "haarcascade_frontalface_default.xml"))
+    assert (d.win_w, d.win_h, d.n_stages) == (24, 24, 25)
+    assert d.stage_threshold[0] == np.float32(np.float32(-5.0425500869750977) - THRESHOLD_EPS)
+    with pytest.raises(ValueError):
+        parse(os.path.join(REF_CASCADES, "haarcascade_licence_plate_rus_16stages.xml"))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASCADES), reason="reference cascades not present")
+def test_reference_cascades_pass_the_abi_validation():
+    # fm_haar_create validates before touching the device: on this CPU-only host a valid
+    # description fails only at the first HIP call (FM_EHIP), never with FM_EINVAL
+    for name in CASCADE_LOOKUP:
+        cs = parse(os.path.join(REF_CASCADES, f"haarcascade_{name}.xml"))
+        rc, msg = _create(cs)
+        assert rc in (_native.FM_OK, _native.FM_EHIP), (name, msg)
+
+
+def _create(cs):
+    L = _native.load()
+    keep = [np.ascontiguousarray(a) for a in (cs.stage_ntrees, cs.stage_threshold, cs.tree_nodes, cs.node_left,
+                                              cs.node_right, cs.node_feature, cs.node_threshold, cs.leaves,
+                                              cs.feat_rects, cs.feat_weights, cs.feat_tilted)]
+    d = _native.FMHaarDesc(cs.win_w, cs.win_h, len(cs.stage_ntrees), len(cs.tree_nodes), len(cs.node_left),
+                           len(cs.leaves), len(cs.feat_tilted), *[a.ctypes.data for a in keep])
+    h = C.c_void_p()
+    rc = L.fm_haar_create(0, C.byref(d), C.byref(h))
+    msg = L.fm_haar_last_error(h).decode()
+    L.fm_haar_destroy(h)
+    return rc, msg
+
+
+def test_abi_rejects_inconsistent_cascades():
+    base = make_cascade(0, tilted=True)
+    assert _create(base)[0] in (_native.FM_OK, _native.FM_EHIP)
+    bad = []
+    c = make_cascade(0)
+    c.node_feature = c.node_feature.copy()
+    c.node_feature[0] = len(c.feat_tilted)
+    bad.append(c)
+    c = make_cascade(0)
+    c.feat_rects = c.feat_rects.copy()
+    c.feat_rects[0, 0, 2] = c.win_w + 1
+    bad.append(c)
+    c = make_cascade(0)
+    c.leaves = c.leaves[:-1]
+    bad.append(c)
+    c = make_cascade(0, depth=2)
+    c.node_left = c.node_left.copy()
+    c.node_left[1] = 5  # link out of the tree
+    bad.append(c)
+    c = make_cascade(0)
+    c.feat_tilted = c.feat_tilted.copy()
+    c.feat_tilted[0] = 1  # the full-window rect cannot be a tilted rect
+    bad.append(c)
+    for c in bad:
+        rc, msg = _create(c)
+        assert rc == _native.FM_EINVAL and msg
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(depth=2), dict(tilted=True, depth=2)])
+def test_xml_round_trip(kw):
+    cs = make_cascade(5, **kw)
+    cs2 = parse(to_xml(cs))
+    for f in cs.__dataclass_fields__:
+        assert np.array_equal(getattr(cs, f), getattr(cs2, f)), f
+
+
+def test_linear_exact_known_answers():
+    # identity, exact 2x (= INTER_AREA fast path (a+b+c+d+2)>>2), 1-row 2 -> 4 upscale
+    rng = np.random.default_rng(0)
+    g = rng.integers(0, 256, (17, 23), dtype=np.uint8)
+    assert np.array_equal(haar.resize_linear_exact(g, 23, 17), g)
+    g = rng.integers(0, 256, (16, 24), dtype=np.uint8)
+    a = g.astype(np.int32)
+    ref = (a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(haar.resize_linear_exact(g, 12, 8), ref)
+    assert haar.resize_linear_exact(np.array([[0, 255]], np.uint8), 4, 1).tolist() == [[0, 64, 191, 255]]
+
+
+def test_integrals_brute_force():
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (9, 13), dtype=np.uint8)
+    S, Q, T = haar.integrals(img, True)
+    h, w = img.shape
+    v = img.astype(np.int64)
+    for Y in range(h + 1):
+        for X in range(w + 1):
+            assert S[Y, X] == v[:Y, :X].sum()
+            assert Q[Y, X] == (v[:Y, :X] ** 2).sum()
+            t = sum(int(v[y, x]) for y in range(Y) for x in range(w) if abs(x - X + 1) <= Y - y - 1)
+            assert T[Y, X] == t
+
+
+def _eval_one(cs, S, Q, T, x, y):
+    """One window, scalar, straight from HaarEvaluator::setWindow + predictOrdered."""
+    W, H = cs.win_w, cs.win_h
+
+    def rs(I, r, tl):
+        rx, ry, rw, rh = (int(v) for v in r)
+        if not tl:
+            v = int(I[y + ry, x + rx]) - int(I[y + ry, x + rx + rw]) - int(I[y + ry + rh, x + rx]) + \
+                int(I[y + ry + rh, x + rx + rw])
+        else:
+            v = int(I[y + ry, x + rx]) - int(I[y + ry + rh, x + rx - rh]) - int(I[y + ry + rw, x + rx + rw]) + \
+                int(I[y + ry + rw + rh, x + rx + rw - rh])
+        return (v + (1 << 31)) % (1 << 32) - (1 << 31)
+
+    area = float((W - 2) * (H - 2))
+    vs = rs(S, (1, 1, W - 2, H - 2), False)
+    vq = rs(Q, (1, 1, W - 2, H - 2), False) & 0xFFFFFFFF
+    nf = area * vq - float(vs) * vs
+    if not nf > 0:
+        return -1
+    vnf = np.float32(1.0 / np.sqrt(nf))
+    if not area * float(vnf) < 0.1:
+        return -1
+    ti = ni = li = 0
+    for si in range(cs.n_stages):
+        tot = 0.0
+        for _ in range(int(cs.stage_ntrees[si])):
+            idx = 0
+            while True:
+                nd = ni + idx
+                f = int(cs.node_feature[nd])
+                I = T if cs.feat_tilted[f] else S
+                val = np.float32(cs.feat_weights[f, 0] * np.float32(rs(I, cs.feat_rects[f, 0], cs.feat_tilted[f])))
+                val = np.float32(val + np.float32(cs.feat_weights[f, 1] *
+                                                  np.float32(rs(I, cs.feat_rects[f, 1], cs.feat_tilted[f]))))
+                if cs.feat_weights[f, 2] != 0:
+                    val = np.float32(val + np.float32(cs.feat_weights[f, 2] *
+                                                      np.float32(rs(I, cs.feat_rects[f, 2], cs.feat_tilted[f]))))
+                val = np.float32(val * vnf)
+                idx = int(cs.node_left[nd] if float(val) < float(cs.node_threshold[nd]) else cs.node_right[nd])
+                if idx <= 0:
+                    break
+            tot += float(cs.leaves[li - idx])
+            ni += int(cs.tree_nodes[ti])
+            li += int(cs.tree_nodes[ti]) + 1
+            ti += 1
+        if tot < float(cs.stage_threshold[si]):
+            return -si
+    return 1
+
+
+@pytest.mark.parametrize("seed,tight,kw", [(1, 0.41, dict(depth=2)), (1, 0.38, dict(depth=2, tilted=True)),
+                                           (3, 0.44, dict())])
+def test_eval_windows_matches_scalar(seed, tight, kw):
+    cs = make_cascade(seed, tight=tight, **kw)
+    img = haar.bgr2gray(make_image(2))[30:140, 130:250]
+    S, Q, T = haar.integrals(img, cs.has_tilted)
+    gy, gx = np.meshgrid(np.arange(0, img.shape[0] + 1 - cs.win_h, 2), np.arange(0, img.shape[1] + 1 - cs.win_w, 2),
+                         indexing="ij")
+    res = haar.eval_windows(cs, S, Q, T, gx.ravel(), gy.ravel())
+    ref = np.array([_eval_one(cs, S, Q, T, int(x), int(y)) for x, y in zip(gx.ravel(), gy.ravel())])
+    assert np.array_equal(res, ref)
+    assert (ref == 0).any() and (ref != 0).any()
+
+
+def test_scale_list_roi_frame():
+    # the reference's ROI frame: width 300 from a 16:9 source -> 300 x 168; 24x24 window
+    sc = haar.scale_list(300, 168, 24, 24, 1.1)
+    assert sc[0] == np.float32(1.0) and len(sc) == 21  # 1.1^20 * 24 = 161 <= 168 < 178
+    assert all(round(24 * float(s)) <= 168 for s in sc)
+    assert haar.scale_list(300, 168, 24, 24, 1.1, min_size=(40, 40))[0] > np.float32(1.6)
+    assert haar.scale_list(20, 20, 24, 24) == []
+
+
+def _partition_scalar(rects, eps):
+    n = len(rects)
+    parent, rank = [-1] * n, [0] * n
+
+    def root(i):
+        while parent[i] >= 0:
+            i = parent[i]
+        return i
+
+    for i in range(n):
+        r = root(i)
+        for j in range(n):
+            if i == j or not haar._similar(rects[i], rects[j], eps):
+                continue
+            r2 = root(j)
+            if r2 != r:
+                if rank[r] > rank[r2]:
+                    parent[r2] = r
+                else:
+                    parent[r] = r2
+                    rank[r2] += rank[r] == rank[r2]
+                    r = r2
+                for k0 in (j, i):
+                    k = k0
+                    while parent[k] >= 0:
+                        p = parent[k]
+                        parent[k] = r
+                        k = p
+    lab, out = {}, []
+    for i in range(n):
+        out.append(lab.setdefault(root(i), len(lab)))
+    return out, len(lab)
+
+
+def test_partition_vectorised_matches_scalar():
+    rng = np.random.default_rng(4)
+    for _ in range(5):
+        rects = [(int(x), int(y), int(s), int(s)) for x, y, s in
+                 zip(rng.integers(0, 60, 120), rng.integers(0, 60, 120), rng.integers(20, 30, 120))]
+        assert haar.partition(rects, 0.2) == _partition_scalar(rects, 0.2)
+
+
+def test_group_rectangles_known_answers():
+    # 6 similar rects -> one class (6 > 5 neighbours) with the rounded mean; a class of 2 is dropped
+    cl = [(100, 100, 40, 40), (101, 100, 40, 40), (100, 102, 41, 41), (99, 100, 40, 40), (100, 99, 40, 40),
+          (102, 101, 40, 40)]
+    far = [(10, 10, 30, 30), (11, 10, 30, 30)]
+    got = haar.group_rectangles(cl + far, 5)
+    assert got == [(100, 100, 40, 40)]  # means 100.33, 100.33, 40.17, 40.17
+    # a weaker class inside a stronger one is dropped; equal-strength nested classes both stay unless n2 > max(3, n1)
+    big = [(50, 50, 100, 100)] * 9
+    small = [(70, 70, 30, 30)] * 6
+    assert haar.group_rectangles(big + small, 5) == [(50, 50, 100, 100)]
+    assert sorted(haar.group_rectangles([(50, 50, 100, 100)] * 6 + small, 5)) == [(50, 50, 100, 100), (70, 70, 30, 30)]
+    # minNeighbors 0: the candidates unchanged
+    assert haar.group_rectangles(cl, 0) == cl
