@@ -28,7 +28,7 @@ EXPORTED = (
     "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
     "fm_host_alloc", "fm_host_free",
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
-    "fm_haar_candidates", "fm_haar_last_ms",
+    "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
 )
 
 
@@ -109,6 +109,7 @@ def load() -> C.CDLL:
     L.fm_haar_window.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
     L.fm_haar_detect.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, i32, i32, i32, i32, vp, i32, vp]
     L.fm_haar_candidates.argtypes = [vp, vp, i32]
+    L.fm_haar_detect_frames.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
     L.fm_haar_last_ms.argtypes = [vp]
     L.fm_haar_last_ms.restype = C.c_double
     for name in EXPORTED:
@@ -363,6 +364,24 @@ class CascadeClassifier:
                                   _ptr(rects), cap, _ptr(counts))
             if rc != FM_OK:
                 raise FMError(rc, f"fm_haar_detect: {L.fm_haar_last_error(self._h).decode()}")
+            if counts.max(initial=0) <= cap:
+                return [rects[i, :counts[i]].copy() for i in range(n)]
+            cap = int(counts.max())
+
+    def detect_frames(self, frames: np.ndarray, roi_w: int = 300, scaleFactor=1.1, minNeighbors=5, cap: int = 256):
+        """find_objects on raw BGR frames [n, H, W, 3]: INTER_AREA to width roi_w on the device, then
+        detectMultiScale; rects are in ROI coordinates (as find_motion.py:724-729 stores them)."""
+        L = load()
+        fr = np.ascontiguousarray(frames, np.uint8)
+        n, H, W = fr.shape[:3]
+        rh = C.c_int32()
+        while True:
+            rects = np.zeros((n, cap, 4), np.int32)
+            counts = np.zeros(n, np.int32)
+            rc = L.fm_haar_detect_frames(self._h, _ptr(fr), n, H, W, 0, int(roi_w), float(scaleFactor),
+                                         int(minNeighbors), _ptr(rects), cap, _ptr(counts), C.byref(rh))
+            if rc != FM_OK:
+                raise FMError(rc, f"fm_haar_detect_frames: {L.fm_haar_last_error(self._h).decode()}")
             if counts.max(initial=0) <= cap:
                 return [rects[i, :counts[i]].copy() for i in range(n)]
             cap = int(counts.max())

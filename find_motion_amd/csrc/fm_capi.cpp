@@ -142,6 +142,8 @@ int fail(fm_ctx* c, int code, const char* fmt, ...) {
 // computeResizeAreaTab (OpenCV imgproc resize.cpp) restated on the product
 // side: for each destination index the weights over consecutive source
 // indices, in the order OpenCV accumulates them.
+}  // namespace
+namespace fm {
 bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A) {
     A.n_dst = dsize;
     std::vector<std::vector<std::pair<int, float>>> taps(dsize);
@@ -173,6 +175,8 @@ bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A) {
     }
     return true;
 }
+}  // namespace fm
+namespace {
 
 // getGaussianKernelBitExact + getGaussianKernelFixedPoint_ED (OpenCV imgproc
 // smooth.dispatch.cpp) restated: the 8-bit fixed-point taps GaussianBlur

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/find_motion_amd.h"
+#include "fm_internal.h"
 
 namespace fm {
 namespace haar {
@@ -246,6 +247,12 @@ struct fm_haar {
     uint32_t *d_S = nullptr, *d_Q = nullptr, *d_T = nullptr;
     int8_t* d_res = nullptr;
     int2* d_taps = nullptr;
+    uint8_t *d_raw = nullptr, *d_roi = nullptr;  // fm_haar_detect_frames: source frames, ROI frames
+    int32_t *d_axo = nullptr, *d_axc = nullptr, *d_ayo = nullptr, *d_ayc = nullptr;
+    float *d_axw = nullptr, *d_ayw = nullptr;
+    int area_key[4] = {0, 0, 0, 0};  // (W, H, w, h) the area tables are for
+    fm::AreaAxis ax, ay;
+    size_t cap_raw = 0, cap_roi = 0;
     size_t cap_src = 0, cap_gray = 0, cap_rimg = 0, cap_S = 0, cap_Q = 0, cap_T = 0, cap_res = 0, cap_taps = 0;
     std::vector<int8_t> h_res;
     std::vector<int32_t> cand;  // last call's candidates of image 0 (x, y, w, h)
@@ -417,7 +424,9 @@ void fm_haar_destroy(fm_haar* h) {
     if (!h) return;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_blob, (void*)h->d_src, (void*)h->d_gray, (void*)h->d_rimg, (void*)h->d_S,
-                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps})
+                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw,
+                    (void*)h->d_roi, (void*)h->d_axo, (void*)h->d_axc, (void*)h->d_ayo, (void*)h->d_ayc,
+                    (void*)h->d_axw, (void*)h->d_ayw})
         if (p) (void)hipFree(p);
     if (h->e0) (void)hipEventDestroy(h->e0);
     if (h->e1) (void)hipEventDestroy(h->e1);
@@ -646,5 +655,66 @@ int fm_haar_candidates(const fm_haar* h, int32_t* rects, int cap) {
 }
 
 double fm_haar_last_ms(const fm_haar* h) { return h ? h->last_ms : 0.; }
+
+int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W, int on_device, int roi_w,
+                          double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
+                          int* roi_h_out) {
+    if (!h || !h->d_blob) return FM_EINVAL;
+    if (!frames || n < 1 || H < 1 || W < 1 || roi_w < 1)
+        return hfail(h, FM_EINVAL, "bad arguments (n >= 1, frame and ROI sizes >= 1)");
+    const int rw = roi_w, rh = (int)(H * ((double)roi_w / (double)W));  // imutils.resize(raw, width=roi_w)
+    if (roi_h_out) *roi_h_out = rh;
+    if (rh < 1) return hfail(h, FM_EINVAL, "ROI height 0 for a %dx%d frame", W, H);
+    const double sx = 1. / ((double)rw / W), sy = 1. / ((double)rh / H);
+    const bool identity = rw == W && rh == H;
+    if (!identity && !(sx >= 1 && sy >= 1))
+        return hfail(h, FM_ENOTSUP, "frame width %d < ROI width %d: INTER_AREA upscaling is not supported", W, rw);
+    HH(h, hipSetDevice(h->device));
+    const size_t fb = (size_t)H * W * 3;
+    const uint8_t* src = frames;
+    int rc;
+    if (!on_device) {
+        if ((rc = grow(h, &h->d_raw, h->cap_raw, n * fb))) return rc;
+        HH(h, hipMemcpyAsync(h->d_raw, frames, n * fb, hipMemcpyHostToDevice, h->stream));
+        src = h->d_raw;
+    }
+    const uint8_t* roi = src;
+    if (!identity) {
+        if ((rc = grow(h, &h->d_roi, h->cap_roi, (size_t)n * rh * rw * 3))) return rc;
+        const int isx = (int)std::lrint(sx), isy = (int)std::lrint(sy);
+        if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16) {
+            HH(h, fm::launch_resize_area_fast(h->stream, src, h->d_roi, n, H, W, rh, rw, isx, isy));
+        } else {
+            if (h->area_key[0] != W || h->area_key[1] != H || h->area_key[2] != rw || h->area_key[3] != rh) {
+                if (!fm::build_area_axis(W, rw, sx, h->ax) || !fm::build_area_axis(H, rh, sy, h->ay))
+                    return hfail(h, FM_ENOTSUP, "INTER_AREA table with non-consecutive taps");
+                HH(h, hipStreamSynchronize(h->stream));
+                for (void* p : {(void*)h->d_axo, (void*)h->d_axc, (void*)h->d_ayo, (void*)h->d_ayc, (void*)h->d_axw,
+                                (void*)h->d_ayw})
+                    if (p) HH(h, hipFree(p));
+                HH(h, hipMalloc((void**)&h->d_axo, h->ax.ofs.size() * 4));
+                HH(h, hipMalloc((void**)&h->d_axc, h->ax.cnt.size() * 4));
+                HH(h, hipMalloc((void**)&h->d_axw, h->ax.wt.size() * 4));
+                HH(h, hipMalloc((void**)&h->d_ayo, h->ay.ofs.size() * 4));
+                HH(h, hipMalloc((void**)&h->d_ayc, h->ay.cnt.size() * 4));
+                HH(h, hipMalloc((void**)&h->d_ayw, h->ay.wt.size() * 4));
+                HH(h, hipMemcpy(h->d_axo, h->ax.ofs.data(), h->ax.ofs.size() * 4, hipMemcpyHostToDevice));
+                HH(h, hipMemcpy(h->d_axc, h->ax.cnt.data(), h->ax.cnt.size() * 4, hipMemcpyHostToDevice));
+                HH(h, hipMemcpy(h->d_axw, h->ax.wt.data(), h->ax.wt.size() * 4, hipMemcpyHostToDevice));
+                HH(h, hipMemcpy(h->d_ayo, h->ay.ofs.data(), h->ay.ofs.size() * 4, hipMemcpyHostToDevice));
+                HH(h, hipMemcpy(h->d_ayc, h->ay.cnt.data(), h->ay.cnt.size() * 4, hipMemcpyHostToDevice));
+                HH(h, hipMemcpy(h->d_ayw, h->ay.wt.data(), h->ay.wt.size() * 4, hipMemcpyHostToDevice));
+                h->area_key[0] = W;
+                h->area_key[1] = H;
+                h->area_key[2] = rw;
+                h->area_key[3] = rh;
+            }
+            HH(h, fm::launch_resize_area(h->stream, src, h->d_roi, n, H, W, rh, rw, h->d_axo, h->d_axc, h->d_axw,
+                                         h->ax.max_taps, h->d_ayo, h->d_ayc, h->d_ayw, h->ay.max_taps));
+        }
+        roi = h->d_roi;
+    }
+    return fm_haar_detect(h, roi, n, rh, rw, 3, 1, scale_factor, min_neighbors, 0, 0, 0, 0, rects, cap, counts);
+}
 
 }  // extern "C"

@@ -114,6 +114,9 @@ struct FusedArgs {
     int32_t coef[kMaxK];
 };
 
+// computeResizeAreaTab restated (fm_capi.cpp); false if a destination's taps are not consecutive
+bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A);
+
 // Kernel launchers (fm_kernels.hip, fm_fused.hip).  All asynchronous on `st`.
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
                               int h, int w, const int32_t* xofs, const int32_t* xcnt, const float* xwt,

@@ -36,6 +36,7 @@ NativeLibraryMissing at VideoMotion construction.
 from __future__ import annotations
 
 import copy
+import importlib.util
 import logging
 import math
 import os
@@ -45,7 +46,7 @@ from collections import deque
 import numpy as np
 
 from . import videoio
-from ._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, MotionEngine, rasterize_masks
+from ._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, CascadeClassifier, MotionEngine, rasterize_masks
 
 log = logging.getLogger("find_motion_amd")
 
@@ -170,7 +171,7 @@ class VideoMotion:
                  cascades: typing.List[str] = None,
                  yolo_tiny: bool = False, *,
                  device: int = 0, batch: int = 1, capture=None, engine: MotionEngine = None,
-                 stream: int = 0, keep_planes: bool = None) -> None:
+                 stream: int = 0, keep_planes: bool = None, cascade_dir: str = None) -> None:
         self.filename = filename
         if self.filename is None and capture is None:
             raise Exception("Filename required")
@@ -194,6 +195,8 @@ class VideoMotion:
         self.mask_areas = mask_areas if mask_areas is not None else []
         self.show = show
         self.cascade_names = cascades
+        self.cascade_dir = cascade_dir
+        self.device = int(device)
         self.codec = codec
         self.debug = log_level == logging.DEBUG
         self.mem = mem
@@ -232,21 +235,28 @@ class VideoMotion:
 
     # -- init (fm.py:383-484) ------------------------------------------------
     def _load_cascades(self) -> None:
-        """fm.py:383-399 (needs OpenCV's CascadeClassifier; without cv2 no cascade is loaded)."""
+        """fm.py:383-399: the named cascades, read from haarcascade_<name>.xml and run on the GPU
+        (find_motion_amd.CascadeClassifier).  Files are looked up in `cascade_dir`, $FM_HAARCASCADES,
+        the installed reference package's haarcascades/ (FIND_MOTION_PATH), then cv2.data."""
         self.cascades = dict()
         if self.cascade_names is None:
             return
         names = copy.copy(CASCADE_LOOKUP) if "ALL" in self.cascade_names else {
             c: CASCADE_LOOKUP[c] for c in self.cascade_names if c in CASCADE_LOOKUP}
+        dirs = [d for d in (self.cascade_dir, os.environ.get("FM_HAARCASCADES")) if d]
+        spec = importlib.util.find_spec("find_motion")
+        if spec is not None and spec.origin:
+            dirs.append(os.path.join(os.path.dirname(spec.origin), "haarcascades"))
         cv2 = videoio.cv2
-        if cv2 is None:
-            if names:
-                self.log.warning("Haar cascades %s need OpenCV, which is not installed: object detection off",
-                                 list(names))
-            return
-        base = os.path.join(cv2.data.haarcascades) if hasattr(cv2, "data") else ""
-        self.cascades = {title: cv2.CascadeClassifier(os.path.join(base, f"haarcascade_{c}.xml"))
-                         for c, title in names.items()}
+        if cv2 is not None and hasattr(cv2, "data"):
+            dirs.append(cv2.data.haarcascades)
+        for c, title in names.items():
+            path = next((os.path.join(d, f"haarcascade_{c}.xml") for d in dirs
+                         if os.path.isfile(os.path.join(d, f"haarcascade_{c}.xml"))), None)
+            if path is None:
+                self.log.warning("cascade %s not found in %s: skipped", c, dirs)
+                continue
+            self.cascades[title] = CascadeClassifier(path, device=self.device)
 
     def _calc_min_area(self) -> None:
         """fm.py:402-406"""
@@ -479,14 +489,13 @@ class VideoMotion:
             return set()
         self.object_counter = 0
         self.last_objects = {}
-        cv2 = videoio.cv2
-        if cv2 is not None and self.cascades:
-            h = int(frame.raw.shape[0] * (width / float(frame.raw.shape[1])))
-            frame.resized = cv2.resize(frame.raw, (width, h), interpolation=cv2.INTER_AREA)
+        if self.cascades:
+            # frame.resized = imutils.resize(frame.raw, width=width) happens on the device inside
+            # detect_frames (INTER_AREA); rects are in ROI coordinates as in the reference
             for title, cascade in self.cascades.items():
-                found = cascade.detectMultiScale(frame.resized, scaleFactor=scaleFactor, minNeighbors=minNeighbours)
+                found = cascade.detect_frames(frame.raw[None], width, scaleFactor, minNeighbours)[0]
                 for rect in found:
-                    self.last_objects.setdefault(title, []).append(VideoMotion.make_area_from_rect(rect))
+                    self.last_objects.setdefault(title, []).append(VideoMotion.make_area_from_rect(tuple(int(v) for v in rect)))
         return set(self.last_objects.keys())
 
     # -- display (fm.py:765-821): only with OpenCV and --show

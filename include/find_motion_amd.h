@@ -190,6 +190,13 @@ int fm_haar_window(const fm_haar* det, int* w, int* h);
 int fm_haar_detect(fm_haar* det, const uint8_t* images, int n, int H, int W, int channels, int on_device,
                    double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h,
                    int32_t* rects, int cap, int32_t* counts);
+/* find_objects (find_motion.py:703-731) on raw frames: each [H][W][3] BGR
+ * frame is resized to width roi_w with INTER_AREA on the device
+ * (imutils.resize: height int(H * roi_w / W), *roi_h_out), then detected as
+ * fm_haar_detect with default min/max sizes.  FM_ENOTSUP when W < roi_w. */
+int fm_haar_detect_frames(fm_haar* det, const uint8_t* frames, int n, int H, int W, int on_device, int roi_w,
+                          double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
+                          int* roi_h_out);
 /* The ungrouped candidates of image 0 of the last fm_haar_detect (parity
  * tests); returns their number. */
 int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);

@@ -9,6 +9,7 @@ import pytest
 
 from find_motion_amd import CascadeClassifier
 from haar_cases import make_cascade, make_image
+import oracle
 from oracle import haar
 
 pytestmark = pytest.mark.gpu
@@ -67,3 +68,49 @@ def test_sizes_scale_factors_and_limits(size, sf, mn, mins, maxs):
     ref = haar.detect_multiscale(cs, img, sf, mn, mins, maxs)
     assert [tuple(r) for r in np.asarray(got).reshape(-1, 4).tolist()] == ref
     det.close()
+
+
+def _raw_frame(seed, W, H):
+    small = make_image(seed, w=300, h=169)
+    ys = (np.arange(H) * 169) // H
+    xs = (np.arange(W) * 300) // W
+    return np.ascontiguousarray(small[ys][:, xs])
+
+
+@pytest.mark.parametrize("W,H", [(640, 360), (600, 338), (300, 169)])  # general INTER_AREA, exact 2x, identity
+def test_detect_frames_resizes_on_device(W, H):
+    # find_objects on raw frames: imutils.resize(raw, width=300) (INTER_AREA) on the device, then detection
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    raws = np.stack([_raw_frame(s, W, H) for s in range(3)])
+    det = CascadeClassifier(cs)
+    got = det.detect_frames(raws, 300, 1.1, 3)
+    for i in range(len(raws)):
+        roi = oracle.resize_area_bgr(raws[i], 300) if W != 300 else raws[i]
+        assert roi.shape[:2] == (int(H * (300 / W)), 300)
+        assert [tuple(r) for r in got[i].tolist()] == haar.detect_multiscale(cs, roi, 1.1, 3), i
+    with pytest.raises(Exception):
+        det.detect_frames(raws[:, :, :200], 300)  # narrower than the ROI: INTER_AREA upscaling unsupported
+    det.close()
+
+
+def test_video_motion_find_objects(tmp_path):
+    # the drop-in loads haarcascade_<name>.xml from cascade_dir and runs find_objects every 15th frame
+    from types import SimpleNamespace
+
+    from find_motion_amd import motion, videoio
+    from find_motion_amd.cascade import to_xml
+
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    (tmp_path / "haarcascade_frontalface_default.xml").write_text(to_xml(cs))
+    vm = motion.VideoMotion(filename=str(tmp_path / "v"), capture=videoio.SyntheticCapture(640, 360, 4, 0),
+                            box_size=100, cascades=["frontalface_default", "fullbody"], cascade_dir=str(tmp_path),
+                            outdir=str(tmp_path))
+    assert list(vm.cascades) == ["Face 4"]  # fullbody has no file there: skipped with a warning
+    fr = SimpleNamespace(raw=_raw_frame(0, 640, 360))
+    for _ in range(14):
+        assert vm.find_objects(fr) == set()
+    seen = vm.find_objects(fr)
+    roi = oracle.resize_area_bgr(fr.raw, 300)
+    ref = haar.detect_multiscale(cs, roi, 1.1, 5)
+    assert seen == ({"Face 4"} if ref else set())
+    assert vm.last_objects.get("Face 4", []) == [((x, y), (x + w, y + h)) for x, y, w, h in ref]
