@@ -86,25 +86,41 @@ __global__ void k_hresize(const uint8_t* __restrict__ gray, uint8_t* __restrict_
     rimg[(size_t)img * g.P + r] = (uint8_t)min(v, 255u);
 }
 
-// integral rows: S[y+1][x+1] = sum_{x'<=x} I(x', y) (row prefix; columns follow)
-__global__ void k_hrows(const uint8_t* __restrict__ rimg, uint32_t* __restrict__ S, uint32_t* __restrict__ Q, Geo g,
-                        int nimg, int maxh) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+// integral rows: S[y+1][x+1] = sum_{x'<=x} I(x', y) (row prefix; columns follow).
+// One wave per row: 64 columns at a time, inclusive wave scan by shuffles, carry in lane 63.
+__global__ __launch_bounds__(64) void k_hrows(const uint8_t* __restrict__ rimg, uint32_t* __restrict__ S,
+                                              uint32_t* __restrict__ Q, Geo g, int nimg, int maxh) {
+    const int row = blockIdx.x, lane = threadIdx.x;
     const int s = blockIdx.y, img = blockIdx.z;
     if (row >= g.sh[s]) return;
     const int sw = g.sw[s];
     const uint8_t* p = rimg + (size_t)img * g.P + g.poff[s] + (size_t)row * sw;
     uint32_t* ps = S + (size_t)img * g.I + g.ioff[s] + (size_t)(row + 1) * (sw + 1);
     uint32_t* pq = Q + (size_t)img * g.I + g.ioff[s] + (size_t)(row + 1) * (sw + 1);
-    uint32_t a = 0, b = 0;
-    ps[0] = 0;
-    pq[0] = 0;
-    for (int x = 0; x < sw; ++x) {
-        const uint32_t v = p[x];
-        a += v;
-        b += v * v;
-        ps[x + 1] = a;
-        pq[x + 1] = b;
+    if (lane == 0) {
+        ps[0] = 0;
+        pq[0] = 0;
+    }
+    uint32_t ca = 0, cb = 0;
+    for (int base = 0; base < sw; base += 64) {
+        const int x = base + lane;
+        const uint32_t v = x < sw ? p[x] : 0u;
+        uint32_t a = v, b = v * v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t ua = __shfl_up(a, d), ub = __shfl_up(b, d);
+            if (lane >= d) {
+                a += ua;
+                b += ub;
+            }
+        }
+        a += ca;
+        b += cb;
+        if (x < sw) {
+            ps[x + 1] = a;
+            pq[x + 1] = b;
+        }
+        ca = __shfl(a, 63);
+        cb = __shfl(b, 63);
     }
 }
 
@@ -148,6 +164,7 @@ __global__ void k_htilt(const uint32_t* __restrict__ S, uint32_t* __restrict__ T
 
 struct CascadeDev {
     int win_w, win_h, n_stages, has_tilted;
+    int stumps;                // every tree is one node (maxNodesPerTree == 1): scalar node/feature loads
     const int* stage_first;    // first tree of each stage
     const int* stage_ntrees;
     const float* stage_thr;
@@ -202,8 +219,24 @@ __global__ __launch_bounds__(256) void k_heval(const uint32_t* __restrict__ S, c
         if (area * (double)vnf < 1e-1) {
             out = 1;
             for (int si = 0; si < c.n_stages; ++si) {
-                const int t0 = c.stage_first[si], nt = c.stage_ntrees[si];
+                // stage, tree and node indices are the same in every lane: readfirstlane keeps them
+                // in SGPRs so the node and feature records come in by scalar loads
+                const int t0 = __builtin_amdgcn_readfirstlane(c.stage_first[si]);
+                const int nt = __builtin_amdgcn_readfirstlane(c.stage_ntrees[si]);
                 double sum = 0.;
+                if (c.stumps) {
+                    for (int t = t0; t < t0 + nt; ++t) {
+                        const Node n = c.nodes[t];  // stump t = node t, leaves 2t, 2t + 1
+                        const Feat& f = c.feats[__builtin_amdgcn_readfirstlane(n.feat)];
+                        const uint32_t* I = f.tilted ? Ti : Si;
+                        float v = __fmul_rn(f.w[0], (float)rsum(I, st, x, y, f.r[0], f.tilted));
+                        v = __fadd_rn(v, __fmul_rn(f.w[1], (float)rsum(I, st, x, y, f.r[1], f.tilted)));
+                        if (f.w[2] != 0.f) v = __fadd_rn(v, __fmul_rn(f.w[2], (float)rsum(I, st, x, y, f.r[2], f.tilted)));
+                        v = __fmul_rn(v, vnf);
+                        const int idx = v < n.thr ? n.left : n.right;
+                        sum += (double)c.leaves[2 * t - idx];
+                    }
+                } else
                 for (int t = t0; t < t0 + nt; ++t) {
                     const Node* nd = c.nodes + c.tree_node_ofs[t];
                     int idx = 0;
@@ -413,7 +446,9 @@ int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
     HH(h, hipMalloc(&h->d_blob, tot));
     HH(h, hipMemcpy(h->d_blob, blob.data(), tot, hipMemcpyHostToDevice));
     auto* b = (uint8_t*)h->d_blob;
-    h->cd = CascadeDev{d->win_w, d->win_h, d->n_stages, tilted,
+    int stumps = 1;
+    for (int t = 0; t < d->n_trees; ++t) stumps &= d->tree_nodes[t] == 1;
+    h->cd = CascadeDev{d->win_w, d->win_h, d->n_stages, tilted, stumps,
                        (const int*)(b + off[0]), (const int*)(b + off[1]), (const float*)(b + off[2]),
                        (const int*)(b + off[3]), (const int*)(b + off[4]), (const Node*)(b + off[5]),
                        (const float*)(b + off[6]), (const Feat*)(b + off[7])};
@@ -532,7 +567,7 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         maxh = std::max(maxh, g.sh[s]);
         maxw = std::max(maxw, g.sw[s]);
     }
-    k_hrows<<<dim3((maxh + 63) / 64, g.n, n), 64, 0, h->stream>>>(h->d_rimg, h->d_S, h->d_Q, g, n, maxh);
+    k_hrows<<<dim3(maxh, g.n, n), 64, 0, h->stream>>>(h->d_rimg, h->d_S, h->d_Q, g, n, maxh);
     k_hcols<<<dim3((maxw + 1 + 63) / 64, g.n, n), 64, 0, h->stream>>>(h->d_S, h->d_Q, g, n);
     if (h->has_tilted)
         k_htilt<<<dim3((unsigned)(((maxw + 1) * (maxh + 1) + 255) / 256), g.n, n), 256, 0, h->stream>>>(h->d_S, h->d_T,
