@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-end rehearsal: every GPU test, smoke(), the default bench line.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/final_parity.log 2>&1 || { tail -30 gpurun_out/final_parity.log; exit 1; }
+tail -1 gpurun_out/final_parity.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final_smoke.log 2>&1 || { tail -20 gpurun_out/final_smoke.log; exit 1; }
+tail -1 gpurun_out/final_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/final_bench.log 2>&1 || { tail -20 gpurun_out/final_bench.log; exit 1; }
+tail -1 gpurun_out/final_bench.log
