@@ -12,8 +12,10 @@
 //   k_htilt    tilted sum T(X,Y) = sum_{y<Y, |x-X+1| <= Y-y-1} I(x,y) (only for
 //              cascades with tilted features)
 //   k_heval    one thread per window of the ystep grid: HaarEvaluator::setWindow
-//              variance normalisation, then the stages (stumps or trees) with
-//              float32 feature sums without FMA and double leaf sums
+//              variance normalisation, then the first stages (stumps or trees)
+//              with float32 feature sums without FMA and double leaf sums;
+//              survivors are compacted into a list
+//   k_heval_tail  the remaining stages over the survivors (dense waves)
 // Host side: the x-skip of rows whose window was rejected by stage 0 and
 // groupRectangles (partition + class means + nested-rect filter), both
 // sequential by definition and tiny next to the window sweep.
@@ -26,6 +28,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -191,75 +194,110 @@ __device__ __forceinline__ int32_t rsum(const uint32_t* I, int st, int x, int y,
     return (int32_t)(p0 - p1 - p2 + p3);
 }
 
-// one thread per window; res: 1 accepted, 0 rejected by stage 0, -1 rejected later or flat
-__global__ __launch_bounds__(256) void k_heval(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
-                                               const uint32_t* __restrict__ T, int8_t* __restrict__ res,
-                                               CascadeDev c, Geo g, int nimg) {
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long long)nimg * g.NW) return;
+struct Win {  // one window: integral bases, stride, position, variance normaliser
+    const uint32_t *S, *T;
+    int st, x, y;
+    float vnf;
+};
+
+// window index -> Win; false for a flat window (HaarEvaluator::setWindow returns false)
+__device__ __forceinline__ bool set_window(const uint32_t* S, const uint32_t* Q, const uint32_t* T,
+                                           const CascadeDev& c, const Geo& g, long long i, Win& w) {
     const int img = (int)(i / g.NW), r = (int)(i - (long long)img * g.NW);
     const int s = find_scale(g.woff, g.n, r);
     const int q = r - g.woff[s], gy = q / g.gw[s], gx = q - gy * g.gw[s];
-    const int x = gx * g.step[s], y = gy * g.step[s];
-    const int st = g.sw[s] + 1;
+    w.x = gx * g.step[s];
+    w.y = gy * g.step[s];
+    w.st = g.sw[s] + 1;
     const size_t base = (size_t)img * g.I + g.ioff[s];
-    const uint32_t* Si = S + base;
-    const uint32_t* Qi = Q + base;
-    const uint32_t* Ti = c.has_tilted ? T + base : nullptr;
-
+    w.S = S + base;
+    w.T = c.has_tilted ? T + base : nullptr;
     const int nr[4] = {1, 1, c.win_w - 2, c.win_h - 2};
-    const int32_t valsum = rsum(Si, st, x, y, nr, false);
-    const uint32_t valsq = (uint32_t)rsum(Qi, st, x, y, nr, false);
+    const int32_t valsum = rsum(w.S, w.st, w.x, w.y, nr, false);
+    const uint32_t valsq = (uint32_t)rsum(Q + base, w.st, w.x, w.y, nr, false);
     const double area = (double)((c.win_w - 2) * (c.win_h - 2));
     double nf = area * (double)valsq - (double)valsum * (double)valsum;
-    int8_t out = -1;
-    if (nf > 0.) {
-        nf = sqrt(nf);
-        const float vnf = (float)(1. / nf);
-        if (area * (double)vnf < 1e-1) {
-            out = 1;
-            for (int si = 0; si < c.n_stages; ++si) {
-                // stage, tree and node indices are the same in every lane: readfirstlane keeps them
-                // in SGPRs so the node and feature records come in by scalar loads
-                const int t0 = __builtin_amdgcn_readfirstlane(c.stage_first[si]);
-                const int nt = __builtin_amdgcn_readfirstlane(c.stage_ntrees[si]);
-                double sum = 0.;
-                if (c.stumps) {
-                    for (int t = t0; t < t0 + nt; ++t) {
-                        const Node n = c.nodes[t];  // stump t = node t, leaves 2t, 2t + 1
-                        const Feat& f = c.feats[__builtin_amdgcn_readfirstlane(n.feat)];
-                        const uint32_t* I = f.tilted ? Ti : Si;
-                        float v = __fmul_rn(f.w[0], (float)rsum(I, st, x, y, f.r[0], f.tilted));
-                        v = __fadd_rn(v, __fmul_rn(f.w[1], (float)rsum(I, st, x, y, f.r[1], f.tilted)));
-                        if (f.w[2] != 0.f) v = __fadd_rn(v, __fmul_rn(f.w[2], (float)rsum(I, st, x, y, f.r[2], f.tilted)));
-                        v = __fmul_rn(v, vnf);
-                        const int idx = v < n.thr ? n.left : n.right;
-                        sum += (double)c.leaves[2 * t - idx];
-                    }
-                } else
-                for (int t = t0; t < t0 + nt; ++t) {
-                    const Node* nd = c.nodes + c.tree_node_ofs[t];
-                    int idx = 0;
-                    do {
-                        const Node n = nd[idx];
-                        const Feat& f = c.feats[n.feat];
-                        const uint32_t* I = f.tilted ? Ti : Si;
-                        float v = __fmul_rn(f.w[0], (float)rsum(I, st, x, y, f.r[0], f.tilted));
-                        v = __fadd_rn(v, __fmul_rn(f.w[1], (float)rsum(I, st, x, y, f.r[1], f.tilted)));
-                        if (f.w[2] != 0.f) v = __fadd_rn(v, __fmul_rn(f.w[2], (float)rsum(I, st, x, y, f.r[2], f.tilted)));
-                        v = __fmul_rn(v, vnf);
-                        idx = v < n.thr ? n.left : n.right;
-                    } while (idx > 0);
-                    sum += (double)c.leaves[c.tree_leaf_ofs[t] - idx];
-                }
-                if (sum < (double)c.stage_thr[si]) {
-                    out = si == 0 ? 0 : -1;
-                    break;
-                }
+    if (!(nf > 0.)) return false;
+    nf = sqrt(nf);
+    w.vnf = (float)(1. / nf);
+    return area * (double)w.vnf < 1e-1;
+}
+
+__device__ __forceinline__ float feature(const Feat& f, const Win& w) {
+    const uint32_t* I = f.tilted ? w.T : w.S;
+    float v = __fmul_rn(f.w[0], (float)rsum(I, w.st, w.x, w.y, f.r[0], f.tilted));
+    v = __fadd_rn(v, __fmul_rn(f.w[1], (float)rsum(I, w.st, w.x, w.y, f.r[1], f.tilted)));
+    if (f.w[2] != 0.f) v = __fadd_rn(v, __fmul_rn(f.w[2], (float)rsum(I, w.st, w.x, w.y, f.r[2], f.tilted)));
+    return __fmul_rn(v, w.vnf);
+}
+
+// stages [s0, s1): the first failing stage, or -1 if all pass
+__device__ __forceinline__ int run_stages(const CascadeDev& c, const Win& w, int s0, int s1) {
+    for (int si = s0; si < s1; ++si) {
+        // stage, tree and node indices are the same in every lane: readfirstlane keeps them
+        // in SGPRs so the node and feature records come in by scalar loads
+        const int t0 = __builtin_amdgcn_readfirstlane(c.stage_first[si]);
+        const int nt = __builtin_amdgcn_readfirstlane(c.stage_ntrees[si]);
+        double sum = 0.;
+        if (c.stumps) {
+            for (int t = t0; t < t0 + nt; ++t) {
+                const Node n = c.nodes[t];  // stump t = node t, leaves 2t, 2t + 1
+                const float v = feature(c.feats[__builtin_amdgcn_readfirstlane(n.feat)], w);
+                const int idx = v < n.thr ? n.left : n.right;
+                sum += (double)c.leaves[2 * t - idx];
             }
+        } else {
+            for (int t = t0; t < t0 + nt; ++t) {
+                const Node* nd = c.nodes + c.tree_node_ofs[t];
+                int idx = 0;
+                do {
+                    const Node n = nd[idx];
+                    idx = feature(c.feats[n.feat], w) < n.thr ? n.left : n.right;
+                } while (idx > 0);
+                sum += (double)c.leaves[c.tree_leaf_ofs[t] - idx];
+            }
+        }
+        if (sum < (double)c.stage_thr[si]) return si;
+    }
+    return -1;
+}
+
+// head: one thread per window of the ystep grid, stages [0, split); survivors are appended
+// to `live` so the later stages run dense waves.  res: 1 accepted, 0 rejected by stage 0,
+// -1 rejected later or flat (the tail overwrites survivors' entries)
+__global__ __launch_bounds__(256) void k_heval(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
+                                               const uint32_t* __restrict__ T, int8_t* __restrict__ res,
+                                               int* __restrict__ live, int* __restrict__ nlive, int split,
+                                               CascadeDev c, Geo g, int nimg) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)nimg * g.NW) return;
+    Win w;
+    int8_t out = -1;
+    if (set_window(S, Q, T, c, g, i, w)) {
+        const int f = run_stages(c, w, 0, split);
+        if (f >= 0) {
+            out = f == 0 ? 0 : -1;
+        } else if (split < c.n_stages) {
+            live[atomicAdd(nlive, 1)] = (int)i;
+        } else {
+            out = 1;
         }
     }
     res[i] = out;
+}
+
+// tail: survivors of the head, grid-stride over the list, stages [split, n_stages)
+__global__ __launch_bounds__(256) void k_heval_tail(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
+                                                    const uint32_t* __restrict__ T, int8_t* __restrict__ res,
+                                                    const int* __restrict__ live, const int* __restrict__ nlive,
+                                                    int split, CascadeDev c, Geo g, int nimg) {
+    const int n = *nlive;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const long long i = live[k];
+        Win w;
+        set_window(S, Q, T, c, g, i, w);  // a survivor's window is not flat
+        res[i] = run_stages(c, w, split, c.n_stages) >= 0 ? -1 : 1;
+    }
 }
 
 }  // namespace haar
@@ -279,6 +317,8 @@ struct fm_haar {
     uint8_t *d_src = nullptr, *d_gray = nullptr, *d_rimg = nullptr;
     uint32_t *d_S = nullptr, *d_Q = nullptr, *d_T = nullptr;
     int8_t* d_res = nullptr;
+    int *d_live = nullptr, *d_nlive = nullptr;
+    size_t cap_live = 0;
     int2* d_taps = nullptr;
     uint8_t *d_raw = nullptr, *d_roi = nullptr;  // fm_haar_detect_frames: source frames, ROI frames
     int32_t *d_axo = nullptr, *d_axc = nullptr, *d_ayo = nullptr, *d_ayc = nullptr;
@@ -459,7 +499,7 @@ void fm_haar_destroy(fm_haar* h) {
     if (!h) return;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_blob, (void*)h->d_src, (void*)h->d_gray, (void*)h->d_rimg, (void*)h->d_S,
-                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw,
+                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw, (void*)h->d_live, (void*)h->d_nlive,
                     (void*)h->d_roi, (void*)h->d_axo, (void*)h->d_axc, (void*)h->d_ayo, (void*)h->d_ayc,
                     (void*)h->d_axw, (void*)h->d_ayw})
         if (p) (void)hipFree(p);
@@ -573,8 +613,19 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         k_htilt<<<dim3((unsigned)(((maxw + 1) * (maxh + 1) + 255) / 256), g.n, n), 256, 0, h->stream>>>(h->d_S, h->d_T,
                                                                                                     g, n);
     const long long nw = (long long)n * g.NW;
-    if (nw > 0)
-        k_heval<<<(unsigned)((nw + 255) / 256), 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->cd, g, n);
+    if (nw > 0) {
+        // stages evaluated for every window before survivors are compacted (FM_HAAR_SPLIT, default 4)
+        static const int split_env = std::getenv("FM_HAAR_SPLIT") ? std::atoi(std::getenv("FM_HAAR_SPLIT")) : 4;
+        const int split = std::max(1, std::min(split_env, h->n_stages));
+        if ((rc = grow(h, &h->d_live, h->cap_live, (size_t)nw))) return rc;
+        if (!h->d_nlive) HH(h, hipMalloc((void**)&h->d_nlive, sizeof(int)));
+        HH(h, hipMemsetAsync(h->d_nlive, 0, sizeof(int), h->stream));
+        k_heval<<<(unsigned)((nw + 255) / 256), 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live,
+                                                                     h->d_nlive, split, h->cd, g, n);
+        if (split < h->n_stages)
+            k_heval_tail<<<2048, 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live, h->d_nlive, split,
+                                                      h->cd, g, n);
+    }
     HH(h, hipGetLastError());
     HH(h, hipEventRecord(h->e1, h->stream));
     h->h_res.resize((size_t)nw);
