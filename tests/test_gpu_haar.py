@@ -4,6 +4,9 @@ the grouped detections must be identical (integer rects, same order).
 Cascades and images are synthetic (tests/haar_cases.py); the reference's
 cascade files are not on the GPU box.  Parity vs OpenCV itself: unpinned.
 """
+import glob
+import os
+
 import numpy as np
 import pytest
 
@@ -114,3 +117,17 @@ def test_video_motion_find_objects(tmp_path):
     ref = haar.detect_multiscale(cs, roi, 1.1, 5)
     assert seen == ({"Face 4"} if ref else set())
     assert vm.last_objects.get("Face 4", []) == [((x, y), (x + w, y + h)) for x, y, w, h in ref]
+
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "haar_*.npz")))
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_golden_fixtures_through_the_c_abi(path):
+    from find_motion_amd.cascade import parse
+    z = np.load(path)
+    det = CascadeClassifier(parse(str(z["xml"])))
+    got = det.detect_batch(z["image"][None], float(z["scale_factor"]), int(z["min_neighbors"]))[0]
+    assert np.array_equal(det.candidates(), z["candidates"])
+    assert np.array_equal(got, z["detections"])
+    det.close()

@@ -255,3 +255,20 @@ def test_group_rectangles_known_answers():
     assert sorted(haar.group_rectangles([(50, 50, 100, 100)] * 6 + small, 5)) == [(50, 50, 100, 100), (70, 70, 30, 30)]
     # minNeighbors 0: the candidates unchanged
     assert haar.group_rectangles(cl, 0) == cl
+
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "haar_*.npz")))
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_oracle_matches_golden_fixtures(path):
+    z = np.load(path)  # allow_pickle=False (default): plain arrays and the XML text
+    cs = parse(str(z["xml"]))
+    cand = haar.detect_candidates(cs, z["image"], float(z["scale_factor"]))
+    assert np.array_equal(np.asarray(cand, np.int32).reshape(-1, 4), z["candidates"])
+    det = haar.group_rectangles(cand, int(z["min_neighbors"]))
+    assert np.array_equal(np.asarray(det, np.int32).reshape(-1, 4), z["detections"])
+
+
+def test_golden_fixtures_present():
+    assert len(GOLDEN) == 3

@@ -111,12 +111,17 @@ def main():
     ap.add_argument("--frames", type=int, default=64, help="raw 1080p frames per call (ROI frames of many streams)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=1)
+    ap.add_argument("--cascade", default=None, help="a real haarcascade_*.xml instead of the synthetic one")
     args = ap.parse_args()
     from find_motion_amd import CascadeClassifier
     from haar_cases import make_image
 
     from haar_cases import make_image as _mi
-    cs = calibrate(face_shaped_cascade(), _mi(1000, 300, 168))
+    if args.cascade:
+        from find_motion_amd.cascade import parse
+        cs = parse(args.cascade)
+    else:
+        cs = calibrate(face_shaped_cascade(), _mi(1000, 300, 168))
     W, H = 1920, 1080
     frames = np.empty((args.frames, H, W, 3), np.uint8)
     ys = (np.arange(H) * 169) // H
@@ -138,7 +143,7 @@ def main():
     n = args.frames * args.iters
     # windows per ROI frame and stage-0 pass rate, from the restatement's geometry
     from oracle import haar
-    geo = haar.scale_geometry(300, 168, 24, 24, haar.scale_list(300, 168, 24, 24, 1.1))
+    geo = haar.scale_geometry(300, 168, cs.win_w, cs.win_h, haar.scale_list(300, 168, cs.win_w, cs.win_h, 1.1))
     nwin = sum(((g["ww"] + g["ystep"] - 1) // g["ystep"]) * ((g["ylim"] + g["ystep"] - 1) // g["ystep"])
                for g in geo)
     res = {"metric": "ROI frames/s through find_objects (1080p raw -> 300 px ROI -> detectMultiScale 1.1/5)",
@@ -146,7 +151,8 @@ def main():
            "device_ms_per_call": round(float(np.mean(gpu_ms)), 3),
            "device_frames_per_s": round(args.frames / (np.mean(gpu_ms) / 1e3), 1),
            "windows_per_frame": nwin, "detections_frame0": int(len(out[0])),
-           "cascade": f"synthetic, frontalface_default shape (24x24, {cs.n_stages} stages, {len(cs.tree_nodes)} stumps)",
+           "cascade": (args.cascade if args.cascade else "synthetic, frontalface_default shape") +
+                      f" ({cs.win_w}x{cs.win_h}, {cs.n_stages} stages, {len(cs.tree_nodes)} trees)",
            "note": "wall includes the H2D copy of the raw frames (PCIe); device_ms covers gray..eval kernels"}
     if args.cpu_frames > 0:
         import oracle as orc
