@@ -55,6 +55,8 @@ RED = (0, 0, 255)
 GREEN = (0, 255, 0)
 
 # fm.py:104-122
+_CASCADES: dict = {}  # (path, device) -> CascadeClassifier
+
 CASCADE_LOOKUP = {
     "frontalcatface": "Cat 1",
     "frontalcatface_extended": "Cat 2",
@@ -256,7 +258,10 @@ class VideoMotion:
             if path is None:
                 self.log.warning("cascade %s not found in %s: skipped", c, dirs)
                 continue
-            self.cascades[title] = CascadeClassifier(path, device=self.device)
+            key = (os.path.realpath(path), self.device)
+            if key not in _CASCADES:  # one device copy per file and device, shared by every stream
+                _CASCADES[key] = CascadeClassifier(path, device=self.device)
+            self.cascades[title] = _CASCADES[key]
 
     def _calc_min_area(self) -> None:
         """fm.py:402-406"""
