@@ -131,3 +131,30 @@ def test_golden_fixtures_through_the_c_abi(path):
     assert np.array_equal(det.candidates(), z["candidates"])
     assert np.array_equal(got, z["detections"])
     det.close()
+
+
+def test_device_resident_images():
+    # on_device = 1: images already in HBM (a decoder's buffer in production; hipMalloc here)
+    import ctypes as C
+
+    from find_motion_amd import _native
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    imgs = np.ascontiguousarray(np.stack([make_image(s) for s in range(3)]))
+    det = CascadeClassifier(cs)
+    hip = C.CDLL("libamdhip64.so")
+    ptr = C.c_void_p()
+    assert hip.hipMalloc(C.byref(ptr), C.c_size_t(imgs.nbytes)) == 0
+    try:
+        assert hip.hipMemcpy(ptr, C.c_void_p(imgs.ctypes.data), C.c_size_t(imgs.nbytes), 1) == 0  # H2D
+        n, H, W = imgs.shape[:3]
+        rects = np.zeros((n, 64, 4), np.int32)
+        counts = np.zeros(n, np.int32)
+        L = _native.load()
+        rc = L.fm_haar_detect(det._h, ptr.value, n, H, W, 3, 1, 1.1, 3, 0, 0, 0, 0, rects.ctypes.data, 64,
+                              counts.ctypes.data)
+        assert rc == 0, L.fm_haar_last_error(det._h)
+        for i in range(n):
+            assert [tuple(r) for r in rects[i, :counts[i]].tolist()] == haar.detect_multiscale(cs, imgs[i], 1.1, 3)
+    finally:
+        hip.hipFree(ptr)
+        det.close()
