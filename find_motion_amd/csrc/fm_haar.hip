@@ -622,8 +622,11 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         HH(h, hipMemsetAsync(h->d_nlive, 0, sizeof(int), h->stream));
         k_heval<<<(unsigned)((nw + 255) / 256), 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live,
                                                                      h->d_nlive, split, h->cd, g, n);
+        // a thread per possible survivor (grid-stride only past 16384 blocks): a smaller fixed grid
+        // (1024 blocks) left survivors queued behind each other, 4.3 vs 3.4 ms per 64 ROI frames
+        const unsigned tb = (unsigned)std::max<long long>(1, std::min<long long>((nw + 255) / 256, 16384));
         if (split < h->n_stages)
-            k_heval_tail<<<2048, 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live, h->d_nlive, split,
+            k_heval_tail<<<tb, 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live, h->d_nlive, split,
                                                       h->cd, g, n);
     }
     HH(h, hipGetLastError());
