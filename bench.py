@@ -175,16 +175,24 @@ def main() -> None:
     def submit(i: int) -> None:
         eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
 
+    ccl = {"heavy_tiles": 0, "shared_nodes_max": 0, "fallback_frames": 0, "batches": 0}
+
     def run(first: int, n: int) -> None:
         for i in range(min(depth, n)):
             submit(first + i)
         for i in range(n):
             eng.wait()  # completes batch i and frees its slot
+            st = eng.ccl_stats()  # two mapped-memory words: no device sync
+            ccl["heavy_tiles"] += st["heavy_tiles"]
+            ccl["shared_nodes_max"] = max(ccl["shared_nodes_max"], st["shared_nodes"])
+            ccl["fallback_frames"] += eng.fallbacks()
+            ccl["batches"] += 1
             if i + depth < n:
                 submit(first + i + depth)
 
     run(0, args.warmup)
     eng.reset_kernel_times()
+    ccl.update(heavy_tiles=0, shared_nodes_max=0, fallback_frames=0, batches=0)
 
     dist.barrier(active)
     torch.cuda.synchronize()
@@ -278,7 +286,10 @@ def main() -> None:
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kernels}
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+               "contour_pass": {"heavy_tiles_per_batch": round(ccl["heavy_tiles"] / max(ccl["batches"], 1), 2),
+                                "shared_nodes_max": ccl["shared_nodes_max"],
+                                "fallback_frames": ccl["fallback_frames"]}}
         print(json.dumps(out), flush=True)
     eng.close()
     dist.finalize(active)

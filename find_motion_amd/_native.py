@@ -26,7 +26,7 @@ EXPORTED = (
     "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
     "fm_kernel_times", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
-    "fm_host_alloc", "fm_host_free",
+    "fm_host_alloc", "fm_host_free", "fm_last_fallbacks", "fm_last_ccl_stats",
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
 )
@@ -101,6 +101,8 @@ def load() -> C.CDLL:
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
     L.fm_max_inflight.argtypes = [vp]
+    L.fm_last_fallbacks.argtypes = [vp]
+    L.fm_last_ccl_stats.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
     L.fm_haar_create.argtypes = [i32, C.POINTER(FMHaarDesc), C.POINTER(vp)]
     L.fm_haar_destroy.argtypes = [vp]
     L.fm_haar_destroy.restype = None
@@ -286,15 +288,33 @@ class MotionEngine:
         self.generation += 1
         self._init = [True] * self.n_streams
 
+    def fallbacks(self) -> int:
+        """Frames of the last waited batch relabelled by the pixel-level fallback (diagnostics)."""
+        return self._check(self._L.fm_last_fallbacks(self._h))
+
+    def ccl_stats(self) -> dict:
+        """Contour pass of the last waited batch: nodes taken from the shared pool, heavy tiles."""
+        a, b = C.c_int32(), C.c_int32()
+        self._check(self._L.fm_last_ccl_stats(self._h, C.byref(a), C.byref(b)))
+        return {"shared_nodes": a.value, "heavy_tiles": b.value}
+
     def counts(self) -> np.ndarray:
         out = np.zeros((self.last_batch, self.n_streams), np.int32)
         self._check(self._L.fm_get_counts(self._h, _ptr(out)))
         return out
 
     def contours(self, frame: int, stream: int) -> list:
-        buf = (FMContour * self.max_contours)()
-        n = self._check(self._L.fm_get_contours(self._h, frame, stream, C.cast(buf, C.c_void_p), self.max_contours))
-        return [Contour(c.x, c.y, c.w, c.h, (c.origin_x, c.origin_y)) for c in buf[: min(n, self.max_contours)]]
+        """Every external contour of (frame, stream), in raster order of their start pixels.
+
+        max_contours only sizes the first fetch: a frame with more contours is fetched
+        whole, so len() is always the true count find_movement needs (fm.py:674-694)."""
+        cap = self.max_contours
+        while True:
+            buf = (FMContour * cap)()
+            n = self._check(self._L.fm_get_contours(self._h, frame, stream, C.cast(buf, C.c_void_p), cap))
+            if n <= cap:
+                return [Contour(c.x, c.y, c.w, c.h, (c.origin_x, c.origin_y)) for c in buf[:n]]
+            cap = n
 
     def mask(self, frame: int, stream: int) -> np.ndarray:
         out = np.empty(self.work_shape, np.uint8)

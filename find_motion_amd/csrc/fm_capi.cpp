@@ -51,18 +51,22 @@ struct BatchSlot {
     int32_t* d_rlist = nullptr;     // [F][ntiles] empty-region representatives
     int32_t* d_regrep = nullptr;    // [F][ntiles] empty tile -> region representative
     int32_t* d_ncr = nullptr;       // [F][2]
-    int32_t* d_heavy = nullptr;
-    int32_t* d_count = nullptr;     // [2F+1]
+    int32_t* d_heavy = nullptr;     // [F * ntiles] heavy-tile list
+    uint8_t* d_hscratch = nullptr;  // [nheavy][kHeavyScratch] heavy-tile labelling scratch
+    int32_t* d_count = nullptr;     // [2F+2]
     int32_t* h_count = nullptr;     // pinned [F]
     int32_t* h_overflow = nullptr;  // pinned [F]
     int32_t* dh_count = nullptr;     // device aliases of the two (mapped): the fused path's k_counts writes them
     int32_t* dh_overflow = nullptr;
+    int32_t* h_stats = nullptr;     // mapped [2]: shared-pool nodes, heavy tiles (k_counts)
+    int32_t* dh_stats = nullptr;
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
     hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr;
     hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
+    FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
     uint64_t gen = 0;               // submits into this slot
 };
 
@@ -92,10 +96,14 @@ struct fm_ctx {
     int32_t* d_label = nullptr;   // pixel-level CCL (v1 path, fused-path overflow fallback)
     int32_t* d_cid = nullptr;
     uint8_t* d_outer = nullptr;
-    int32_t* d_rec_dev = nullptr;
+    int32_t* d_rec_dev = nullptr;  // pixel-level CCL records [rec_dev_cap][5]
+    size_t rec_dev_cap = 0;
+    int32_t* d_rec_all = nullptr;  // k_emit_all records of one frame [rec_all_cap][5] + counter
+    size_t rec_all_cap = 0;
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
-    int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;
+    int ntx = 0, nty = 0, ntiles = 0, nnodes = 0, nheavy = 0;  // nnodes, nheavy: per batch slot
+    int nquota = 0;                                             // nodes of each frame's quota
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
     float *d_xwt = nullptr, *d_ywt = nullptr;
 
@@ -107,6 +115,8 @@ struct fm_ctx {
     int ready_slot = -1;           // slot of the last waited batch
     uint64_t ready_gen = 0;
     int ready = 0;                 // frames of the last waited batch
+    int fallbacks = 0;             // its frames relabelled by the pixel-level CCL (node pool exhausted)
+    int32_t stats[2] = {0, 0};     // its contour pass: nodes from the shared pool, heavy tiles
     std::vector<int32_t> ready_counts;                    // [ready * S]
     std::vector<std::vector<fm_contour>> contours;        // per (t*S+s), sorted
 
@@ -246,6 +256,60 @@ int check_frame(fm_ctx* c, int frame, int stream, bool device_data) {
     if (device_data && (c->ready_slot < 0 || c->slots[c->ready_slot].gen != c->ready_gen))
         return fail(c, FM_ESTATE, "the batch's device results were overwritten by a later submit");
     return FM_OK;
+}
+
+// every record of frame f of a finished fused-path batch (count known from k_emit)
+int emit_all(fm_ctx* c, BatchSlot& B, size_t f, int count, std::vector<int32_t>& out) {
+    if ((size_t)count > c->rec_all_cap) {
+        dfree(c->d_rec_all);
+        c->rec_all_cap = 0;
+        if (int rc = dalloc(c, &c->d_rec_all, (size_t)count * 5 + 1)) return rc;
+        c->rec_all_cap = (size_t)count;
+    }
+    hipStream_t st = c->aux_stream;
+    int32_t* cnt = c->d_rec_all + (size_t)count * 5;
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+    HIP_TRY(c, launch_emit_all(st, B.fa, (int)f, c->d_rec_all, cnt, count));
+    out.resize((size_t)count * 5 + 1);
+    HIP_TRY(c, hipMemcpyAsync(out.data(), c->d_rec_all, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (out.back() != count) return fail(c, FM_EHIP, "re-emit of frame %zu found %d contours, not %d", f, out.back(), count);
+    out.pop_back();
+    return FM_OK;
+}
+
+// frame f of a fused-path batch through the pixel-level CCL (from its dilated bit rows):
+// all records into out, the count into count
+int relabel_frame(fm_ctx* c, BatchSlot& B, size_t f, std::vector<int32_t>& out, int& count) {
+    hipStream_t st = c->aux_stream;
+    int32_t* dcnt = B.d_count + f;  // this frame's contour counter (the batch is finished)
+    const uint8_t* mask = c->d_mask + f * c->work_plane;  // per-frame path: the batch's dilated masks
+    if (c->use_fused) {
+        HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, B.d_candf + f * c->ntiles, c->d_mask, c->h,
+                                      c->w, c->ntx));
+        mask = c->d_mask;
+    }
+    for (int pass = 0; pass < 2; pass++) {
+        HIP_TRY(c, hipMemsetAsync(dcnt, 0, sizeof(int32_t), st));
+        HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, st));
+        CclArgs ca{mask, c->d_label, c->d_outer, c->d_cid, dcnt, c->d_rec_dev, 1, c->h, c->w, (int)c->rec_dev_cap};
+        HIP_TRY(c, launch_ccl(st, ca, nullptr));
+        int32_t n = 0;
+        HIP_TRY(c, hipMemcpyAsync(&n, dcnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+        if ((size_t)n <= c->rec_dev_cap) {
+            count = n;
+            out.resize((size_t)n * 5);
+            HIP_TRY(c, hipMemcpyAsync(out.data(), c->d_rec_dev, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipStreamSynchronize(st));
+            return FM_OK;
+        }
+        dfree(c->d_rec_dev);
+        c->rec_dev_cap = 0;
+        if (int rc = dalloc(c, &c->d_rec_dev, (size_t)n * 5)) return rc;
+        c->rec_dev_cap = (size_t)n;
+    }
+    return fail(c, FM_EHIP, "pixel-level relabel of frame %zu did not converge", f);
 }
 
 }  // namespace
@@ -404,21 +468,31 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         c->ntx = (c->w + 63) / 64;
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
-        c->nnodes = c->ntiles * kTileMaxRuns;
+        // union-find nodes: one per empty-tile region slot, each frame's quota, and a shared
+        // overflow pool that holds at least one worst-case frame (frames past it take the
+        // pixel-level fallback)
+        const size_t tf = frames * (size_t)c->ntiles;
+        c->nquota = c->ntiles * kNodesPerTileFrame;
+        const size_t nn = tf + tf * kNodesPerTileFrame + std::max(tf * kNodesShared, (size_t)c->ntiles * kTileMaxRuns);
+        if (nn >= (size_t)INT32_MAX) return fail(nullptr, FM_ENOTSUP, "batch too large for 32-bit node ids (%zu)", nn);
+        c->nnodes = (int)nn;
+        c->nheavy = kHeavyWaves;
     }
     for (int i = 0; i < c->nslots; i++) {
         BatchSlot& b = c->slots[i];
         if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &b.d_work, px * 3))) return rc;
-        if ((rc = dalloc(cp, &b.d_count, 2 * frames + 1))) return rc;
+        if ((rc = dalloc(cp, &b.d_count, 3 * frames + 2))) return rc;
         if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
         if (c->use_fused) {
-            if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
+            if ((rc = dalloc(cp, &b.d_hscratch, (size_t)c->nheavy * kHeavyScratch)) ||
+                (rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) ||
+                (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_tflag, frames * c->ntiles * 8)) || (rc = dalloc(cp, &b.d_candf, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_clist, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_rlist, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_regrep, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_ncr, frames * 2)) ||
                 (rc = dalloc(cp, &b.d_dbits, frames * c->ntiles * 64)) ||
                 (c->use_pix && (rc = dalloc(cp, &b.d_bits, frames * c->ntiles * 64))) ||
-                (rc = dalloc(cp, &b.d_nodes, frames * (size_t)c->nnodes)))
+                (rc = dalloc(cp, &b.d_nodes, (size_t)c->nnodes)))
                 return rc;
         }
         // contour records: mapped pinned host memory written directly by the kernels
@@ -428,6 +502,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_count, b.h_count, 0));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, hipHostMalloc((void**)&b.h_stats, 2 * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_stats, b.h_stats, 0));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_overflow, b.h_overflow, 0));
         if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * 8 * sizeof(uint32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
@@ -443,6 +519,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         (rc = dalloc(cp, &c->d_outer, ccl_px)) ||
         (rc = dalloc(cp, &c->d_rec_dev, (c->use_fused ? 1 : frames) * (size_t)p.max_contours * 5)))
         return rc;
+    c->rec_dev_cap = (size_t)p.max_contours;
     HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
     HIP_TRY(cp, hipMemset(c->d_bg[0], 0, S * c->work_plane * sizeof(double)));
     HIP_TRY(cp, hipMemset(c->d_bg[1], 0, S * c->work_plane * sizeof(double)));
@@ -509,16 +586,16 @@ void fm_destroy(fm_ctx* c) {
         }
     for (auto& b : c->slots) {
         dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
-        dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
+        dfree(b.d_nodes); dfree(b.d_hscratch); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
         dfree(b.d_clist); dfree(b.d_rlist); dfree(b.d_regrep); dfree(b.d_ncr);
-        for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init})
+        for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init, (void*)b.h_stats})
             if (hp) (void)hipHostFree(hp);
         if (b.ev_pix) (void)hipEventDestroy(b.ev_pix);
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
-    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev);
+    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_all);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamDestroy(st);
@@ -654,7 +731,9 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.ncr = B.d_ncr;
         fa.nodes = B.d_nodes;
         fa.count = B.d_count;
+        fa.hscratch = B.d_hscratch;
         fa.heavy = B.d_heavy;
+        fa.nheavy = c->nheavy;
         fa.rec = B.d_rec;
         fa.h_count = B.dh_count;
         fa.h_overflow = B.dh_overflow;
@@ -668,6 +747,8 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.nty = c->nty;
         fa.ntiles = c->ntiles;
         fa.nnodes = c->nnodes;
+        fa.nquota = c->nquota;
+        fa.h_stats = B.dh_stats;
         fa.cap = c->p.max_contours;
         fa.cvt_simd = npx >= 16;
         fa.alpha = c->p.avg;
@@ -712,6 +793,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
         HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
         HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer));  // counts land in mapped h_count / h_overflow
+        B.fa = fa;
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));
     } else {
         PixelArgs a{};
@@ -775,28 +857,29 @@ int fm_wait(fm_ctx* c) {
     }
     const int n = B.n, S = c->p.n_streams, cap = c->p.max_contours;
     const size_t F = (size_t)n * S;
-    {
-        // Fused path: a tile with more runs than kTileMaxRuns cannot come from a
-        // dilated mask (<= 24 runs per 64-px row), but if it ever happens the
-        // frame is relabelled on the GPU by the pixel-level CCL.
-        bool redo = false;
-        for (size_t f = 0; f < F; f++) {
-            if (!B.h_overflow[f]) continue;
-            redo = true;
-            hipStream_t st = c->aux_stream;
-            HIP_TRY(c, hipMemsetAsync(B.d_count + f, 0, sizeof(int32_t), st));
-            HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, st));
-            HIP_TRY(c, launch_expand_bits(st, B.d_dbits + f * c->ntiles * 64, B.d_candf + f * c->ntiles, c->d_mask, c->h, c->w,
-                                          c->ntx));
-            CclArgs ca{c->d_mask, c->d_label, c->d_outer, c->d_cid, B.d_count + f,
-                       c->d_rec_dev, 1, c->h, c->w, c->p.max_contours};
-            HIP_TRY(c, launch_ccl(st, ca, nullptr));
-            HIP_TRY(c, hipMemcpyAsync(B.h_rec + f * cap * 5, c->d_rec_dev, cap * 5 * sizeof(int32_t),
-                                      hipMemcpyDeviceToHost, st));
-            HIP_TRY(c, hipMemcpyAsync(B.h_count + f, B.d_count + f, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-            HIP_TRY(c, hipStreamSynchronize(st));
+    // Frames whose records do not fit the cap are fetched whole, so len(frame.contours)
+    // and the records kept never depend on max_contours (fm.py:674-694 counts them all).
+    std::vector<std::pair<size_t, std::vector<int32_t>>> whole;
+    c->fallbacks = 0;
+    if (c->use_fused) {
+        c->stats[0] = B.h_stats[0];
+        c->stats[1] = B.h_stats[1];
+    }
+    for (size_t f = 0; f < F; f++) {
+        const bool ovf = c->use_fused && B.h_overflow[f];
+        if (!ovf && B.h_count[f] <= cap) continue;
+        std::vector<int32_t> v;
+        if (c->use_fused && !ovf) {
+            if (int rc = emit_all(c, B, f, B.h_count[f], v)) return rc;
+        } else {
+            // the contour pass ran out of nodes for this frame (fused path), or the per-frame
+            // path kept only cap records: relabel it with the pixel-level CCL, every record
+            int cnt = 0;
+            if (int rc = relabel_frame(c, B, f, v, cnt)) return rc;
+            B.h_count[f] = cnt;
+            c->fallbacks += ovf;
         }
-        (void)redo;
+        whole.emplace_back(f, std::move(v));
     }
     c->timer.collect();
     if (c->d_ts) {  // profiling: mean cycles between consecutive stamps of each labelled tile
@@ -816,12 +899,18 @@ int fm_wait(fm_ctx* c) {
     }
     c->ready_counts.assign(B.h_count, B.h_count + F);
     c->contours.assign(F, {});
+    size_t wi = 0;
     for (size_t f = 0; f < F; f++) {
-        const int cnt = std::min(B.h_count[f], cap);
+        const int32_t* r = B.h_rec + f * cap * 5;
+        int cnt = std::min(B.h_count[f], cap);
+        if (wi < whole.size() && whole[wi].first == f) {
+            r = whole[wi].second.data();
+            cnt = (int)(whole[wi].second.size() / 5);
+            wi++;
+        }
         auto& v = c->contours[f];
         v.resize(cnt);
         std::vector<std::pair<int32_t, int>> order(cnt);
-        const int32_t* r = B.h_rec + f * cap * 5;
         for (int i = 0; i < cnt; i++) order[i] = {r[i * 5], i};
         std::sort(order.begin(), order.end());
         for (int i = 0; i < cnt; i++) {
@@ -840,6 +929,15 @@ int fm_wait(fm_ctx* c) {
     c->ready_slot = si;
     c->ready_gen = B.gen;
     B.n = 0;
+    return FM_OK;
+}
+
+int fm_last_fallbacks(const fm_ctx* c) { return c ? c->fallbacks : fail(nullptr, FM_EINVAL, "null context"); }
+
+int fm_last_ccl_stats(const fm_ctx* c, int32_t* shared_nodes, int32_t* heavy_tiles) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (shared_nodes) *shared_nodes = c->stats[0];
+    if (heavy_tiles) *heavy_tiles = c->stats[1];
     return FM_OK;
 }
 

@@ -10,16 +10,19 @@
 // Work is proportional to motion.  A tile is a CANDIDATE when its dilated mask
 // can be non-empty: it has threshold bits, or a neighbour has them within 2 px
 // of the shared edge/corner (per-tile flags written by the pixel kernel).
-// Every other tile is empty background.  Global union-find nodes are
-// (tile, component ordinal), id = tile * kTileMaxRuns + ordinal, per frame.
+// Every other tile is empty background.  Union-find nodes of a batch slot:
+// node f*ntiles + r for the empty-tile region represented by tile r of frame f,
+// then a pool from which each labelled candidate tile takes one node per
+// component (TileRec::nbase + ordinal) -- memory follows the motion present, not
+// the worst case.
 //   k_regions    one workgroup per frame: candidate list; empty tiles grouped
 //                into 4-connected regions in LDS, one node per region (at its
 //                representative tile), "outer" when the region reaches the grid border.
 //   k_tile_ccl   one wave per candidate: 5x5 dilation of its bit rows
-//                (fm.py:266), run-length labelling in LDS, a tile record (edge
-//                labels) and one node per component.
-//   k_tile_heavy tiles with more runs than the light pass holds (never for real
-//                dilated masks: <= 24 runs per 64-px row; kept for safety).
+//                (fm.py:266), run-length labelling in LDS (256 runs), a tile
+//                record (edge labels) and one node per component.
+//   k_tile_heavy tiles with more runs (a dense texture of blobs): persistent waves,
+//                global-memory scratch of kTileMaxRuns runs each, no LDS.
 //   k_merge      one wave per candidate: unions along its edges with candidate
 //                neighbours (right / below) and empty regions (all sides).
 //   k_fold       one wave per candidate tile (lanes = its components) or region:
@@ -28,8 +31,8 @@
 //   k_emit       one wave per candidate tile: the external test at each
 //                foreground root and the contour records (mapped host memory).
 //   k_counts     per frame: counts / overflow flags into mapped host memory.
-// A frame with a tile beyond even the heavy pass is flagged (count[F+f]); the
-// host relabels it with the pixel-level CCL of fm_kernels.hip.
+// A frame whose tiles exhaust the scratch slots or the node pool is flagged
+// (count[F+f]); the host relabels it with the pixel-level CCL of fm_kernels.hip.
 #include "fm_internal.h"
 
 namespace fm {
@@ -227,9 +230,52 @@ __device__ __forceinline__ int run_at(int base, uint64_t starts, int p) {
         if (a.dbg_ts && ln == 0) a.dbg_ts[((size_t)f * a.ntiles + ti) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// returns false (nothing written) if the tile has more than CAP runs
-template <int CAP>
-__device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc) {
+// Scratch access: all in LDS for the light pass; for a heavy tile the union-find parents
+// and the run pairs (hit every hook/shortcut round) stay in LDS, the per-run arrays live
+// in global memory (G: agent-scope loads of everything updated by atomics, so no load
+// can see a stale L1 line; plain stores are made visible to the other lanes by waiting
+// on vmcnt)
+template <bool G>
+__device__ __forceinline__ int sld(int* p) {
+    if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool G>
+__device__ __forceinline__ int srd(const int* p) {
+    if constexpr (G) return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool G>
+__device__ __forceinline__ void sfence() {
+    if constexpr (G) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+enum : int { TCCL_OK = 0, TCCL_RUNS = 1, TCCL_NODES = 2 };
+
+// the tile's node ids: n consecutive ids from its frame's quota (one counter per frame, so
+// the tiles of different frames never contend on one atomic), or past the quota from the
+// slot's shared overflow pool; -1 (TCCL_NODES) when that is exhausted too: the frame is
+// relabelled by the pixel-level fallback
+__device__ __forceinline__ int take_nodes(const FusedArgs& a, size_t f, int n, int ln) {
+    const size_t F = (size_t)a.T * a.S;
+    const long long q0 = (long long)F * a.ntiles, sh0 = q0 + (long long)F * a.nquota;
+    long long first = -1;
+    if (ln == 0) {
+        const int b = atomicAdd(&a.count[2 * F + 2 + f], n);
+        if (b + n <= a.nquota) {
+            first = q0 + (long long)f * a.nquota + b;
+        } else {
+            const int c = atomicAdd(&a.count[2 * F], n);
+            if (sh0 + c + n <= (long long)a.nnodes) first = sh0 + c;
+        }
+    }
+    return __shfl((int)first, 0, 64);
+}
+
+// TCCL_RUNS (nothing written) if the tile has more than CAP runs
+template <int CAP, bool G>
+__device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc) {
     int* par = sc.par;
     int* amin = sc.amin;
     int* amax = sc.amax;
@@ -242,24 +288,26 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
     const int h = a.h, w = a.w;
     const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
     TileRec* TR = a.tiles + f * a.ntiles + ti;
-    NodeRec* NR = a.nodes + f * (size_t)a.nnodes + (size_t)ti * MAXR;
 
     if (__ballot(m != 0) == 0) {  // empty tile: one background component
+        const int nb = take_nodes(a, f, 1, ln);
+        if (nb < 0) return TCCL_NODES;
         TR->edges[ln] = 0;
         TR->edges[64 + ln] = 0;
         TR->edges[128 + ln] = 0;
         TR->edges[192 + ln] = 0;
         if (ln == 0) {
             TR->nroots = 1;
+            TR->nbase = nb;
             const bool outer = x0 == 0 || y0 == 0 || x0 + TS - 1 >= w - 1 || y0 + TS - 1 >= h - 1;
             NodeRec nrec;
             nrec.key = 0;
-            nrec.parent = ti * MAXR;
+            nrec.parent = nb;
             nrec.flags = outer ? 2u : 0u;
             nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
-            NR[0] = nrec;
+            a.nodes[nb] = nrec;
         }
-        return true;
+        return TCCL_OK;
     }
 
     const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
@@ -272,7 +320,7 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
     }
     const int total = __shfl(incl, 63, 64);
     const int base = incl - nr;
-    if (total > CAP) return false;
+    if (total > CAP) return TCCL_RUNS;
     FM_STAMP(3);
     rb[ln] = base;
     if (ln == 63) rb[64] = total;
@@ -324,7 +372,7 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
         if (ln >= o) pin += v;
     }
     const int np = __shfl(pin, 63, 64);
-    if (np > 2 * CAP) return false;
+    if (np > 2 * CAP) return TCCL_RUNS;
     const int pbase = pin - npl;
     if (ln < 63) {  // write pass
         uint64_t sb = s2;
@@ -346,7 +394,7 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
             id2++;
         }
     }
-    lds_fence();
+    sfence<G>();
     FM_STAMP(5);
     // Shiloach-Vishkin style rounds: hook the larger of the two parents under the
     // smaller (atomicMin, so parents only decrease), then shortcut par[i] = par[par[i]];
@@ -362,7 +410,7 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
                 ch = true;
             }
         }
-        lds_fence();
+        sfence<G>();
         for (int i = ln; i < total; i += 64) {
             const int pi = lload(&par[i]);
             const int ppi = lload(&par[pi]);
@@ -371,12 +419,12 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
                 ch = true;
             }
         }
-        lds_fence();
+        sfence<G>();
         if (__ballot(ch) == 0) break;
     }
     FM_STAMP(6);
     for (int i = base; i < base + nr; i++) {  // fold into roots (par[] is flat now)
-        const int rt = par[i];
+        const int rt = (par[i]);
         if (rt != i) {
             if (rf[i] & 1) {
                 atomicMin(&amin[rt], (int)rx0[i]);
@@ -387,29 +435,37 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
             }
         }
     }
-    lds_fence();
+    sfence<G>();
     FM_STAMP(7);
     // ordinals of the roots in raster order
     int myr = 0;
-    for (int i = base; i < base + nr; i++) myr += (par[i] == i);
+    for (int i = base; i < base + nr; i++) myr += ((par[i]) == i);
     int rin = myr;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const int v = __shfl_up(rin, o, 64);
         if (ln >= o) rin += v;
     }
-    if (ln == 63) TR->nroots = rin;
+    const int nroots = __shfl(rin, 63, 64);
+    const int nb = take_nodes(a, f, nroots, ln);
+    if (nb < 0) return TCCL_NODES;
+    if (ln == 63) {
+        TR->nroots = nroots;
+        TR->nbase = nb;
+    }
     {
         int kk = rin - myr;
         for (int i = base; i < base + nr; i++)
-            if (par[i] == i) ord[i] = (uint16_t)kk++;
+            if ((par[i]) == i) ord[i] = (uint16_t)kk++;
     }
-    lds_fence();
+    sfence<G>();
+    NodeRec* NR = a.nodes + nb;
     for (int i = base; i < base + nr; i++) {
-        if (par[i] != i) continue;
+        const int pi = (par[i]);
+        if (pi != i) continue;
         const int fg = rf[i] & 1;
         NodeRec nrec;
-        nrec.parent = ti * MAXR + ord[i];
+        nrec.parent = nb + ord[i];
         nrec.key = 0;
         nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
         if (fg) {
@@ -417,14 +473,14 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
             uint32_t ref;
             if (x0 + xs == 0) ref = REF_OUTER;
             else if (xs == 0) ref = REF_EDGE | (uint32_t)ln;
-            else ref = (uint32_t)ord[par[i - 1]];  // the background run left of this run
+            else ref = (uint32_t)ord[(par[i - 1])];  // the background run left of this run
             nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
             nrec.flags = 1u;
-            nrec.minx = x0 + amin[i];
-            nrec.maxx = x0 + amax[i];
-            nrec.maxy = y0 + ay[i];
+            nrec.minx = x0 + srd<G>(&amin[i]);
+            nrec.maxx = x0 + srd<G>(&amax[i]);
+            nrec.maxy = y0 + srd<G>(&ay[i]);
         } else {
-            nrec.flags = amin[i] ? 2u : 0u;
+            nrec.flags = srd<G>(&amin[i]) ? 2u : 0u;
         }
         NR[ord[i]] = nrec;
     }
@@ -433,12 +489,12 @@ __device__ bool tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t 
     const uint64_t m0 = __shfl(m, 0, 64), m63 = __shfl(m, 63, 64);
     const int id0 = rb[0] + __popcll(s0 & mask_c) - 1;
     const int id63 = rb[63] + __popcll(s63 & mask_c) - 1;
-    TR->edges[ln] = (uint16_t)(ord[par[base]] | ((rf[base] & 1) << 15));
-    TR->edges[64 + ln] = (uint16_t)(ord[par[base + nr - 1]] | ((rf[base + nr - 1] & 1) << 15));
-    TR->edges[128 + ln] = (uint16_t)(ord[par[id0]] | (((m0 >> ln) & 1) << 15));
-    TR->edges[192 + ln] = (uint16_t)(ord[par[id63]] | (((m63 >> ln) & 1) << 15));
+    TR->edges[ln] = (uint16_t)(ord[(par[base])] | ((rf[base] & 1) << 15));
+    TR->edges[64 + ln] = (uint16_t)(ord[(par[base + nr - 1])] | ((rf[base + nr - 1] & 1) << 15));
+    TR->edges[128 + ln] = (uint16_t)(ord[(par[id0])] | (((m0 >> ln) & 1) << 15));
+    TR->edges[192 + ln] = (uint16_t)(ord[(par[id63])] | (((m63 >> ln) & 1) << 15));
     FM_STAMP(8);
-    return true;
+    return TCCL_OK;
 }
 
 // candidate: the tile's dilated mask can be non-empty.  With threshold bits
@@ -484,7 +540,11 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
         // this batch's counters (the slot's previous batch was read back before reuse)
         a.count[f] = 0;
         a.count[(size_t)a.T * a.S + f] = 0;
-        if (f == 0) a.count[2 * (size_t)a.T * a.S] = 0;
+        a.count[2 * (size_t)a.T * a.S + 2 + f] = 0;
+        if (f == 0) {  // node pool and heavy scratch of the slot (read only by later kernels)
+            a.count[2 * (size_t)a.T * a.S] = 0;
+            a.count[2 * (size_t)a.T * a.S + 1] = 0;
+        }
     }
     __syncthreads();
     for (int t = tid; t < nt; t += RG) {
@@ -512,8 +572,8 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
         if (r < 0) continue;
         a.regrep[(size_t)f * nt + t] = r;
         if (t == r) {
-            NodeRec* rep = a.nodes + (size_t)f * a.nnodes + (size_t)r * MAXR;
-            rep->parent = r * MAXR;
+            NodeRec* rep = a.nodes + (size_t)f * nt + r;
+            rep->parent = (int)((size_t)f * nt + r);
             rep->flags = 0u;
             a.rlist[(size_t)f * nt + atomicAdd(&s_nr, 1)] = r;
         }
@@ -524,7 +584,7 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
         if (r < 0) continue;
         const int tx = t % ntx, ty = t / ntx;
         if (tx == 0 || ty == 0 || tx == ntx - 1 || ty == nty - 1)
-            atomicOr(&a.nodes[(size_t)f * a.nnodes + (size_t)r * MAXR].flags, 2u);
+            atomicOr(&a.nodes[(size_t)f * nt + r].flags, 2u);
     }
     __syncthreads();
     if (tid == 0) {
@@ -533,8 +593,27 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     }
 }
 
-// light pass: grid (GW, F); each wave labels candidates of the frame's list with a
-// stride; tiles with too many runs go to the heavy list
+// global part of heavy-tile slot i's scratch (kHeavyScratch bytes); par, pairs and rb are LDS
+__device__ __forceinline__ Scratch heavy_scratch(const FusedArgs& a, int i, int* par, uint32_t* pairs, int* rb) {
+    uint8_t* p = a.hscratch + (size_t)i * kHeavyScratch;
+    Scratch sc;
+    sc.par = par;
+    sc.pairs = pairs;
+    sc.rb = rb;
+    sc.amin = (int*)p;
+    sc.amax = sc.amin + MAXR;
+    sc.ay = sc.amax + MAXR;
+    sc.ord = (uint16_t*)(sc.ay + MAXR);
+    sc.rx0 = (uint8_t*)(sc.ord + MAXR);
+    sc.rx1 = sc.rx0 + MAXR;
+    sc.rf = sc.rx1 + MAXR;
+    return sc;
+}
+static_assert(4 * 3 * MAXR + 2 * MAXR + 3 * MAXR <= kHeavyScratch, "heavy scratch too small");
+
+// grid (GW, F); each wave labels candidates of the frame's list with a stride, in LDS
+// (LIGHT runs); a tile with more runs (a dense texture of small blobs) goes to the
+// heavy list
 template <bool DILATE>
 __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
     __shared__ int par[CW][LIGHT], amin[CW][LIGHT], amax[CW][LIGHT], ay[CW][LIGHT];
@@ -542,7 +621,6 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
     __shared__ uint16_t ord[CW][LIGHT];
     __shared__ uint32_t pairs[CW][2 * LIGHT];
     __shared__ int rb[CW][66];
-    __shared__ uint64_t hv[CW][68];
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
@@ -553,51 +631,54 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
         FM_STAMP(1);
         uint64_t m;
         if (DILATE && !(a.dbg_skip & 128)) {
-            m = dilate_tile(a, f, ti, ln, hv[wv]);
+            m = dilate_tile(a, f, ti, ln, nullptr);
             a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
         } else {
             m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
         }
         FM_STAMP(2);
         if (a.dbg_skip & 64) continue;  // profiling ablation (results invalid)
-        if (!tile_ccl<LIGHT>(a, f, ti, ln, m, sc) && ln == 0) {
-            const int slot = atomicAdd(&a.count[2 * F], 1);
-            a.heavy[slot] = (int)(f * a.ntiles + ti);
+        const int r = tile_ccl<LIGHT, false>(a, f, ti, ln, m, sc);
+        if (ln == 0) {
+            if (r == TCCL_RUNS) a.heavy[atomicAdd(&a.count[2 * F + 1], 1)] = (int)(f * a.ntiles + ti);
+            else if (r != TCCL_OK) a.count[F + f] = 1;
         }
     }
 }
 
-// heavy pass: persistent workgroups drain the work list with full-size LDS
+// heavy pass: NHW persistent waves drain the heavy list (kTileMaxRuns runs per tile), union-
+// find parents and run pairs in 19.5 KB of LDS (small enough to sit beside the pixel
+// kernel's workgroups), the other per-run arrays in a global scratch slot per wave
+constexpr int NHW = kHeavyWaves;
 __global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
-    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
-    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
-    __shared__ uint16_t ord[MAXR];
+    __shared__ int par[MAXR];
     __shared__ uint32_t pairs[2 * MAXR];
-    __shared__ int rb[66];
+    __shared__ int rb[68];
     const size_t F = (size_t)a.T * a.S;
-    const int n = a.count[2 * F];
-    const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
+    const int n = a.count[2 * F + 1];
+    const int ln = threadIdx.x;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         const size_t f = item / a.ntiles;
         const int ti = (int)(item - (long long)f * a.ntiles);
-        if (!tile_ccl<MAXR>(a, f, ti, threadIdx.x, a.dbits[(f * a.ntiles + ti) * 64 + threadIdx.x], sc) &&
-            threadIdx.x == 0)
-            a.count[F + f] = 1;
+        const int r = tile_ccl<MAXR, true>(a, f, ti, ln, a.dbits[(f * a.ntiles + ti) * 64 + ln],
+                                           heavy_scratch(a, blockIdx.x, par, pairs, rb));
+        if (r != TCCL_OK && ln == 0) a.count[F + f] = 1;
     }
 }
 
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
-__device__ __forceinline__ int enode(int tile, uint16_t e) { return tile * MAXR + (e & 0x7FFF); }
+// node of the component with edge label e of candidate tile `tile`
+__device__ __forceinline__ int enode(const TileRec* TR, int tile, uint16_t e) { return TR[tile].nbase + (e & 0x7FFF); }
 
 // Background component `nd` of a candidate touches empty region `rep`.  An outer
 // region only contributes its outer-ness, so the node is marked directly (no union:
 // every candidate around a moving object borders the big outer background, and
 // unions into that one root serialise on its atomics); an enclosed region is unioned.
-__device__ __forceinline__ void touch_region(NodeRec* N, int nd, int rep) {
-    if (N[rep * MAXR].flags & 2) atomicOr(&N[nd].flags, 2u);
-    else gunion(N, nd, rep * MAXR);
+__device__ __forceinline__ void touch_region(NodeRec* N, int nd, int rnode) {
+    if (N[rnode].flags & 2) atomicOr(&N[nd].flags, 2u);
+    else gunion(N, nd, rnode);
 }
 
 // one wave per candidate, lane = edge position
@@ -610,7 +691,8 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const uint8_t* cf = a.candf + f * nt;
     const int32_t* rr = a.regrep + f * nt;
     const TileRec* TR = a.tiles + f * nt;
-    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    NodeRec* N = a.nodes;
+    const int rb0 = (int)(f * nt);  // region node ids of this frame: rb0 + representative tile
     const int nc = a.ncr[2 * f];
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int t = a.clist[f * nt + k];
@@ -623,19 +705,19 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
             if (cf[t + 1]) {
                 const uint16_t B = TR[t + 1].edges[ln];
                 const int Bp = __shfl_up((int)B, 1, 64);
-                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(t, A), enode(t + 1, B));
+                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, t + 1, B));
                 if (efg(A)) {
                     if (ln > 0) {
                         const uint16_t Bu = TR[t + 1].edges[ln - 1];
-                        if (efg(Bu) && Bu != B) gunion(N, enode(t, A), enode(t + 1, Bu));
+                        if (efg(Bu) && Bu != B) gunion(N, enode(TR, t, A), enode(TR, t + 1, Bu));
                     }
                     if (ln < 63) {
                         const uint16_t Bd = TR[t + 1].edges[ln + 1];
-                        if (efg(Bd) && Bd != B) gunion(N, enode(t, A), enode(t + 1, Bd));
+                        if (efg(Bd) && Bd != B) gunion(N, enode(TR, t, A), enode(TR, t + 1, Bd));
                     }
                 }
             } else if (!efg(A) && !(ln > 0 && Ap == A)) {
-                touch_region(N, enode(t, A), rr[t + 1]);
+                touch_region(N, enode(TR, t, A), rb0 + rr[t + 1]);
             }
         }
         // bottom edge
@@ -646,40 +728,40 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
             if (cf[n]) {
                 const uint16_t B = TR[n].edges[128 + ln];
                 const int Bp = __shfl_up((int)B, 1, 64);
-                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(t, A), enode(n, B));
+                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, n, B));
                 if (efg(A)) {
                     if (ln > 0) {
                         const uint16_t Bl = TR[n].edges[128 + ln - 1];
-                        if (efg(Bl) && Bl != B) gunion(N, enode(t, A), enode(n, Bl));
+                        if (efg(Bl) && Bl != B) gunion(N, enode(TR, t, A), enode(TR, n, Bl));
                     }
                     if (ln < 63) {
                         const uint16_t Br = TR[n].edges[128 + ln + 1];
-                        if (efg(Br) && Br != B) gunion(N, enode(t, A), enode(n, Br));
+                        if (efg(Br) && Br != B) gunion(N, enode(TR, t, A), enode(TR, n, Br));
                     }
                 }
             } else if (!efg(A) && !(ln > 0 && Ap == A)) {
-                touch_region(N, enode(t, A), rr[n]);
+                touch_region(N, enode(TR, t, A), rb0 + rr[n]);
             }
             // corner diagonals (foreground only: both tiles candidates)
             if (ln == 0 && hasR && cf[n + 1]) {  // (63,63) <-> (0,0) of the down-right tile
                 const uint16_t P = TR[t].edges[192 + 63], Q = TR[n + 1].edges[128];
-                if (efg(P) && efg(Q)) gunion(N, enode(t, P), enode(n + 1, Q));
+                if (efg(P) && efg(Q)) gunion(N, enode(TR, t, P), enode(TR, n + 1, Q));
             }
             if (ln == 0 && tx > 0 && cf[n - 1]) {  // (0,63) <-> (63,0) of the down-left tile
                 const uint16_t P = TR[t].edges[192], Q = TR[n - 1].edges[128 + 63];
-                if (efg(P) && efg(Q)) gunion(N, enode(t, P), enode(n - 1, Q));
+                if (efg(P) && efg(Q)) gunion(N, enode(TR, t, P), enode(TR, n - 1, Q));
             }
         }
         // left / top edges against empty regions (candidate pairs are done by the neighbour)
         if (tx > 0 && !cf[t - 1]) {
             const uint16_t A = TR[t].edges[ln];
             const int Ap = __shfl_up((int)A, 1, 64);
-            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(t, A), rr[t - 1]);
+            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - 1]);
         }
         if (ty > 0 && !cf[t - ntx]) {
             const uint16_t A = TR[t].edges[128 + ln];
             const int Ap = __shfl_up((int)A, 1, 64);
-            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(t, A), rr[t - ntx]);
+            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - ntx]);
         }
     }
 }
@@ -699,10 +781,6 @@ __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
     }
 }
 
-// one workgroup per frame: (1) path compression with outer flags, bboxes and first
-// pixels folded into the roots, one thread per candidate tile (all its nodes) or
-// enclosed empty region; (2) after a workgroup barrier, the external test at every
-// foreground root and the contour records.
 // one wave per candidate tile (lanes = its components) or per empty-tile region: path
 // compression with outer flags, bboxes and raster-first pixels folded into the roots
 __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
@@ -710,37 +788,37 @@ __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     if (a.count[F + f]) return;  // relabelled by the host's pixel-level fallback
-    NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+    NodeRec* N = a.nodes;
     const TileRec* TRf = a.tiles + f * a.ntiles;
     const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
     for (int k = blockIdx.x * CW + wv; k < nc + nr; k += gridDim.x * CW) {
         if (k < nc) {
             const int t = a.clist[f * a.ntiles + k];
-            const int k1 = TRf[t].nroots;
-            for (int i = ln; i < k1; i += 64) fold_node(N, t * MAXR + i);
+            const int k1 = TRf[t].nroots, nb = TRf[t].nbase;
+            for (int i = ln; i < k1; i += 64) fold_node(N, nb + i);
         } else if (ln == 0) {
-            fold_node(N, a.rlist[f * a.ntiles + (k - nc)] * MAXR);
+            fold_node(N, (int)(f * a.ntiles) + a.rlist[f * a.ntiles + (k - nc)]);
         }
     }
 }
 
 // one wave per candidate tile, lanes = its components: the external test at every
-// foreground root and its contour record (after k_fold: every node points at its root)
-__global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const size_t f = blockIdx.y;
-    const size_t F = (size_t)a.T * a.S;
-    if (a.count[F + f]) return;
-    const NodeRec* N = a.nodes + f * (size_t)a.nnodes;
+// foreground root and its contour record (after k_fold: every node points at its root).
+// Records beyond cap are counted, not written (fm_wait re-emits such a frame whole with
+// k_emit_all, so len(frame.contours) and the records kept never depend on the cap).
+__device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wave, int nwaves, int ln, int32_t* recs,
+                                           int32_t* cnt, int cap) {
+    const NodeRec* N = a.nodes;
     const TileRec* TRf = a.tiles + f * a.ntiles;
     const uint8_t* cf = a.candf + f * a.ntiles;
     const int32_t* rr = a.regrep + f * a.ntiles;
+    const int rb0 = (int)(f * a.ntiles);
     const int nc = a.ncr[2 * f];
-    for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
+    for (int k = wave; k < nc; k += nwaves) {
         const int t = a.clist[f * a.ntiles + k];
-        const int k1 = TRf[t].nroots;
+        const int k1 = TRf[t].nroots, nbt = TRf[t].nbase;
         for (int i = ln; i < k1; i += 64) {
-            const int n = t * MAXR + i;
+            const int n = nbt + i;
             if (N[n].parent != n || !(N[n].flags & 1)) continue;
             const uint64_t key = N[n].key;
             const uint32_t first = (uint32_t)(key >> 32), ref = (uint32_t)key;
@@ -753,16 +831,16 @@ __global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
                 int bn;
                 if (ref & REF_EDGE) {
                     const int lt = tf - 1;
-                    bn = cf[lt] ? enode(lt, TRf[lt].edges[64 + (ref & 63)]) : rr[lt] * MAXR;
+                    bn = cf[lt] ? enode(TRf, lt, TRf[lt].edges[64 + (ref & 63)]) : rb0 + rr[lt];
                 } else {
-                    bn = tf * MAXR + (int)ref;
+                    bn = TRf[tf].nbase + (int)ref;
                 }
                 ext = (N[N[bn].parent].flags & 2) != 0;
             }
             if (!ext) continue;
-            const int id = atomicAdd(&a.count[f], 1);
-            if (id < a.cap) {
-                int32_t* rec = a.rec + (f * a.cap + id) * 5;
+            const int id = atomicAdd(cnt, 1);
+            if (id < cap) {
+                int32_t* rec = recs + (size_t)id * 5;
                 rec[0] = (int32_t)first;
                 rec[1] = N[n].minx;
                 rec[2] = fy;
@@ -771,6 +849,20 @@ __global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
             }
         }
     }
+}
+
+__global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.count[F + f]) return;
+    emit_frame(a, f, blockIdx.x * CW + wv, gridDim.x * CW, ln, a.rec + f * a.cap * 5, &a.count[f], a.cap);
+}
+
+// one frame of a finished batch, every record (cap = its known count)
+__global__ __launch_bounds__(64 * CW) void k_emit_all(FusedArgs a, int f, int32_t* recs, int32_t* cnt, int cap) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    emit_frame(a, (size_t)f, blockIdx.x * CW + wv, gridDim.x * CW, ln, recs, cnt, cap);
 }
 
 // one workgroup per frame: counts and overflow flags straight into mapped host memory
@@ -786,6 +878,10 @@ __global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
         const bool ovf = a.count[F + f] != 0;
         a.h_count[f] = ovf ? 0 : a.count[f];
         a.h_overflow[f] = ovf ? 1 : 0;
+        if (f == 0) {
+            a.h_stats[0] = a.count[2 * F];
+            a.h_stats[1] = a.count[2 * F + 1];
+        }
     }
 }
 
@@ -817,7 +913,7 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     tok = tm ? tm->begin("tile_ccl", st) : -1;
     if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), 0, st, a);
     else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), 0, st, a);
-    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(8), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), 0, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
@@ -827,6 +923,11 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     hipLaunchKernelGGL(cc::k_emit, gf, dim3(64 * cc::CW), 0, st, a);
     hipLaunchKernelGGL(cc::k_counts, dim3(F), dim3(cc::FT), 0, st, a);
     if (tm) tm->end(tok);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap) {
+    hipLaunchKernelGGL(cc::k_emit_all, dim3(cc::GW), dim3(64 * cc::CW), 0, st, a, f, rec, cnt, cap);
     return hipGetLastError();
 }
 

@@ -15,6 +15,11 @@ namespace fm {
 constexpr int kMaxK = 255;        // largest Gaussian size handled by the tiled kernel
 constexpr int kCclBlock = 32;     // CCL block edge (pixels)
 constexpr int kTileMaxRuns = 1600; // runs per 64x64 tile of a dilated mask (<= 24 per row => 1536)
+constexpr int kHeavyScratch = 27264; // bytes of global labelling scratch per heavy-pass wave (fm_ccl.hip)
+constexpr int kHeavyWaves = 64;       // k_tile_heavy persistent waves, one scratch slot each
+constexpr int kNodesPerTileFrame = 32; // union-find nodes each frame owns per tile (its quota)
+constexpr int kNodesShared = 16;       // + a shared overflow pool of this many per tile-frame (at least one
+                                       //   worst-case frame), taken from only by frames past their quota
 
 // Host-built INTER_AREA tables (computeResizeAreaTab restated in fm_capi.cpp).
 // Per destination index d: taps start at src index ofs[d], cnt[d] taps, weights
@@ -55,8 +60,11 @@ struct CclArgs {
     int F, h, w, cap;
 };
 
-// Temporally blocked fused kernel + tile-summary CCL (fm_fused.hip).
-// Global CCL node = (tile, local component): index tile * kTileMaxRuns + local.
+// Temporally blocked fused kernel + tile-summary CCL (fm_fused.hip, fm_ccl.hip).
+// Global CCL nodes of one batch slot: ids [0, F*ntiles) are the empty-tile regions
+// (node f*ntiles + representative tile); a labelled candidate tile takes nroots
+// consecutive ids (TileRec::nbase) from its frame's quota [F*ntiles + f*nquota, +nquota),
+// or past that from the slot's shared overflow pool (ids from F*ntiles + F*nquota).
 struct NodeRec {
     uint64_t key;     // foreground: (raster-first pixel << 32) | left-background reference
     int32_t parent;   // global union-find
@@ -64,7 +72,9 @@ struct NodeRec {
     int32_t minx, maxx, maxy, pad;
 };
 struct TileRec {
-    int32_t nroots, pad[3];           // components of the tile (ordinals 0..nroots-1, raster order)
+    int32_t nroots;                   // components of the tile (ordinals 0..nroots-1, raster order)
+    int32_t nbase;                    // node id of ordinal 0 (nodes of a candidate tile are consecutive)
+    int32_t pad[2];
     uint16_t edges[256];              // 0..63 left col, 64.. right col, 128.. top row, 192.. bottom row:
                                       // component ordinal | fg << 15
 };
@@ -96,15 +106,21 @@ struct FusedArgs {
     int32_t* rlist;              // [F][ntiles] representative tile of each empty-tile region
     int32_t* regrep;             // [F][ntiles] empty tile -> its region's representative tile
     int32_t* ncr;                // [F][2] candidates, regions
-    NodeRec* nodes;              // [F][nnodes]
-    int32_t* count;              // [2F+1]: [f] external contours, [F+f] overflow flag, [2F] heavy-tile count
+    NodeRec* nodes;              // [nnodes]: F*ntiles region nodes, then the pool of candidate-tile nodes
+    int32_t* count;              // [3F+2]: [f] external contours, [F+f] overflow flag, [2F] shared node-pool
+                                 // fill, [2F+1] heavy tiles listed, [2F+2+f] frame f's node-quota fill
+    int32_t* h_stats;            // mapped host [2]: nodes taken from the shared pool, heavy tiles (written by
+                                 // k_counts; diagnostics)
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
+    uint8_t* hscratch;           // [nheavy][kHeavyScratch] k_tile_heavy's labelling scratch
     int32_t* rec;                // [F][cap][5]
     int32_t* h_count;            // mapped host [F]: external contours per frame (written by k_fold_emit)
     int32_t* h_overflow;         // mapped host [F]: frame needs the pixel-level fallback
     int T, S, h, w, ksize, thresh;
     int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
+    int nquota;                  // nodes per frame quota
+    int nheavy;                  // heavy-tile scratch slots (= k_tile_heavy's waves)
     int tflag_waves;             // words per tile-frame in tflag: 1 (k_fused, atomicOr) or 8 (k_pix, one per wave)
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
@@ -137,6 +153,9 @@ int pix_lds_bytes(int ksize);
 bool pix_supported(int ksize);
 // CCL over tile summaries; dilate = true: a.bits are threshold rows to dilate into a.dbits
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer);
+// every external-contour record of frame f of a finished batch (all of them, unlike the
+// capped k_emit), into rec [cap][5]; *cnt must be 0 before
+hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap);
 // dilated bit rows of one frame -> mask bytes (VideoFrame.thresh) [h][w]; non-candidate tiles are 0
 hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, uint8_t* out, int h, int w,
                               int ntx);

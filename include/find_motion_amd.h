@@ -62,7 +62,8 @@ typedef struct fm_params {
     int threshold;    /* -t / threshold (fm.py:256, 1476) */
     double avg;       /* -a / avg, accumulateWeighted alpha (fm.py:659, 1479) */
     int max_batch;    /* max frames per stream per fm_submit */
-    int max_contours; /* capacity of the per-frame contour records */
+    int max_contours; /* per-frame contour records kept in mapped host memory (a frame
+                         with more is fetched whole at fm_wait: no contour is lost) */
     unsigned flags;   /* FM_FLAG_* */
 } fm_params;
 
@@ -123,8 +124,18 @@ int fm_wait(fm_ctx* ctx);
 int fm_get_counts(fm_ctx* ctx, int32_t* counts);
 
 /* Contours of one (frame, stream) of the last batch, in raster order of their
- * start pixels.  Returns the count (records written: min(count, cap)). */
+ * start pixels.  Returns the count (records written: min(count, cap)).  Every
+ * contour is kept whatever fm_params.max_contours is (a frame with more is
+ * fetched whole by fm_wait), so a second call with cap = count gets them all. */
 int fm_get_contours(fm_ctx* ctx, int frame, int stream, fm_contour* out, int cap);
+
+/* Diagnostics: frames of the last waited batch whose contours came from the
+ * pixel-level fallback (the batch exhausted its contour-pass node pool). */
+int fm_last_fallbacks(const fm_ctx* ctx);
+/* Diagnostics of the last waited batch's contour pass: union-find nodes its frames
+ * took from the shared pool (past their own quotas) and tiles labelled by the heavy
+ * pass (more than 256 runs: dense speckle). */
+int fm_last_ccl_stats(const fm_ctx* ctx, int32_t* shared_nodes, int32_t* heavy_tiles);
 
 /* Dilated threshold mask (VideoFrame.thresh after find_contours, fm.py:266), h*w bytes. */
 int fm_read_mask(fm_ctx* ctx, int frame, int stream, uint8_t* out);

@@ -520,3 +520,94 @@ int fmo_run_streams(const fmo_cfg* c, const uint8_t* frames, int S, int F, int n
     }
     return used;
 }
+
+/* ------------------------------------------------------------------------- */
+/* fmo_process_sequence: fmo_process_frame over F consecutive frames of one   */
+/* stream, scheduled in parallel where find_diff's data flow allows it, with  */
+/* the identical arithmetic per pixel (so it is checked against              */
+/* fmo_process_frame by tests/test_oracle_kat.py):                            */
+/*   blur_frame + mask (fm.py:487-494, 619-636): frames are independent;      */
+/*   diff / threshold / accumulateWeighted (fm.py:246-257, 651-659): a        */
+/*     recurrence over frames but independent per pixel (each pixel keeps     */
+/*     fmo_diff_thresh's SIMD rule and fmo_accumulate's frame-global vector-  */
+/*     body / scalar-tail split);                                            */
+/*   dilate + findContours (fm.py:260-276): frames are independent.           */
+/* masks: NULL or [F] pointers (NULL entries: mask not kept).                 */
+/* rec: [F][cap][7] as fmo_find_contours_ext, areas [F][cap] or NULL.         */
+/* Returns 0, or -1 when a frame's resize/blur is unsupported.                */
+int fmo_process_sequence(const fmo_cfg* c, const uint8_t* frames, int F, const uint8_t* keep,
+                         double* bg, int* bg_init, uint8_t* const* masks, int32_t* counts,
+                         int32_t* rec, double* areas, int cap, int nthreads)
+{
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const size_t n = (size_t)c->h * c->w, fb = (size_t)c->H * c->W * 3;
+    const int CH = 32;
+    const int simd = n >= 16;
+    const size_t vec_end = n - (n % 16);
+    const double a = c->alpha, b = 1.0 - c->alpha;
+    uint8_t* blur = (uint8_t*)malloc(n * CH);
+    uint8_t* th = (uint8_t*)malloc(n * CH);
+    int bad = 0;
+    for (int f0 = 0; f0 < F; f0 += CH) {
+        const int nf = F - f0 < CH ? F - f0 : CH;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : bad)
+#endif
+        for (int j = 0; j < nf; j++) {
+            uint8_t* small = (uint8_t*)malloc(n * 3);
+            uint8_t* gray = (uint8_t*)malloc(n);
+            uint8_t* bl = blur + (size_t)j * n;
+            int rc = fmo_resize_area_bgr(frames + (size_t)(f0 + j) * fb, c->H, c->W, small, c->h, c->w);
+            if (rc == 0) {
+                fmo_bgr2gray(small, n, gray);
+                rc = fmo_gauss_blur(gray, c->h, c->w, c->ksize, bl);
+            }
+            if (rc) bad |= 1;
+            if (keep)
+                for (size_t i = 0; i < n; i++) if (!keep[i]) bl[i] = 0;
+            free(small); free(gray);
+        }
+        if (bad) break;
+        const int init0 = *bg_init;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+        for (long blk = 0; blk < (long)((n + 4095) / 4096); blk++) {
+            const size_t i0 = (size_t)blk * 4096, i1 = i0 + 4096 < n ? i0 + 4096 : n;
+            for (size_t i = i0; i < i1; i++) {
+                double v = bg[i];
+                for (int j = 0; j < nf; j++) {
+                    const uint8_t s = blur[(size_t)j * n + i];
+                    if (!init0 && j == 0) v = (double)s;
+                    const int q = simd ? rne_f(fabsf((float)v)) : rne_d(fabs(v));
+                    const int d = abs((int)s - (int)sat_u8(q));
+                    th[(size_t)j * n + i] = (d > c->thresh) ? 255 : 0;
+                    if (i < vec_end) {
+                        v = fma(v, b, (double)s * a);
+                    } else {
+                        volatile double p1 = (double)s * a;
+                        volatile double p2 = v * b;
+                        v = p1 + p2;
+                    }
+                }
+                bg[i] = v;
+            }
+        }
+        *bg_init = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+        for (int j = 0; j < nf; j++) {
+            const int f = f0 + j;
+            uint8_t* m = (masks && masks[f]) ? masks[f] : (uint8_t*)malloc(n);
+            fmo_dilate5(th + (size_t)j * n, c->h, c->w, m);
+            counts[f] = fmo_find_contours_ext(m, c->h, c->w, rec + (size_t)f * cap * 7, areas ? areas + (size_t)f * cap : 0,
+                                              cap, 0, 0);
+            if (!(masks && masks[f])) free(m);
+        }
+    }
+    free(blur); free(th);
+    return bad ? -1 : 0;
+}

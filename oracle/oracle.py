@@ -50,6 +50,10 @@ def lib():
             C.c_void_p, u8p, C.c_void_p, f64p, C.POINTER(C.c_int),
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, i32p, f64p, C.c_int,
         ]
+        L.fmo_process_sequence.argtypes = [
+            C.c_void_p, u8p, C.c_int, C.c_void_p, f64p, C.POINTER(C.c_int), C.c_void_p,
+            i32p, i32p, C.c_void_p, C.c_int, C.c_int,
+        ]
         L.fmo_run_streams.argtypes = [C.c_void_p, u8p, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
         _lib = L
     return _lib
@@ -211,6 +215,50 @@ class OracleStream:
         origins = [(int(rec[i, 4]), int(rec[i, 5])) for i in range(min(n, cap))]
         return {"gray": gray, "blur": blur, "delta": delta, "mask": mask, "count": int(n),
                 "boxes": boxes, "origins": origins, "areas": areas[: min(n, cap)].copy()}
+
+
+class _SeqResult:
+    """Per-frame results of OracleStream.run: counts[F], boxes(f), origins(f), areas(f), masks{f: plane}."""
+
+    def __init__(self, counts, rec, areas, masks):
+        self.counts, self._rec, self._areas, self.masks = counts, rec, areas, masks
+
+    def boxes(self, f: int) -> list:
+        n = min(int(self.counts[f]), self._rec.shape[1])
+        return [tuple(int(v) for v in self._rec[f, i, :4]) for i in range(n)]
+
+    def origins(self, f: int) -> list:
+        n = min(int(self.counts[f]), self._rec.shape[1])
+        return [(int(self._rec[f, i, 4]), int(self._rec[f, i, 5])) for i in range(n)]
+
+    def areas(self, f: int) -> np.ndarray:
+        n = min(int(self.counts[f]), self._rec.shape[1])
+        return self._areas[f, :n].copy()
+
+
+def _run_sequence(self, frames: np.ndarray, cap: int = 4096, mask_frames=(), nthreads: int = 0) -> _SeqResult:
+    """step() over frames [F][H][W][3] (one stream, in order), frames in parallel where
+    find_diff's data flow allows it (fmo_process_sequence; identical arithmetic)."""
+    c = self.cfg
+    frames = np.ascontiguousarray(frames)
+    assert frames.ndim == 4 and frames.shape[1:] == (c.H, c.W, 3) and frames.dtype == np.uint8
+    F = frames.shape[0]
+    counts = np.zeros(F, np.int32)
+    rec = np.zeros((F, cap, 7), np.int32)
+    areas = np.zeros((F, cap), np.float64)
+    masks = {int(f): np.empty((c.h, c.w), np.uint8) for f in mask_frames}
+    ptrs = (C.c_void_p * F)(*[masks[f].ctypes.data if f in masks else None for f in range(F)])
+    rc = lib().fmo_process_sequence(
+        C.byref(self._c), frames, F, self.keep.ctypes.data if self.keep is not None else None,
+        self.bg, C.byref(self._init), ptrs, counts, rec, areas.ctypes.data, cap, int(nthreads))
+    if rc < 0:
+        raise RuntimeError("oracle sequence failed")
+    if int(counts.max(initial=0)) > cap:
+        raise RuntimeError("contour capacity exceeded")
+    return _SeqResult(counts, rec, areas, masks)
+
+
+OracleStream.run = _run_sequence
 
 
 def run_streams(cfg: OracleConfig, frames: np.ndarray, nthreads: int = 0, n_streams: int | None = None):

@@ -1,0 +1,177 @@
+"""GPU parity at the BASELINE configurations and on the product paths the small
+cases do not reach, against the CPU oracle (oracle.OracleStream.run: the same
+arithmetic as step(), frames scheduled in parallel where find_diff's data flow
+allows, so full-size sequences finish in seconds).
+
+* the bench workload itself: 1080p, mode F, T = 128 frames per launch from a
+  device-resident ring cycling 64 synthetic frames, the production
+  k_pix<5, false, false> (no planes kept), fm_max_inflight batches submitted
+  before the first wait, a ring wrap onto reused batch slots;
+* configs[2]: 8 x 1080p streams on one GPU, batches in flight;
+* configs[4] geometry: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the two
+  MASK_SCHEMA polygons (find_motion.py:86-100);
+* more contours than max_contours (a dot lattice: every contour counted and
+  kept, in raster order, fm.py:674-694), heavy tiles, and the pixel-level
+  fallback once a batch exhausts its node pool;
+* k = 97 (-B 1920 -b 20, fm.py:478-484: the per-frame k_pixel path) and k_fused
+  at k 11, 33, 49.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle
+from find_motion_amd import MotionEngine, make_gaussian, rasterize_masks
+from find_motion_amd.synthetic import batch
+
+pytestmark = pytest.mark.gpu
+
+CONFIG5_MASKS = [((0, 0), (639, 359)), ((3839, 2159), (3200, 2159), (3839, 1600))]
+
+
+def _check_frame(eng, res, t, s, f, tag, mask=True):
+    """Engine results (batch frame t, stream s) against oracle result res (sequence frame f)."""
+    got = eng.contours(t, s)
+    assert eng.counts()[t, s] == res.counts[f], f"count {tag}"
+    assert len(got) == res.counts[f], f"len(contours) {tag}"
+    assert [c.bbox for c in got] == res.boxes(f), f"boxes {tag}"
+    assert [c.origin for c in got] == res.origins(f), f"origins {tag}"
+    if mask and f in res.masks:
+        np.testing.assert_array_equal(eng.mask(t, s), res.masks[f], err_msg=f"mask {tag}")
+
+
+def test_bench_shape_inflight_ring_wrap():
+    """bench.py's exact workload through the production kernel, against the oracle on every frame."""
+    torch = pytest.importorskip("torch")
+    W, H, T, NB = 1920, 1080, 128, 6
+    uniq = batch(W, H, 1, 0, 64)                      # bench: 64 synthetic frames cycled through a 128 ring
+    ring_h = np.concatenate([uniq, uniq])              # [128][1][H][W][3]
+    ring = torch.from_numpy(ring_h).to("cuda:0")
+    torch.cuda.synchronize()
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    assert not eng.keep_planes
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=5))
+    depth = eng.max_inflight
+    assert depth == 4
+    for b in range(depth):
+        eng.submit_device(ring.data_ptr(), T)
+    total = 0
+    for b in range(NB):
+        res = orc.run(ring_h[:, 0], mask_frames=range(b % 7, T, 23))
+        eng.wait()
+        for t in range(T):
+            _check_frame(eng, res, t, 0, t, f"batch {b} frame {t}")
+        total += int(res.counts.sum())
+        if b + depth < NB:                             # slot of batch b reused: the ring wrap
+            eng.submit_device(ring.data_ptr(), T)
+    np.testing.assert_array_equal(eng.background(0), orc.bg)
+    assert total > 0
+    eng.close()
+
+
+def _run_streams(W, H, box, k, S, T, NB, masks=None, start=0, mask_every=7, threads=4):
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=T)
+    h, w = eng.work_shape
+    cfg = oracle.OracleConfig(H=H, W=W, box=box, ksize=k)
+    keeps = [None] * S
+    if masks:
+        for s in range(S):
+            keeps[s] = rasterize_masks(h, w, box / W, masks)
+            eng.set_mask(s, keeps[s])
+    orc = [oracle.OracleStream(cfg, keeps[s]) for s in range(S)]
+    batches = [batch(W, H, S, start + b * T, T) for b in range(NB)]
+    depth = min(eng.max_inflight, NB)
+    for b in range(depth):
+        eng.submit(batches[b])
+    pool = ThreadPoolExecutor(S)
+    for b in range(NB):
+        fr = batches[b]
+        res = list(pool.map(lambda s: orc[s].run(fr[:, s], mask_frames=range(s % mask_every, T, mask_every),
+                                                 nthreads=threads), range(S)))
+        eng.wait()
+        for s in range(S):
+            for t in range(T):
+                _check_frame(eng, res[s], t, s, t, f"batch {b} frame {t} stream {s}")
+        if b + depth < NB:
+            eng.submit(batches[b + depth])
+    for s in range(S):
+        np.testing.assert_array_equal(eng.background(s), orc[s].bg, err_msg=f"background stream {s}")
+    pool.shutdown()
+    eng.close()
+
+
+def test_config3_eight_1080p_streams_inflight():
+    """configs[2]: 8 x 1080p streams batched on one GPU, per-stream background, 5 batches of 8 frames
+    (4 in flight, one slot reused)."""
+    _run_streams(1920, 1080, 1920, 5, S=8, T=8, NB=5, start=40, threads=2)
+
+
+def test_config5_four_4k_streams_k21_masks():
+    """configs[4] geometry: 4 x 3840x2160, -B 3840 -b 183 -> k 21, MASK_SCHEMA rect + triangle."""
+    k = make_gaussian(3840, 183)
+    assert k == 21
+    _run_streams(3840, 2160, 3840, k, S=4, T=3, NB=2, masks=CONFIG5_MASKS, start=10, mask_every=2)
+
+
+def _lattice_frames(H, W, pitch, n, offset=0):
+    """Frame 0 black (background init), then n frames of single-pixel dots on a pitch grid:
+    dilated 5x5 with 1-px gaps at pitch 6, one contour per dot (ksize 1, threshold 0)."""
+    fr = np.zeros((n + 1, 1, H, W, 3), np.uint8)
+    for i in range(n):
+        o = (offset + i) % pitch
+        fr[i + 1, 0, o::pitch, o::pitch] = 255
+    return fr
+
+
+@pytest.mark.parametrize("cap", [4096, 100])
+def test_contours_past_max_contours(cap):
+    """A 1080p dot lattice (~57,600 contours per frame, every tile heavy): the count and every record
+    are exact whatever max_contours is, records in raster order of their start pixels."""
+    H, W = 1080, 1920
+    fr = _lattice_frames(H, W, 6, 2)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.5,
+                       max_batch=fr.shape[0], max_contours=cap)
+    eng.submit(fr)
+    eng.wait()
+    assert eng.fallbacks() == 0
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=1, thresh=0, alpha=0.5))
+    res = orc.run(fr[:, 0], cap=1 << 17, mask_frames=[1, 2])
+    assert res.counts[1] > 50000
+    for t in range(fr.shape[0]):
+        _check_frame(eng, res, t, 0, t, f"frame {t}")
+    eng.close()
+
+
+def test_node_pool_exhaustion_falls_back_to_pixel_ccl():
+    """32 dense-lattice frames in one batch (~107 components per tile-frame) need more union-find nodes
+    than the slot's pool holds (64 per tile-frame on average): the frames that fail to get nodes are
+    relabelled by the pixel-level CCL in fm_wait (fm_kernels.hip) -- every frame still equals the oracle."""
+    H, W = 540, 960
+    fr = _lattice_frames(H, W, 6, 32, offset=1)
+    # avg 0: the background stays black, so every frame's threshold mask is its own lattice
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.0,
+                       max_batch=fr.shape[0], max_contours=512)
+    eng.submit(fr)
+    eng.wait()
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=1, thresh=0, alpha=0.0))
+    res = orc.run(fr[:, 0], cap=1 << 16, mask_frames=range(fr.shape[0]))
+    assert res.counts[1:].min() > 10000
+    assert eng.fallbacks() > 0  # all frames allocate concurrently, so typically every one of them
+    for t in range(fr.shape[0]):
+        _check_frame(eng, res, t, 0, t, f"frame {t}")
+    eng.close()
+
+
+def test_k97_per_frame_path():
+    """-B 1920 -b 20 (the CLI's default blur scale at full width): k = 97 > 49 takes the per-frame k_pixel
+    kernel and the pixel-level CCL (fm_kernels.hip)."""
+    k = make_gaussian(1920, 20)
+    assert k == 97
+    _run_streams(1920, 120, 1920, k, S=2, T=3, NB=2, mask_every=1)
+
+
+@pytest.mark.parametrize("k", [11, 33, 49])
+def test_k_fused_generic_taps(k):
+    """k outside k_pix's {3, 5, 7, 21} and <= 49: the generic temporally blocked k_fused kernel."""
+    _run_streams(256, 200, 256, k, S=2, T=4, NB=2, mask_every=1)

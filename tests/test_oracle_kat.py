@@ -400,3 +400,27 @@ def test_cross_check_against_real_opencv():
     cnts = cv2.findContours(d, cv2.RETR_EXTERNAL, cv2.CHAIN_APPROX_SIMPLE)[-2]
     assert len(cnts) == len(oracle.find_contours_ext(d))
     assert sorted(cv2.boundingRect(c) for c in cnts) == sorted(c["bbox"] for c in oracle.find_contours_ext(d))
+
+
+@pytest.mark.parametrize("W,H,box,k,masked", [(160, 120, 160, 5, False), (203, 131, 203, 21, True),
+                                               (640, 480, 100, 5, True), (7, 5, 7, 3, False)])
+def test_sequence_schedule_equals_frame_steps(oracle_lib, W, H, box, k, masked):
+    """OracleStream.run (frames in parallel where find_diff's data flow allows) == step() frame by frame:
+    counts, boxes, origins, areas, masks and the background, across two calls (the init frame in the first)."""
+    from find_motion_amd.synthetic import batch as syn_batch
+
+    cfg = oracle_lib.OracleConfig(H=H, W=W, box=box, ksize=k, thresh=10, alpha=0.2)
+    keep = None
+    if masked:
+        keep = np.ones((cfg.h, cfg.w), np.uint8)
+        keep[: cfg.h // 3, : cfg.w // 2] = 0
+    a, b = oracle_lib.OracleStream(cfg, keep), oracle_lib.OracleStream(cfg, keep)
+    fr = syn_batch(W, H, 1, 3, 45)[:, 0]
+    for lo, hi in ((0, 37), (37, 45)):
+        ref = [a.step(fr[i]) for i in range(lo, hi)]
+        got = b.run(fr[lo:hi], mask_frames=range(hi - lo), nthreads=3)
+        for j, r in enumerate(ref):
+            assert got.counts[j] == r["count"] and got.boxes(j) == r["boxes"] and got.origins(j) == r["origins"]
+            np.testing.assert_array_equal(got.areas(j), r["areas"])
+            np.testing.assert_array_equal(got.masks[j], r["mask"])
+        np.testing.assert_array_equal(b.bg, a.bg)
