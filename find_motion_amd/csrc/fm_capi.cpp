@@ -124,6 +124,8 @@ struct fm_ctx {
     std::string err;
     uint64_t* d_ts = nullptr;     // FM_TS: contour-pass phase stamps (profiling)
     uint64_t* d_pts = nullptr;    // FM_PTS=<file>: k_pix workgroup stamps of the last launch (profiling)
+    int32_t* h_err = nullptr;     // mapped: FM_OOB violation bits (checked build), 0 otherwise
+    int32_t* dh_err = nullptr;
     std::vector<double> ts_sum;   // summed phase deltas (cycles)
     std::vector<int64_t> ts_n;
     bool serial = false;  // FM_SERIAL: contour pass on the pixel stream (profiling: no overlap)
@@ -433,12 +435,12 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         // sharing one (in order) with a contour-pass stream
         int lo = 0, hi = 0;
         HIP_TRY(cp, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        if (std::getenv("FM_PIX_PRIO_OFF")) hi = lo;
+        if (dev_env("FM_PIX_PRIO_OFF")) hi = lo;
         HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
     }
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
-    if (!std::getenv("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
+    if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
@@ -452,13 +454,13 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
                    ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
     c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
-                 std::getenv("FM_NO_PIX") == nullptr;
+                 dev_env("FM_NO_PIX") == nullptr;
     c->nslots = c->use_fused ? kSlots : 1;
     // contour-pass streams shared round-robin by the slots: few streams, because the
     // runtime multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order,
     // and a contour kernel queued ahead of a pixel kernel on a shared queue stalls it
     c->nccl = 2;
-    if (const char* e = std::getenv("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
+    if (const char* e = dev_env("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
@@ -520,6 +522,9 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         (rc = dalloc(cp, &c->d_rec_dev, (c->use_fused ? 1 : frames) * (size_t)p.max_contours * 5)))
         return rc;
     c->rec_dev_cap = (size_t)p.max_contours;
+    HIP_TRY(cp, hipHostMalloc((void**)&c->h_err, sizeof(int32_t), hipHostMallocMapped));
+    HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->dh_err, c->h_err, 0));
+    *c->h_err = 0;
     HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
     HIP_TRY(cp, hipMemset(c->d_bg[0], 0, S * c->work_plane * sizeof(double)));
     HIP_TRY(cp, hipMemset(c->d_bg[1], 0, S * c->work_plane * sizeof(double)));
@@ -536,13 +541,13 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     }
     c->bg_init.assign(S, 0);
     c->has_keep.assign(S, 0);
-    if (const char* e = std::getenv("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
-    c->serial = std::getenv("FM_SERIAL") != nullptr;
-    if (std::getenv("FM_PTS") && c->use_pix) {
+    if (const char* e = dev_env("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
+    c->serial = dev_env("FM_SERIAL") != nullptr;
+    if (dev_env("FM_PTS") && c->use_pix) {
         if ((rc = dalloc(cp, &c->d_pts, (size_t)S * c->ntiles * 4))) return rc;
         HIP_TRY(cp, hipMemset(c->d_pts, 0, (size_t)S * c->ntiles * 4 * sizeof(uint64_t)));
     }
-    if (std::getenv("FM_TS") && c->use_fused) {
+    if (dev_env("FM_TS") && c->use_fused) {
         if ((rc = dalloc(cp, &c->d_ts, frames * c->ntiles * 16))) return rc;
         c->ts_sum.assign(16, 0.0);
         c->ts_n.assign(16, 0);
@@ -561,7 +566,7 @@ void fm_destroy(fm_ctx* c) {
         std::vector<uint64_t> v(n);
         if (hipDeviceSynchronize() == hipSuccess &&
             hipMemcpy(v.data(), c->d_pts, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess) {
-            if (FILE* fh = std::fopen(std::getenv("FM_PTS"), "wb")) {
+            if (FILE* fh = std::fopen(dev_env("FM_PTS"), "wb")) {  // dev build only (d_pts)
                 std::fwrite(v.data(), sizeof(uint64_t), n, fh);
                 std::fclose(fh);
             }
@@ -599,6 +604,7 @@ void fm_destroy(fm_ctx* c) {
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamDestroy(st);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     delete c;
 }
 
@@ -757,6 +763,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.dbg_skip = c->dbg_skip;
         fa.dbg_ts = c->d_ts;
         fa.dbg_pts = c->d_pts;
+        fa.dbg_err = c->dh_err;
         if (c->d_ts) HIP_TRY(c, hipMemsetAsync(c->d_ts, 0, F * c->ntiles * 16 * sizeof(uint64_t), ps));
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];
         fa.t_begin = 0;
@@ -860,6 +867,9 @@ int fm_wait(fm_ctx* c) {
     // Frames whose records do not fit the cap are fetched whole, so len(frame.contours)
     // and the records kept never depend on max_contours (fm.py:674-694 counts them all).
     std::vector<std::pair<size_t, std::vector<int32_t>>> whole;
+#ifdef FM_BOUNDS_CHECK
+    if (*c->h_err) return fail(c, FM_EHIP, "contour-pass bounds check failed: codes 0x%x", *c->h_err);
+#endif
     c->fallbacks = 0;
     if (c->use_fused) {
         c->stats[0] = B.h_stats[0];

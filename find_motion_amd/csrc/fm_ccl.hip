@@ -459,6 +459,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             if ((par[i]) == i) ord[i] = (uint16_t)kk++;
     }
     sfence<G>();
+    if (FM_OOB(a, (long long)nb + nroots <= (long long)a.nnodes, 3)) return TCCL_NODES;
     NodeRec* NR = a.nodes + nb;
     for (int i = base; i < base + nr; i++) {
         const int pi = (par[i]);
@@ -626,8 +627,10 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
     const size_t F = (size_t)a.T * a.S;
     const int nc = a.ncr[2 * f];
     const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
+    if (FM_OOB(a, nc >= 0 && nc <= a.ntiles, 1)) return;
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int ti = a.clist[f * a.ntiles + k];
+        if (FM_OOB(a, ti >= 0 && ti < a.ntiles, 1)) continue;
         FM_STAMP(1);
         uint64_t m;
         if (DILATE && !(a.dbg_skip & 128)) {
@@ -640,7 +643,10 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
         if (a.dbg_skip & 64) continue;  // profiling ablation (results invalid)
         const int r = tile_ccl<LIGHT, false>(a, f, ti, ln, m, sc);
         if (ln == 0) {
-            if (r == TCCL_RUNS) a.heavy[atomicAdd(&a.count[2 * F + 1], 1)] = (int)(f * a.ntiles + ti);
+            if (r == TCCL_RUNS) {
+                const int hi = atomicAdd(&a.count[2 * F + 1], 1);
+                if (!FM_OOB(a, hi < (int)(F * a.ntiles), 2)) a.heavy[hi] = (int)(f * a.ntiles + ti);
+            }
             else if (r != TCCL_OK) a.count[F + f] = 1;
         }
     }
@@ -657,8 +663,10 @@ __global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
     const size_t F = (size_t)a.T * a.S;
     const int n = a.count[2 * F + 1];
     const int ln = threadIdx.x;
+    if (FM_OOB(a, n <= (int)(F * a.ntiles), 2)) return;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
+        if (FM_OOB(a, item >= 0 && item < (int)(F * a.ntiles), 4)) continue;
         const size_t f = item / a.ntiles;
         const int ti = (int)(item - (long long)f * a.ntiles);
         const int r = tile_ccl<MAXR, true>(a, f, ti, ln, a.dbits[(f * a.ntiles + ti) * 64 + ln],
@@ -677,6 +685,8 @@ __device__ __forceinline__ int enode(const TileRec* TR, int tile, uint16_t e) { 
 // every candidate around a moving object borders the big outer background, and
 // unions into that one root serialise on its atomics); an enclosed region is unioned.
 __device__ __forceinline__ void touch_region(NodeRec* N, int nd, int rnode) {
+    // (rnode = f*ntiles + a representative tile < F*ntiles: regrep is written for every
+    // empty tile by k_regions of this batch)
     if (N[rnode].flags & 2) atomicOr(&N[nd].flags, 2u);
     else gunion(N, nd, rnode);
 }
@@ -696,6 +706,7 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const int nc = a.ncr[2 * f];
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int t = a.clist[f * nt + k];
+        if (FM_OOB(a, t >= 0 && t < nt && TR[t].nbase >= 0 && TR[t].nbase + TR[t].nroots <= a.nnodes, 5)) continue;
         const int tx = t % ntx, ty = t / ntx;
         const bool hasR = tx + 1 < ntx, hasD = ty + 1 < a.nty;
         // right edge
@@ -794,10 +805,14 @@ __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
     for (int k = blockIdx.x * CW + wv; k < nc + nr; k += gridDim.x * CW) {
         if (k < nc) {
             const int t = a.clist[f * a.ntiles + k];
+            if (FM_OOB(a, t >= 0 && t < a.ntiles, 1)) continue;
             const int k1 = TRf[t].nroots, nb = TRf[t].nbase;
+            if (FM_OOB(a, nb >= 0 && (long long)nb + k1 <= a.nnodes, 5)) continue;
             for (int i = ln; i < k1; i += 64) fold_node(N, nb + i);
         } else if (ln == 0) {
-            fold_node(N, (int)(f * a.ntiles) + a.rlist[f * a.ntiles + (k - nc)]);
+            const int r = a.rlist[f * a.ntiles + (k - nc)];
+            if (FM_OOB(a, r >= 0 && r < a.ntiles, 6)) continue;
+            fold_node(N, (int)(f * a.ntiles) + r);
         }
     }
 }
@@ -816,6 +831,7 @@ __device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wav
     const int nc = a.ncr[2 * f];
     for (int k = wave; k < nc; k += nwaves) {
         const int t = a.clist[f * a.ntiles + k];
+        if (FM_OOB(a, t >= 0 && t < a.ntiles, 1)) continue;
         const int k1 = TRf[t].nroots, nbt = TRf[t].nbase;
         for (int i = ln; i < k1; i += 64) {
             const int n = nbt + i;
@@ -828,6 +844,7 @@ __device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wav
                 ext = true;
             } else {
                 const int tf = (fy / TS) * a.ntx + fx / TS;  // tile of the raster-first pixel (a candidate)
+                if (FM_OOB(a, tf >= 0 && tf < a.ntiles && (!(ref & REF_EDGE) || tf % a.ntx > 0), 7)) continue;
                 int bn;
                 if (ref & REF_EDGE) {
                     const int lt = tf - 1;
@@ -835,6 +852,7 @@ __device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wav
                 } else {
                     bn = TRf[tf].nbase + (int)ref;
                 }
+                if (FM_OOB(a, bn >= 0 && bn < a.nnodes && N[bn].parent >= 0 && N[bn].parent < a.nnodes, 5)) continue;
                 ext = (N[N[bn].parent].flags & 2) != 0;
             }
             if (!ext) continue;

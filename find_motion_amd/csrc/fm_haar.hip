@@ -615,7 +615,11 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
     const long long nw = (long long)n * g.NW;
     if (nw > 0) {
         // stages evaluated for every window before survivors are compacted (FM_HAAR_SPLIT, default 4)
+        #ifdef FM_DEV_SWITCHES  // A/B switch of the dev build only (make VARIANT=dev)
         static const int split_env = std::getenv("FM_HAAR_SPLIT") ? std::atoi(std::getenv("FM_HAAR_SPLIT")) : 4;
+#else
+        static const int split_env = 4;
+#endif
         const int split = std::max(1, std::min(split_env, h->n_stages));
         if ((rc = grow(h, &h->d_live, h->cap_live, (size_t)nw))) return rc;
         if (!h->d_nlive) HH(h, hipMalloc((void**)&h->d_nlive, sizeof(int)));

@@ -5,12 +5,34 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
 #include "../../include/find_motion_amd.h"
 
 namespace fm {
+
+// Developer switches (A/B experiments, profiling stamps) are read from the environment
+// only by the dev build (make VARIANT=dev -> libfm_hip_dev.so); the product library
+// ignores the environment.
+inline const char* dev_env(const char* name) {
+#ifdef FM_DEV_SWITCHES
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// Bounds checks on every data-dependent index of the contour pass (make VARIANT=checked ->
+// libfm_hip_checked.so): a violation sets bit `code` of the mapped error word, the access is
+// skipped, and fm_wait fails with the codes.  Compiled out of the product library.
+#ifdef FM_BOUNDS_CHECK
+#define FM_OOB(a, cond, code) (!(cond) ? (atomicOr((a).dbg_err, 1 << (code)), true) : false)
+#else
+#define FM_OOB(a, cond, code) false
+#endif
 
 constexpr int kMaxK = 255;        // largest Gaussian size handled by the tiled kernel
 constexpr int kCclBlock = 32;     // CCL block edge (pixels)
@@ -125,6 +147,7 @@ struct FusedArgs {
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
     uint64_t* dbg_pts;           // profiling-only k_pix workgroup stamps [S][ntiles][4] (FM_PTS); nullptr in normal use
+    int32_t* dbg_err;            // mapped host word: FM_OOB violation bits (checked build only)
     double alpha, beta;
     long long acc_vec_end;
     int32_t coef[kMaxK];

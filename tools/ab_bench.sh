@@ -1,4 +1,6 @@
 #!/bin/bash
+# FM_* developer switches are honoured only by the dev build: make -C find_motion_amd/csrc VARIANT=dev
+export FM_HIP_LIB=${FM_HIP_LIB:-$PWD/find_motion_amd/libfm_hip_dev.so}
 # Serial-mode bench of each A/B library variant under abvar/ (pixel kernel time, frames/s).
 for D in abvar/*/; do
   N=$(basename $D)

@@ -1,4 +1,6 @@
 #!/bin/bash
+# FM_* developer switches are honoured only by the dev build: make -C find_motion_amd/csrc VARIANT=dev
+export FM_HIP_LIB=${FM_HIP_LIB:-$PWD/find_motion_amd/libfm_hip_dev.so}
 # Pipelined (default-mode) bench under stage ablations (results invalid): which side bounds the steady state.
 mkdir -p gpurun_out
 for M in ${MASKS:-0 64 15 79}; do

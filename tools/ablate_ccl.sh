@@ -1,4 +1,6 @@
 #!/bin/bash
+# FM_* developer switches are honoured only by the dev build: make -C find_motion_amd/csrc VARIANT=dev
+export FM_HIP_LIB=${FM_HIP_LIB:-$PWD/find_motion_amd/libfm_hip_dev.so}
 # Contour-pass ablations (FM_DEBUG_SKIP bits >= 64; results invalid), serial mode.
 mkdir -p gpurun_out
 for M in 0 64 128 192 256; do

@@ -1,4 +1,6 @@
 #!/bin/bash
+# FM_* developer switches are honoured only by the dev build: make -C find_motion_amd/csrc VARIANT=dev
+export FM_HIP_LIB=${FM_HIP_LIB:-$PWD/find_motion_amd/libfm_hip_dev.so}
 # Pixel-kernel stage ablations (FM_DEBUG_SKIP bits 1 gray, 2 chain, 4 raw loads, 8 raw->LDS, 16 barrier; results
 # invalid), serial mode, with workgroup-duration percentiles from FM_PTS stamps.
 mkdir -p gpurun_out

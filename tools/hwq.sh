@@ -1,4 +1,6 @@
 #!/bin/bash
+# FM_* developer switches are honoured only by the dev build: make -C find_motion_amd/csrc VARIANT=dev
+export FM_HIP_LIB=${FM_HIP_LIB:-$PWD/find_motion_amd/libfm_hip_dev.so}
 # Contour-stream count x pixel-stream priority sweep of the default bench.
 for P in "" "FM_PIX_PRIO_OFF=1"; do
 for N in ${NS:-2 3 4}; do
