@@ -74,21 +74,73 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(cfg: dict, frames_host: np.ndarray, n_frames: int) -> dict:
-    """The oracle (C restatement, not OpenCV) on a bounded sample of the same workload."""
+    """The oracle (C restatement, not OpenCV) on a bounded sample of the same workload, per SURVEY.md §8d:
+    P worker threads, one stream each (run_pool's one video per worker, find_motion.py:1071-1075), frames
+    pre-generated in RAM, 10 warm-up frames, the median of 5 timed runs; plus one thread on one stream."""
     import oracle
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    aff = len(os.sched_getaffinity(0))
+    # P = len(sched_getaffinity(0)), capped by OMP_NUM_THREADS: the GPU box sets it to the CPU share of
+    # one GPU (16) and allows no larger worker pools
+    cap = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    threads = max(1, min(aff, cap))
     ocfg = oracle.OracleConfig(H=cfg["H"], W=cfg["W"], box=cfg["box"], ksize=cfg["ksize"],
                                thresh=cfg["threshold"], alpha=cfg["avg"])
     seq = np.ascontiguousarray(frames_host[:n_frames])
-    oracle.run_streams(ocfg, seq[:2], threads, n_streams=threads)  # warm-up (page-in, OpenMP pool)
+    warm = np.ascontiguousarray(frames_host[:10])
+    oracle.run_streams(ocfg, warm, threads, n_streams=threads)  # 10 warm-up frames per worker
+    runs = []
+    used = threads
+    for _ in range(5):
+        t0 = time.perf_counter()
+        _, used = oracle.run_streams(ocfg, seq, threads, n_streams=threads)
+        runs.append(time.perf_counter() - t0)
+    dt = float(np.median(runs))
     t0 = time.perf_counter()
-    _, used = oracle.run_streams(ocfg, seq, threads, n_streams=threads)
-    dt = time.perf_counter() - t0
+    oracle.run_streams(ocfg, seq, 1, n_streams=1)
+    single = n_frames / (time.perf_counter() - t0)
     return {"value": round(threads * n_frames / dt, 2), "unit": "frames/s", "cores": used, "kind": "port",
-            "sample": f"{threads} streams x {n_frames} frames {cfg['W']}x{cfg['H']} box {cfg['box']} k {cfg['ksize']}, "
-                      f"C restatement of the OpenCV chain (oracle/fm_oracle.c, -O2, one OpenMP thread per stream; "
-                      f"not OpenCV, which is not installed), {dt:.2f}s wall, CPU: {cpu_model()}"}
+            "single_stream_1_core": round(single, 2),
+            "sample": f"{threads} workers x 1 stream x {n_frames} frames {cfg['W']}x{cfg['H']} box {cfg['box']} "
+                      f"k {cfg['ksize']}, median of 5 runs after 10 warm-up frames ({aff} CPUs in affinity, "
+                      f"OMP_NUM_THREADS cap {cap}); CPU restatement of the OpenCV chain, not OpenCV "
+                      f"(oracle/fm_oracle.c, gcc -O3 -march=x86-64-v3; cv2 is not installed); CPU: {cpu_model()}"}
+
+
+def spawn_ranks(n: int) -> int:
+    """bench.py --gpus N without a launcher: start N ranks of this script (one per GPU, RANK = LOCAL_RANK =
+    device ordinal, rendezvous on 127.0.0.1) before any GPU call in this process, and return the worst
+    exit status.  Rank 0's stdout carries the JSON line."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, abs(p.wait()))
+            if rc:
+                break
+    finally:
+        for p in procs:  # a failed rank: stop the others (exact child PIDs)
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+            rc = max(rc, abs(p.returncode or 0))
+    return rc
 
 
 def main() -> None:
@@ -115,9 +167,13 @@ def main() -> None:
                     help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     from find_motion_amd import dist
 
     pl = dist.placement_from_env()
+    if pl.world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={pl.world} (launch {args.gpus} ranks, or none)")
     rank, world, local = pl.rank, pl.world, pl.local_rank
 
     import torch
