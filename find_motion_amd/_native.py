@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_PKG, "libfm_hip.so")
 LIB_PATH = os.environ.get("FM_HIP_LIB", LIB_PATH)
 
 FM_OK, FM_EINVAL, FM_EHIP, FM_ENOMEM, FM_ESTATE, FM_ENOTSUP = 0, -1, -2, -3, -4, -5
-FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE, FM_FLAG_PROFILE_PIX = 0x1, 0x2, 0x4
+FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE, FM_FLAG_PROFILE_PIX, FM_FLAG_CONTOUR_AREA = 0x1, 0x2, 0x4, 0x8
 PLANE_GRAY, PLANE_BLUR, PLANE_DELTA = 0, 1, 2
 
 EXPORTED = (
@@ -59,7 +59,7 @@ class FMHaarDesc(C.Structure):
 
 class FMContour(C.Structure):
     _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("w", C.c_int32), ("h", C.c_int32),
-                ("origin_x", C.c_int32), ("origin_y", C.c_int32), ("reserved0", C.c_int32),
+                ("origin_x", C.c_int32), ("origin_y", C.c_int32), ("area2", C.c_int32),
                 ("reserved1", C.c_int32)]
 
 
@@ -144,12 +144,14 @@ class Contour:
     """One external contour of VideoFrame.contours (fm.py:269-276).
 
     bbox is cv2.boundingRect's (x, y, w, h) (fm.py:792); origin is the border
-    start (the component's raster-first pixel)."""
+    start (the component's raster-first pixel); area is cv2.contourArea of the
+    CHAIN_APPROX_SIMPLE contour (fm.py:679), None unless the engine traces it."""
     x: int
     y: int
     w: int
     h: int
     origin: tuple
+    area: float | None = None
 
     @property
     def bbox(self):
@@ -161,12 +163,13 @@ class MotionEngine:
 
     def __init__(self, *, n_streams: int, src_w: int, src_h: int, box_size: int, ksize: int,
                  threshold: int, avg: float, max_batch: int = 1, max_contours: int = 4096,
-                 keep_planes: bool = False, profile: bool | str = False, device: int = 0):
+                 keep_planes: bool = False, profile: bool | str = False, device: int = 0,
+                 contour_area: bool = False):
         # profile: True = every kernel timed with HIP events, "pix" = pixel-stream kernels only
         self._L = load()
         p = FMParams(device, n_streams, src_w, src_h, box_size, ksize, int(threshold), float(avg),
                      max_batch, max_contours,
-                     (FM_FLAG_KEEP_PLANES if keep_planes else 0) |
+                     (FM_FLAG_KEEP_PLANES if keep_planes else 0) | (FM_FLAG_CONTOUR_AREA if contour_area else 0) |
                      (FM_FLAG_PROFILE_PIX if profile == "pix" else FM_FLAG_PROFILE if profile else 0))
         h = C.c_void_p()
         rc = self._L.fm_create(C.byref(h), C.byref(p))
@@ -313,7 +316,8 @@ class MotionEngine:
             buf = (FMContour * cap)()
             n = self._check(self._L.fm_get_contours(self._h, frame, stream, C.cast(buf, C.c_void_p), cap))
             if n <= cap:
-                return [Contour(c.x, c.y, c.w, c.h, (c.origin_x, c.origin_y)) for c in buf[:n]]
+                return [Contour(c.x, c.y, c.w, c.h, (c.origin_x, c.origin_y), c.area2 / 2 if c.area2 >= 0 else None)
+                        for c in buf[:n]]
             cap = n
 
     def mask(self, frame: int, stream: int) -> np.ndarray:

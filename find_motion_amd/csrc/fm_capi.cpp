@@ -98,6 +98,8 @@ struct fm_ctx {
     uint8_t* d_outer = nullptr;
     int32_t* d_rec_dev = nullptr;  // pixel-level CCL records [rec_dev_cap][5]
     size_t rec_dev_cap = 0;
+    int32_t* d_area = nullptr;     // FM_FLAG_CONTOUR_AREA: jobs [area_cap][3] + areas [area_cap]
+    size_t area_cap = 0;
     int32_t* d_rec_all = nullptr;  // k_emit_all records of one frame [rec_all_cap][5] + counter
     size_t rec_all_cap = 0;
     bool use_fused = false;
@@ -312,6 +314,42 @@ int relabel_frame(fm_ctx* c, BatchSlot& B, size_t f, std::vector<int32_t>& out, 
         c->rec_dev_cap = (size_t)n;
     }
     return fail(c, FM_EHIP, "pixel-level relabel of frame %zu did not converge", f);
+}
+
+// FM_FLAG_CONTOUR_AREA: 2 x contourArea of every contour of the finished batch in slot B, traced
+// on the GPU from its start pixel on the batch's dilated masks (fm.py:679)
+int contour_areas(fm_ctx* c, BatchSlot& B, size_t F) {
+    std::vector<int32_t> jobs;
+    for (size_t f = 0; f < F; f++)
+        for (const fm_contour& o : c->contours[f]) {
+            jobs.push_back((int32_t)f);
+            jobs.push_back(o.origin_x);
+            jobs.push_back(o.origin_y);
+        }
+    const size_t n = jobs.size() / 3;
+    if (n == 0) return FM_OK;
+    if (n > c->area_cap) {
+        dfree(c->d_area);
+        c->area_cap = 0;
+        if (int rc = dalloc(c, &c->d_area, n * 4)) return rc;
+        c->area_cap = n;
+    }
+    hipStream_t st = c->aux_stream;
+    std::vector<int32_t> a2(n);
+    HIP_TRY(c, hipMemcpyAsync(c->d_area, jobs.data(), n * 3 * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(c, launch_contour_area(st, c->use_fused ? B.d_dbits : nullptr, c->use_fused ? B.d_candf : nullptr,
+                                   c->use_fused ? nullptr : c->d_mask, c->ntiles, c->ntx, c->h, c->w, c->d_area, (int)n,
+                                   c->d_area + n * 3));
+    HIP_TRY(c, hipMemcpyAsync(a2.data(), c->d_area + n * 3, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    size_t k = 0;
+    for (size_t f = 0; f < F; f++)
+        for (fm_contour& o : c->contours[f]) {
+            if (a2[k] < 0) return fail(c, FM_EHIP, "contour of frame %zu at (%d, %d) has no closed border", f, o.origin_x,
+                                       o.origin_y);
+            o.area2 = a2[k++];
+        }
+    return FM_OK;
 }
 
 }  // namespace
@@ -600,7 +638,7 @@ void fm_destroy(fm_ctx* c) {
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
-    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_all);
+    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_all); dfree(c->d_area);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamDestroy(st);
@@ -932,9 +970,12 @@ int fm_wait(fm_ctx* c) {
             o.h = q[4] - q[2] + 1;
             o.origin_x = q[0] % c->w;
             o.origin_y = q[0] / c->w;
-            o.reserved0 = o.reserved1 = 0;
+            o.area2 = -1;
+            o.reserved1 = 0;
         }
     }
+    if (c->p.flags & FM_FLAG_CONTOUR_AREA)
+        if (int rc = contour_areas(c, B, F)) return rc;
     c->ready = n;
     c->ready_slot = si;
     c->ready_gen = B.gen;

@@ -918,7 +918,89 @@ __global__ __launch_bounds__(256) void k_expand_bits(const uint64_t* __restrict_
     for (int i = 0; i < 8 && xs + i < w; i++) dst[i] = ((b >> i) & 1) ? 255 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// cv2.contourArea of an external contour (fm.py:679), for the area filter of fm.py:684.
+// One thread per contour follows its outer border from the start pixel with the rule of
+// OpenCV's icvFetchContour (restated in oracle/fm_oracle.c fetch_contour; the path depends
+// only on which pixels are non-zero) and sums the shoelace over the CHAIN_APPROX_SIMPLE
+// points (the direction changes).  Out-of-image pixels are zero (the 1-px pad).
+struct AreaMask {
+    const uint64_t* dbits;
+    const uint8_t* candf;
+    const uint8_t* mask;
+    int ntiles, ntx, h, w;
+    __device__ __forceinline__ bool px(int f, int x, int y) const {
+        if ((unsigned)x >= (unsigned)w || (unsigned)y >= (unsigned)h) return false;
+        if (mask) return mask[((size_t)f * h + y) * w + x] != 0;
+        const size_t t = (size_t)f * ntiles + (y >> 6) * ntx + (x >> 6);
+        return candf[t] && ((dbits[t * 64 + (y & 63)] >> (x & 63)) & 1ull);
+    }
+};
+
+__global__ __launch_bounds__(256) void k_contour_area(AreaMask m, const int32_t* __restrict__ jobs, int n,
+                                                      int32_t* __restrict__ area2) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    constexpr int dx[8] = {1, 1, 0, -1, -1, -1, 0, 1};
+    constexpr int dy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+    const int f = jobs[3 * i], x0 = jobs[3 * i + 1], y0 = jobs[3 * i + 2];
+    int s = 4, x1 = x0, y1 = y0;
+    do {  // first non-zero neighbour clockwise from the left (outer border: s_end = 4)
+        s = (s - 1) & 7;
+        x1 = x0 + dx[s];
+        y1 = y0 + dy[s];
+    } while (!m.px(f, x1, y1) && s != 4);
+    if (s == 4) {  // an isolated pixel: one point, area 0
+        area2[i] = 0;
+        return;
+    }
+    int x3 = x0, y3 = y0, prev_s = s ^ 4;
+    long long a = 0;
+    int fx = 0, fy = 0, lx = 0, ly = 0, np = 0;
+    const long long cap = 4ll * ((long long)m.w + 2) * ((long long)m.h + 2) + 16;
+    for (long long it = 0;; it++) {
+        if (it > cap) {  // not a border start of this mask: report, never loop forever
+            area2[i] = -1;
+            return;
+        }
+        int x4 = x3, y4 = y3;
+        while (s < 15) {
+            ++s;
+            x4 = x3 + dx[s & 7];
+            y4 = y3 + dy[s & 7];
+            if (m.px(f, x4, y4)) break;
+        }
+        s &= 7;
+        if (s != prev_s) {  // CHAIN_APPROX_SIMPLE keeps the point where the direction changes
+            if (np == 0) {
+                fx = x3;
+                fy = y3;
+            } else {
+                a += (long long)lx * y3 - (long long)ly * x3;
+            }
+            lx = x3;
+            ly = y3;
+            np++;
+            prev_s = s;
+        }
+        if (x4 == x0 && y4 == y0 && x3 == x1 && y3 == y1) break;
+        x3 = x4;
+        y3 = y4;
+        s = (s + 4) & 7;
+    }
+    if (np > 0) a += (long long)lx * fy - (long long)ly * fx;
+    area2[i] = (int32_t)(a < 0 ? -a : a);
+}
+
 }  // namespace cc
+
+hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, const uint8_t* mask, int ntiles,
+                               int ntx, int h, int w, const int32_t* jobs, int n, int32_t* area2) {
+    if (n <= 0) return hipSuccess;
+    const cc::AreaMask m{dbits, candf, mask, ntiles, ntx, h, w};
+    hipLaunchKernelGGL(cc::k_contour_area, dim3((n + 255) / 256), dim3(256), 0, st, m, jobs, n, area2);
+    return hipGetLastError();
+}
 
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
     if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;

@@ -179,6 +179,10 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
 // every external-contour record of frame f of a finished batch (all of them, unlike the
 // capped k_emit), into rec [cap][5]; *cnt must be 0 before
 hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap);
+// 2 x contourArea of external contours by border following (fm_ccl.hip): jobs [n][3] = (frame, origin x,
+// origin y); the dilated mask of frame f is dbits/candf (fused path, [F][ntiles]...) or mask [F][h*w] bytes
+hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, const uint8_t* mask, int ntiles,
+                               int ntx, int h, int w, const int32_t* jobs, int n, int32_t* area2);
 // dilated bit rows of one frame -> mask bytes (VideoFrame.thresh) [h][w]; non-candidate tiles are 0
 hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, uint8_t* out, int h, int w,
                               int ntx);

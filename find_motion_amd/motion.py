@@ -47,6 +47,7 @@ import numpy as np
 
 from . import videoio
 from ._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, CascadeClassifier, MotionEngine, rasterize_masks
+from .feeder import BatchFeeder
 
 log = logging.getLogger("find_motion_amd")
 
@@ -162,9 +163,11 @@ class VideoFrame:
 class VideoMotion:
     """fm.py:294-926 with the per-frame chain on the GPU (see the module docstring)."""
 
+    DEFAULT_MIN_BOX_SCALE = 50  # -m / min_box_scale default (fm.py:300)
     # pylint: disable=too-many-instance-attributes,too-many-arguments
     def __init__(self, filename: typing.Union[str, int, None] = None, outdir: str = "", fps: int = 30,
-                 box_size: int = 100, min_box_scale: int = 50, cache_time: float = 2.0, min_time: float = 0.5,
+                 box_size: int = 100, min_box_scale: int = DEFAULT_MIN_BOX_SCALE, cache_time: float = 2.0,
+                 min_time: float = 0.5,
                  threshold: int = 7, avg: float = 0.1, blur_scale: int = 20,
                  mask_areas: list = None, show: bool = False,
                  codec: str = "MJPG", log_level: int = logging.INFO,
@@ -173,7 +176,8 @@ class VideoMotion:
                  cascades: typing.List[str] = None,
                  yolo_tiny: bool = False, *,
                  device: int = 0, batch: int = 1, capture=None, engine: MotionEngine = None,
-                 stream: int = 0, keep_planes: bool = None, cascade_dir: str = None) -> None:
+                 stream: int = 0, keep_planes: bool = None, cascade_dir: str = None,
+                 pipeline_depth: int = None) -> None:
         self.filename = filename
         if self.filename is None and capture is None:
             raise Exception("Filename required")
@@ -189,6 +193,7 @@ class VideoMotion:
         self.min_box_scale = min_box_scale
         self.min_area = -1
         self.max_area = -1
+        self.area_filter = False  # max_area < min_area: fm.py:684 filters by contourArea
         self.gaussian_scale = blur_scale
         self.cache_frames = int(cache_time * fps)
         self.min_movement_frames = int(min_time * fps)
@@ -226,6 +231,10 @@ class VideoMotion:
         self.keep_planes = (show or self.debug) if keep_planes is None else bool(keep_planes)
         self._engine = engine
         self._own_engine = engine is None
+        self._pipe = None  # BatchFeeder iterator of read() (single-stream engine)
+        # batches in flight on the GPU ahead of the frame being consumed (None: fm_max_inflight);
+        # 1 keeps ref_frame readable after every batch (the engine is idle when a batch is handed out)
+        self.pipeline_depth = pipeline_depth
         self._stream = int(stream)
         self._capture = capture
         self._ahead: typing.Deque[VideoFrame] = deque()
@@ -283,16 +292,14 @@ class VideoMotion:
             return False
         self.scale = self.box_size / self.frame_width
         self.max_area = int((self.frame_width * self.frame_height) / 2 * self.scale)
-        if self.max_area < self.min_area:
-            # the contourArea filter of fm.py:684 is live only in this corner; it needs
-            # traced contour areas, which the GPU path does not produce
-            raise VideoError(f"max_area {self.max_area} < min_area {self.min_area}: the contour-area filter "
-                             f"(fm.py:684) is not supported by the GPU path")
+        # the contourArea filter of fm.py:684 can skip a contour only when max_area < min_area:
+        # then the engine traces every external contour's border on the GPU for its area
+        self.area_filter = self.max_area < self.min_area
         if self._engine is None:
             self._engine = MotionEngine(n_streams=1, src_w=self.frame_width, src_h=self.frame_height,
                                         box_size=self.box_size, ksize=self.gaussian[0], threshold=self.delta_thresh,
                                         avg=self.avg, max_batch=self.batch, keep_planes=self.keep_planes,
-                                        device=self.device)
+                                        device=self.device, contour_area=self.area_filter)
         if self.mask_areas:
             h, w = self._engine.work_shape
             self._engine.set_mask(self._stream, rasterize_masks(h, w, self.scale, self.mask_areas))
@@ -334,30 +341,23 @@ class VideoMotion:
 
     # -- I/O (fm.py:497-546) ---------------------------------------------------
     def read(self) -> bool:
-        """fm.py:497-506, with up to `batch` frames decoded ahead and processed in one launch."""
+        """fm.py:497-506.  Frames are decoded ahead by a BatchFeeder thread into page-locked
+        batches of `batch` frames, up to fm_max_inflight batches in flight on the GPU; read()
+        hands out the processed frames one by one, in order."""
         if not self._ahead:
-            frames = []
-            for _ in range(self.batch):
-                ok, fr = self.cap.read()
-                if not ok:
-                    break
-                frames.append(fr)
-            if not frames:
+            eng = self._engine
+            if eng.n_streams != 1:
+                raise RuntimeError("a shared multi-stream engine is driven by StreamGroup")
+            if self._pipe is None:
+                self._pipe = iter(BatchFeeder(eng, [self.cap], self.batch, self.pipeline_depth))
+            b = next(self._pipe, None)
+            if b is None:
                 return False
-            self._process(frames)
+            vfs = [VideoFrame(r, self.show) for r in b.frames[0]]
+            self.bind_results(vfs, eng, 0)
+            self._ahead.extend(vfs)
         self.current_frame = self._ahead.popleft()
         return True
-
-    def _process(self, raws: list) -> None:
-        """The hot path for a run of frames of this stream (single-stream engine)."""
-        eng = self._engine
-        if eng.n_streams != 1:
-            raise RuntimeError("a shared multi-stream engine is driven by StreamGroup")
-        vfs = [VideoFrame(r, self.show) for r in raws]
-        eng.submit(np.stack([r[None] for r in raws]))
-        eng.wait()
-        self.bind_results(vfs, eng, 0)
-        self._ahead.extend(vfs)
 
     def bind_results(self, vfs, eng, stream: int) -> None:
         for t, vf in enumerate(vfs):
@@ -413,6 +413,8 @@ class VideoMotion:
             self._process_external(frame)
 
     def _process_external(self, frame: VideoFrame) -> None:
+        if self._pipe is not None:
+            raise RuntimeError("cannot process an external frame while the decode-ahead pipeline is running")
         eng = self._engine
         eng.submit(np.asarray(frame.raw, dtype=np.uint8)[None, None])
         eng.wait()
@@ -431,12 +433,14 @@ class VideoMotion:
     # -- consumer state machine (fm.py:549-601, 665-700) -----------------------
     def find_movement(self, frame: VideoFrame = None) -> None:
         """fm.py:665-700.  The area filter of fm.py:684 can only skip a contour when
-        max_area < min_area, which _load_video rejects, so every contour counts."""
+        max_area < min_area (area_filter): then contour.area is the GPU-traced contourArea."""
         frame = self.current_frame if frame is None else frame
         self.movement = False
         self.movement_decay -= 1 if self.movement_decay > 0 else 0
         if frame.contours is not None and len(frame.contours) > 0:
             for contour in frame.contours:
+                if self.area_filter and self.max_area < contour.area < self.min_area:
+                    continue
                 if self.show:
                     self.draw_box(self.make_box(contour, frame), frame)
                 self.movement_counter += 1
@@ -551,6 +555,9 @@ class VideoMotion:
 
     def cleanup(self) -> None:
         """fm.py:824-849, plus releasing the device context."""
+        if self._pipe is not None:  # stop the decoder thread, drain batches in flight
+            self._pipe.close()
+            self._pipe = None
         if self.cap is not None:
             self.cap.release()
         if self.outfile is not None:
@@ -641,40 +648,23 @@ class StreamGroup:
         dbg = kwargs.get("log_level", logging.INFO) == logging.DEBUG
         self.batch = max(1, int(batch))
         make = engine if engine is not None else MotionEngine  # engine: a factory with MotionEngine's signature
+        mbs = kwargs.get("min_box_scale", VideoMotion.DEFAULT_MIN_BOX_SCALE)
+        area_filter = int(W * H / 2 * (box / W)) < int(math.pow(box / mbs, 2))  # as _load_video decides
         self.engine = make(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=make_gaussian_size(box, blur_scale),
                            threshold=kwargs.get("threshold", 7), avg=kwargs.get("avg", 0.1), max_batch=self.batch,
-                           keep_planes=show or dbg, device=device)
+                           keep_planes=show or dbg, device=device, contour_area=area_filter)
         self.videos = [VideoMotion(filename=f, capture=c, engine=self.engine, stream=s, batch=self.batch, **kwargs)
                        for s, (f, c) in enumerate(zip(self.filenames, caps))]
-        self._staging = np.empty((self.batch, S, H, W, 3), np.uint8)
 
     def find_motion(self) -> list:
-        S = len(self.videos)
-        live = [v.loaded for v in self.videos]
-        last = [None] * S
-        while any(live):
-            got = [[] for _ in range(S)]
+        """Decode-ahead into page-locked batches (BatchFeeder), up to fm_max_inflight batches in
+        flight, each waited batch consumed frame by frame by every stream's state machine."""
+        caps = [v.cap if v.loaded else videoio.ArrayCapture([]) for v in self.videos]
+        for b in BatchFeeder(self.engine, caps, self.batch):
             for s, v in enumerate(self.videos):
-                while live[s] and len(got[s]) < self.batch:
-                    ok, fr = v.cap.read()
-                    if not ok:
-                        live[s] = False
-                        break
-                    got[s].append(fr)
-            T = max(len(g) for g in got)
-            if T == 0:
-                break
-            for s in range(S):
-                for t in range(T):
-                    if t < len(got[s]):
-                        self._staging[t, s] = got[s][t]
-                        last[s] = got[s][t]
-                    elif last[s] is not None:
-                        self._staging[t, s] = last[s]  # ended stream: padding, results dropped
-            self.engine.submit(self._staging[:T])
-            self.engine.wait()
-            for s, v in enumerate(self.videos):
-                vfs = [VideoFrame(r, v.show) for r in got[s]]
+                if not b.frames[s]:
+                    continue
+                vfs = [VideoFrame(r, v.show) for r in b.frames[s]]
                 v.bind_results(vfs, self.engine, s)
                 for vf in vfs:
                     v.current_frame = vf

@@ -43,6 +43,9 @@ extern "C" {
 #define FM_FLAG_KEEP_PLANES 0x1u /* keep gray/blur/frame_delta per frame (show/debug, fm.py:907-926) */
 #define FM_FLAG_PROFILE 0x2u     /* time every kernel launch with HIP events */
 #define FM_FLAG_PROFILE_PIX 0x4u /* time only the pixel-stream kernels (cheap enough for the bench's timed loop) */
+#define FM_FLAG_CONTOUR_AREA 0x8u /* trace every external contour's border on the GPU at fm_wait and return
+                                     2 x cv2.contourArea (fm.py:679) in fm_contour.area2: needed only where
+                                     the area filter of fm.py:684 is live (max_area < min_area) */
 
 /* planes for fm_read_plane */
 #define FM_PLANE_GRAY 0  /* VideoFrame.gray        (fm.py:493) */
@@ -71,7 +74,9 @@ typedef struct fm_params {
 typedef struct fm_contour {
     int32_t x, y, w, h;          /* cv2.boundingRect (fm.py:792) */
     int32_t origin_x, origin_y;  /* border start = raster-first pixel of the component */
-    int32_t reserved0, reserved1;
+    int32_t area2;               /* 2 x cv2.contourArea of the CHAIN_APPROX_SIMPLE contour (an integer: the
+                                    shoelace sum); -1 unless the context has FM_FLAG_CONTOUR_AREA */
+    int32_t reserved1;
 } fm_contour;
 
 /* Library version (FM_ABI_VERSION) */

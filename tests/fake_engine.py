@@ -4,6 +4,8 @@ TEST ONLY: it lets tests drive find_motion_amd.motion.VideoMotion's unchanged
 state machine with exact per-frame results.  The product never uses it (the
 product's engine is the HIP library; there is no CPU fallback).
 """
+from collections import deque
+
 import numpy as np
 
 import oracle
@@ -11,8 +13,10 @@ from find_motion_amd._native import Contour
 
 
 class OracleEngine:
+    max_inflight = 4  # like the HIP engine: batches may be submitted before the oldest is waited
+
     def __init__(self, *, n_streams, src_w, src_h, box_size, ksize, threshold, avg, max_batch=1,
-                 keep_planes=False, **_):
+                 keep_planes=False, contour_area=False, **_):
         self.n_streams = n_streams
         self.cfg = oracle.OracleConfig(H=src_h, W=src_w, box=box_size, ksize=ksize, thresh=threshold, alpha=avg)
         self.work_shape = (self.cfg.h, self.cfg.w)
@@ -21,6 +25,9 @@ class OracleEngine:
         self.streams = [oracle.OracleStream(self.cfg) for _ in range(n_streams)]
         self.generation = 0
         self.results = []
+        self._queue = deque()
+        self.src_shape = (src_h, src_w, 3)
+        self.contour_area = contour_area
         self.submits = 0
         self.closed = False
 
@@ -45,10 +52,16 @@ class OracleEngine:
         if frames.ndim == 4:
             frames = frames[None]
         assert frames.shape[0] <= self.max_batch and frames.shape[1] == self.n_streams
-        self.results = [[st.step(frames[t, s]) for s, st in enumerate(self.streams)] for t in range(frames.shape[0])]
+        assert len(self._queue) < self.max_inflight
+        self._queue.append([[st.step(frames[t, s]) for s, st in enumerate(self.streams)] for t in range(frames.shape[0])])
         self.submits += 1
 
+    def host_buffer(self, n_frames):
+        return np.empty((n_frames, self.n_streams) + self.src_shape, np.uint8)
+
     def wait(self):
+        if self._queue:
+            self.results = self._queue.popleft()
         self.generation += 1
 
     def counts(self):
@@ -56,7 +69,8 @@ class OracleEngine:
 
     def contours(self, t, s):
         r = self.results[t][s]
-        return [Contour(*b, o) for b, o in zip(r["boxes"], r["origins"])]
+        areas = r["areas"] if self.contour_area else [None] * len(r["boxes"])
+        return [Contour(*b, o, None if a is None else float(a)) for b, o, a in zip(r["boxes"], r["origins"], areas)]
 
     def mask(self, t, s):
         return self.results[t][s]["mask"]

@@ -175,3 +175,65 @@ def test_k97_per_frame_path():
 def test_k_fused_generic_taps(k):
     """k outside k_pix's {3, 5, 7, 21} and <= 49: the generic temporally blocked k_fused kernel."""
     _run_streams(256, 200, 256, k, S=2, T=4, NB=2, mask_every=1)
+
+
+# --- contourArea for the live area filter (fm.py:679-684) ------------------------
+
+def _area_case(frames, **kw):
+    H, W = frames.shape[2:4]
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, max_batch=frames.shape[0], contour_area=True, **kw)
+    eng.submit(frames)
+    eng.wait()
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=kw["ksize"], thresh=kw["threshold"],
+                                                  alpha=kw["avg"]))
+    res = orc.run(frames[:, 0], cap=1 << 17)
+    for t in range(frames.shape[0]):
+        got = eng.contours(t, 0)
+        assert [c.bbox for c in got] == res.boxes(t), t
+        np.testing.assert_array_equal(np.array([c.area for c in got]), res.areas(t), err_msg=f"areas frame {t}")
+    eng.close()
+    return res
+
+
+def test_contour_area_fixtures_and_random_masks():
+    from golden_cases import contour_cases
+
+    for name, case in sorted(contour_cases().items()):
+        m = case["mask"]
+        fr = np.zeros((2, 1) + m.shape + (3,), np.uint8)
+        fr[1, 0] = m[..., None]
+        _area_case(fr, ksize=1, threshold=0, avg=0.5)
+    rng = np.random.default_rng(11)
+    fr = np.zeros((4, 1, 150, 230, 3), np.uint8)
+    for t in range(1, 4):
+        fr[t, 0] = ((rng.random((150, 230)) < 0.003 * t) * 255).astype(np.uint8)[..., None]
+    res = _area_case(fr, ksize=1, threshold=0, avg=0.0)
+    assert res.counts[1:].min() > 10
+
+
+def test_contour_area_synthetic_video_and_lattice():
+    _area_case(batch(640, 360, 1, 90, 12), ksize=5, threshold=12, avg=0.1)   # includes a flash frame (97)
+    _area_case(_lattice_frames(270, 480, 6, 2), ksize=1, threshold=0, avg=0.0)
+
+
+def test_video_motion_live_area_filter_on_gpu(tmp_path):
+    """-m 1: max_area 5400 < min_area 10000 (192x108, box 100): contours with contourArea in
+    (5400, 10000) are skipped (fm.py:684), on the engine's GPU-traced areas."""
+    from find_motion_amd import motion, videoio
+    from oracle.decision import written_indices
+
+    W, H, n = 192, 108, 110
+    vm = motion.VideoMotion(filename=str(tmp_path / "v"), capture=videoio.SyntheticCapture(W, H, n, 0), box_size=100,
+                            min_box_scale=1, threshold=12, cache_time=0.3, min_time=0.1, batch=8, outdir=str(tmp_path))
+    assert vm.area_filter
+    vm.find_motion()
+    st = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=100, ksize=5))
+    vid = videoio.SyntheticCapture(W, H, n, 0).video
+    counts, skipped = [], 0
+    for i in range(n):
+        a = st.step(vid.frame(i))["areas"]
+        keep = [x for x in a if not (5400 < x < 10000)]
+        skipped += len(a) - len(keep)
+        counts.append(len(keep))
+    assert skipped > 0
+    assert vm.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3)

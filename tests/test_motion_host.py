@@ -95,7 +95,7 @@ def test_output_avi_holds_the_written_source_frames(tmp_path):
 
 
 def test_frame_attributes_bound_from_engine(tmp_path):
-    vm, eng = make_vm(tmp_path, n=6, keep_planes=True)
+    vm, eng = make_vm(tmp_path, n=6, keep_planes=True, pipeline_depth=1)  # ref_frame after every frame
     cfg = eng.cfg
     st = oracle.OracleStream(cfg)
     seen = 0
@@ -152,9 +152,29 @@ def test_external_frame_through_blur_frame(tmp_path):
     assert fr.processed and fr.contours == [] and eng.initialized(0)
 
 
-def test_live_area_filter_configuration_rejected(tmp_path):
-    with pytest.raises(motion.VideoError):
-        make_vm(tmp_path, W=64, H=4, box=64, min_box_scale=1, blur_scale=20)
+def test_live_area_filter_skips_by_contour_area(tmp_path):
+    """-m 1 at 192x108, box 100: max_area 5400 < min_area 10000, so the filter of fm.py:684 is live and
+    contours whose contourArea lies in (5400, 10000) do not count (the flash frames' full-frame blobs)."""
+    W, H, n, box = 192, 108, 110, 100
+    cap = videoio.SyntheticCapture(W, H, n, 0)
+    k = motion.make_gaussian_size(box, 20)
+    eng = OracleEngine(n_streams=1, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=4,
+                       contour_area=True)
+    vm = motion.VideoMotion(filename=str(tmp_path / "v"), capture=cap, engine=eng, batch=4, box_size=box,
+                            min_box_scale=1, cache_time=0.3, min_time=0.1, outdir=str(tmp_path))
+    assert vm.area_filter and (vm.max_area, vm.min_area) == (5400, 10000)
+    vm.find_motion()
+    cfg = oracle.OracleConfig(H=H, W=W, box=box, ksize=k)
+    st = oracle.OracleStream(cfg)
+    vid = videoio.SyntheticCapture(W, H, n, 0).video
+    counts, skipped = [], 0
+    for i in range(n):
+        r = st.step(vid.frame(i))
+        keep = [a for a in r["areas"] if not (5400 < a < 10000)]
+        skipped += len(r["areas"]) - len(keep)
+        counts.append(len(keep))
+    assert skipped > 0  # the flash frames (every 97th) make full-frame contours of area ~5300-5600
+    assert vm.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3)
 
 
 def test_run_vid_error_tuple():
