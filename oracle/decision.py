@@ -15,7 +15,9 @@ return the source frame indices the reference writes, in write order:
 from collections import deque
 
 
-def written_indices(counts, fps: int = 30, min_time: float = 0.5, cache_time: float = 1.0):
+def written_indices(counts, fps: int = 30, min_time: float = 0.5, cache_time: float = 1.0, current_only: bool = False):
+    """current_only: only the frames written as the current frame -- the ones decide_output also
+    runs find_objects on (fm.py:571-575); flushed cache frames are left out."""
     cache_frames = int(cache_time * fps)
     min_frames = int(min_time * fps)
     cache = deque(maxlen=cache_frames)
@@ -31,7 +33,8 @@ def written_indices(counts, fps: int = 30, min_time: float = 0.5, cache_time: fl
         if counter >= min_frames or decay > 0:
             if movement:
                 decay = cache_frames
-                out.extend(cache)
+                if not current_only:
+                    out.extend(cache)
                 cache.clear()
             out.append(i)
         else:

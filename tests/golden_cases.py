@@ -36,3 +36,19 @@ def contour_cases():
     return {n: {"mask": d[n + "__mask"], "boxes": [tuple(int(v) for v in r) for r in d[n + "__boxes"]],
                 "origins": [tuple(int(v) for v in r) for r in d[n + "__origins"]], "areas": d[n + "__areas"]}
             for n in names}
+
+
+def load_frontalface():
+    """(Cascade, fixture dict) of tests/golden/cascade_frontalface_default.npz (make_golden_cascade.py)."""
+    from find_motion_amd.cascade import Cascade
+
+    z = dict(np.load(os.path.join(GOLDEN, "cascade_frontalface_default.npz"), allow_pickle=False))
+    fields = ("stage_ntrees", "stage_threshold", "tree_nodes", "node_left", "node_right", "node_feature",
+              "node_threshold", "leaves", "feat_rects", "feat_weights", "feat_tilted")
+    cs = Cascade(int(z["win"][0]), int(z["win"][1]), *[z[f] for f in fields])
+    dets, k = [], 0
+    for n in z["frames_counts"]:
+        dets.append([tuple(int(v) for v in r) for r in z["frames_detections"][k:k + n]])
+        k += n
+    z["frames_detections_list"] = dets
+    return cs, z

@@ -92,3 +92,37 @@ def make_image(seed=0, w=300, h=169, squares=4, channels=3) -> np.ndarray:
         return img
     return np.stack([img, np.clip(img.astype(np.int32) + rng.integers(-8, 9, img.shape), 0, 255).astype(np.uint8),
                      img], -1)
+
+
+def draw_faces(img: np.ndarray, faces, bg: int = 110, noise: int = 6, seed: int = 0) -> np.ndarray:
+    """A gray BGR image (H, W, 3) of cartoon frontal faces: (cx, cy, r) each an ellipse of skin tone with
+    dark eyes and brows, a light nose bridge and a dark mouth, over a flat background with uniform noise.
+    The reference's haarcascade_frontalface_default.xml detects them (tests/golden/make_golden_cascade.py)."""
+    H, W = img.shape[:2]
+    g = np.full((H, W), bg, np.int16)
+    yy, xx = np.mgrid[:H, :W]
+    for cx, cy, r in faces:
+        g[((xx - cx) / (0.8 * r)) ** 2 + ((yy - cy) / r) ** 2 <= 1] = 175
+        for ex in (-0.38, 0.38):
+            g[((xx - (cx + ex * r)) / (0.2 * r)) ** 2 + ((yy - (cy - 0.22 * r)) / (0.09 * r)) ** 2 <= 1] = 50
+            g[(np.abs(xx - (cx + ex * r)) < 0.25 * r) & (np.abs(yy - (cy - 0.42 * r)) < 0.05 * r)] = 70
+        g[(np.abs(xx - cx) < 0.07 * r) & (yy > cy - 0.15 * r) & (yy < cy + 0.2 * r)] = 150
+        g[((xx - cx) / (0.32 * r)) ** 2 + ((yy - (cy + 0.45 * r)) / (0.08 * r)) ** 2 <= 1] = 80
+    rng = np.random.default_rng(seed)
+    g = np.clip(g + rng.integers(-noise, noise + 1, g.shape), 0, 255).astype(np.uint8)
+    img[...] = g[..., None]
+    return img
+
+
+# 3840x2160 frames of config 5 (find_motion.py:703-731 resizes them to width 300 for the cascades)
+FACE_FRAMES_4K = [
+    dict(faces=[(1024, 1024, 576), (2688, 1152, 448)], seed=1),
+    dict(faces=[(1900, 1000, 700)], seed=2),
+    dict(faces=[(700, 900, 420), (2000, 1100, 420), (3200, 1000, 420)], seed=3),
+    dict(faces=[], seed=4),
+]
+
+
+def face_frame_4k(i: int) -> np.ndarray:
+    c = FACE_FRAMES_4K[i]
+    return draw_faces(np.empty((2160, 3840, 3), np.uint8), c["faces"], seed=c["seed"])

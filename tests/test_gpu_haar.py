@@ -158,3 +158,69 @@ def test_device_resident_images():
     finally:
         hip.hipFree(ptr)
         det.close()
+
+
+# --- the reference's own cascade (haarcascade_frontalface_default.xml, config 5) ----------------
+
+def test_frontalface_roi_candidates_and_detections():
+    from golden_cases import load_frontalface
+
+    cs, z = load_frontalface()
+    det = CascadeClassifier(cs)
+    got = det.detectMultiScale(z["roi_image"], scaleFactor=1.1, minNeighbors=5)
+    assert [tuple(r) for r in det.candidates().tolist()] == [tuple(int(v) for v in r) for r in z["roi_candidates"]]
+    assert [tuple(r) for r in np.asarray(got).reshape(-1, 4).tolist()] == [tuple(int(v) for v in r)
+                                                                          for r in z["roi_detections"]]
+    det.close()
+
+
+def test_frontalface_on_4k_frames_resized_on_device():
+    """find_objects on config 5's 3840x2160 frames: INTER_AREA to width 300 on the device, then
+    detectMultiScale(1.1, 5) with the real cascade, four frames per call."""
+    from golden_cases import load_frontalface
+    from haar_cases import FACE_FRAMES_4K, face_frame_4k
+
+    cs, z = load_frontalface()
+    frames = np.stack([face_frame_4k(i) for i in range(len(FACE_FRAMES_4K))])
+    det = CascadeClassifier(cs)
+    got = det.detect_frames(frames, 300, 1.1, 5)
+    want = z["frames_detections_list"]
+    assert [[tuple(int(v) for v in r) for r in np.asarray(g).reshape(-1, 4)] for g in got] == want
+    assert sum(len(w) for w in want) == 6
+    det.close()
+
+
+def test_config5_workload_streams_masks_and_faces(tmp_path):
+    """configs[4] as one workload: 4 streams of 3840x2160 through StreamGroup with -B 3840 -b 183 (k 21),
+    the MASK_SCHEMA polygons and the frontalface_default cascade on every 15th written frame
+    (find_motion.py:549-589, 703-731).  Written frames equal the decision restatement on oracle counts;
+    the objects seen equal the fixture's detections of the 15th written frame of each stream."""
+    from find_motion_amd import motion, videoio
+    from find_motion_amd.cascade import to_xml
+    from golden_cases import load_frontalface
+    from haar_cases import FACE_FRAMES_4K, face_frame_4k
+    from oracle.decision import written_indices
+
+    cs, z = load_frontalface()
+    (tmp_path / "haarcascade_frontalface_default.xml").write_text(to_xml(cs))
+    uniq = [face_frame_4k(i) for i in range(len(FACE_FRAMES_4K))]
+    S, n = 4, 20
+    order = [[(s + t) % len(uniq) for t in range(n)] for s in range(S)]  # stream s cycles the frames from s
+    masks = [((0, 0), (639, 359)), ((3839, 2159), (3200, 2159), (3839, 1600))]
+    caps = [videoio.ArrayCapture([uniq[i] for i in order[s]]) for s in range(S)]
+    grp = motion.StreamGroup([str(tmp_path / f"s{s}") for s in range(S)], batch=4, captures=caps, box_size=3840,
+                             blur_scale=183, threshold=12, cache_time=0.3, min_time=0.1, mask_areas=masks,
+                             cascades=["frontalface_default"], cascade_dir=str(tmp_path), outdir=str(tmp_path))
+    res = grp.find_motion()
+    cfg = oracle.OracleConfig(H=2160, W=3840, box=3840, ksize=21)
+    keep = motion.rasterize_masks(2160, 3840, 1.0, masks)
+    for s, v in enumerate(grp.videos):
+        r = oracle.OracleStream(cfg, keep).run(np.stack([uniq[i] for i in order[s]]), nthreads=8)
+        want = written_indices(list(r.counts), min_time=0.1, cache_time=0.3)
+        assert v.written_indices == want, s
+        # find_objects runs on every frame written as the current one (not on flushed cache frames)
+        # and detects on its 15th call
+        cur = written_indices(list(r.counts), min_time=0.1, cache_time=0.3, current_only=True)
+        fifteenth = order[s][cur[14]] if len(cur) >= 15 else None
+        seen = {"Face 4"} if fifteenth is not None and z["frames_detections_list"][fifteenth] else set()
+        assert set(res[s][3]) == seen, (s, fifteenth)

@@ -272,3 +272,33 @@ def test_oracle_matches_golden_fixtures(path):
 
 def test_golden_fixtures_present():
     assert len(GOLDEN) == 3
+
+
+# --- the reference's own cascade (tests/golden/cascade_frontalface_default.npz) --------------
+
+REF_XML = "/root/reference/find_motion/haarcascades/haarcascade_frontalface_default.xml"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_XML), reason="reference tree not mounted (GPU box)")
+def test_frontalface_fixture_is_the_reference_cascade():
+    """The fixture's arrays are find_motion_amd.cascade.parse of the reference's XML (config 5's cascade)."""
+    from golden_cases import load_frontalface
+
+    cs, _ = load_frontalface()
+    ref = parse(REF_XML)
+    assert (cs.win_w, cs.win_h) == (ref.win_w, ref.win_h) == (24, 24) and cs.n_stages == 25
+    for f in ("stage_ntrees", "stage_threshold", "tree_nodes", "node_left", "node_right", "node_feature",
+              "node_threshold", "leaves", "feat_rects", "feat_weights", "feat_tilted"):
+        np.testing.assert_array_equal(getattr(cs, f), getattr(ref, f), err_msg=f)
+
+
+def test_frontalface_fixture_detections_from_oracle():
+    """oracle/haar.py on the fixture's ROI image reproduces its stored candidates and detections
+    (the two cartoon faces are found by the real cascade)."""
+    from golden_cases import load_frontalface
+
+    cs, z = load_frontalface()
+    cand = haar.detect_candidates(cs, z["roi_image"], 1.1)
+    assert cand == [tuple(int(v) for v in r) for r in z["roi_candidates"]]
+    assert haar.group_rectangles(cand, 5) == [tuple(int(v) for v in r) for r in z["roi_detections"]]
+    assert len(z["roi_detections"]) == 2
