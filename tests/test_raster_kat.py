@@ -115,10 +115,10 @@ def test_config5_triangle_edges_and_rows():
                                                  (int(np.argmax(m[y])) for y in range(1600, 2160)))
 
 
-def _convex_polys(rng, n, lo=-6, hi=46):
+def _convex_polys(rng, n, vmin=-6, vmax=46):
     out = []
     while len(out) < n:
-        pts = rng.integers(lo, hi, (12, 2))
+        pts = rng.integers(vmin, vmax, (12, 2))
         # convex hull (monotone chain), counter-clockwise in image coordinates
         pts = sorted(set(map(tuple, pts.tolist())))
         if len(pts) < 3:
