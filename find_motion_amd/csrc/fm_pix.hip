@@ -56,7 +56,7 @@ __host__ __device__ constexpr int a16(int v) { return (v + 15) & ~15; }
 // columns x0-PC .. x0+63+PC with PC = 4*ceil(r/4) (quad aligned)
 struct Geo {
     int r, PC, GW, NQ, GH, RS, CPR, nchunks, RSH;
-    int o_raw, o_H, o_rowy, o_colx, bytes;
+    int o_raw, o_H, o_rowy, o_colx, o_atab, bytes;
     int raw_bytes, H_bytes;  // per buffer; raw and H are double buffered
     __host__ __device__ explicit Geo(int rr) {
         r = rr;
@@ -76,7 +76,8 @@ struct Geo {
         o_H = o_raw + 2 * raw_bytes;
         o_rowy = o_H + 2 * H_bytes;
         o_colx = o_rowy + a16(GH * 4);
-        bytes = o_colx + a16(GW * 4);
+        o_atab = o_colx + a16(GW * 4);
+        bytes = o_atab + 256 * 8;  // blur * alpha for blur = 0..255 (f64)
     }
 };
 
@@ -249,7 +250,8 @@ struct ChainCtx {
 // keep-mask bytes (off when the stream has no mask).  TAIL: the wave's rows reach
 // accumulateWeighted's scalar tail (per-pixel test of the product order).
 template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
-__device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const Geo& g, double (&bg)[RPWV],
+__device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const double* atab, const Geo& g,
+                                           double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
                                            bool init, uint32_t& colbits, uint32_t& flags) {
     constexpr int R = KC >> 1;
@@ -269,10 +271,12 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         }
         P[NP] = 0;
     }
-    const double alpha = a.alpha, beta = a.beta;
-    // d in [0, 255]: clamping the threshold to [-1, 255] keeps d > t, and makes the sign of
-    // t - d that test
+    const double beta = a.beta;
+    // d in [0, 255]: with the threshold clamped to [-1, 255] (which keeps d > t), d + (255 - t)
+    // is in [0, 511] and its bit 8 is d > t; v_sad_u8 adds the bias for free and one v_dot4 per
+    // row moves that bit (byte 1 of the sum) to bit j of the lane's column byte
     const int thr = min(max(a.thresh, -1), 255);
+    const uint32_t bias = (uint32_t)(255 - thr);
     uint32_t tb = 0;  // bit j: row 8*wv + j of this lane's column is over the threshold
     static_for<RPWV>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -294,20 +298,22 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8 -- into byte 2 of a copy
         // of acc, so that the byte-wise absdiff of the two words is |blur - q|
 #if FM_PIX_ABL & 2  // timing ablation only (results invalid): no convertScaleAbs / absdiff
-        const uint32_t d = acc >> 16;
+        const uint32_t r = (acc >> 16) + bias;
 #else
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
-        const uint32_t d = __builtin_amdgcn_sad_u8(acc, q, 0u);  // absdiff
+        const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);  // absdiff + bias
 #endif
 #if !(FM_PIX_ABL & 4)  // timing ablation only: no threshold bits
-        tb |= ((uint32_t)(thr - (int)d) >> 31) << j;
+        tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
 #endif
 #if FM_PIX_ABL & 1  // timing ablation only: no f64 background update
         double nb = b + 0.0;
         const double bl = 0.0;
-        (void)alpha; (void)beta;
+        (void)beta;
 #else
-        const double bl = __dmul_rn((double)blur, alpha);
+        // (double)blur * alpha from a 256-entry LDS table (the same correctly rounded product):
+        // an LDS read instead of two f64-rate VALU ops per pixel
+        const double bl = atab[blur];
         double nb = __fma_rn(b, beta, bl);
 #endif
         if (TAIL) {  // accumulateWeighted's scalar tail: two products, one add there
@@ -320,7 +326,7 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
             const size_t plane = (size_t)a.h * w;
             const size_t li = (size_t)(y0 + RPWV * wv + j) * w + x0 + ln;
             a.planes[(size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)blur;
-            a.planes[2 * (size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)d;
+            a.planes[2 * (size_t)a.T * a.S * plane + f * plane + li] = (uint8_t)(r - bias);
         }
     });
     // out-of-image pixels are background for the contour pass
@@ -347,6 +353,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + g.o_H);
     int* rowy = reinterpret_cast<int*>(smem + g.o_rowy);
     int* colx = reinterpret_cast<int*>(smem + g.o_colx);
+    double* atab = reinterpret_cast<double*>(smem + g.o_atab);
 
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -374,6 +381,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
 
     for (int i = tid; i < g.GH; i += NT) rowy[i] = reflect101(y0 - R + i, h);
     for (int i = tid; i < g.GW; i += NT) colx[i] = 3 * (min(max(reflect101(gx0 + i, w), cx0), cx1 - 1) - cx0);
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
     __syncthreads();
 
     // background of the wave's 8 rows x 64 columns -> registers; keep bytes likewise
@@ -587,7 +595,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
             if constexpr (NT == 512) asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
             asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
             if (!(skip & 2))
-                chain_rows<KC, PLANES, INIT, KEEP, TAIL>(a, Hs + b * (g.H_bytes / 2), g, bg, wvf, ln, x0f, y0f, f, ccf,
+                chain_rows<KC, PLANES, INIT, KEEP, TAIL>(a, Hs + b * (g.H_bytes / 2), atab, g, bg, wvf, ln, x0f, y0f, f, ccf,
                                                          init0 && t == t0, colbits, fl);
             // column-major bit tile: word c of the tile = column c, bit r = row r; this wave
             // owns byte wv of every column word
@@ -620,6 +628,243 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_pix5: the 5x5 steady-state chain (the bench configuration, and every k = 5
+// run without planes) with gray computed where the frame is loaded.
+//
+// k_pix stages each frame's raw BGR tile in LDS and then converts it: every raw
+// byte crosses LDS twice (a 16-B store, three 4-B reads per quad at a 12-B lane
+// stride -- the gray stage's bank conflicts) and the 18 gray quads of a row are
+// recomputed by the lanes that own the horizontal taps, so 24 wave-iterations of
+// gray + taps cover 68 x 18 quad jobs.  Here:
+//   gray  : a thread loads whole pixel quads (12 B, global_load_dwordx3) straight
+//           into registers, two frames ahead, and turns them into one gray dword
+//           (gray4) stored to LDS: 1224 quad jobs (68 rows x 18 quads) per frame;
+//   taps  : 1088 jobs (68 rows x 16 quads) read three gray dwords each and store
+//           the quad's four horizontal sums (u16) row-major, as k_pix does;
+//   chain : k_pix's chain_rows on the 8 rows of each wave, unchanged.
+// The image border: rows come from reflect101 source rows; a gray quad left of
+// column 0 or right of the last column is never loaded, the taps rebuild the one
+// quad just outside the image from the mirrored quad beside it (REFLECT_101).
+// Needs w % 4 == 0 and w >= 8 (4-B aligned quads, one real quad each side);
+// one barrier per frame as in k_pix.
+constexpr int P5_GH = TS + 4;            // gray rows y0-2 .. y0+65
+constexpr int P5_GQ = 18;                // gray quads per row: columns x0-4 .. x0+67
+constexpr int P5_NG = P5_GH * P5_GQ;     // gray jobs per frame
+constexpr int P5_GJ = (P5_NG + NT - 1) / NT;
+constexpr int P5_NH = P5_GH * (TS / 4);  // tap jobs per frame
+constexpr int P5_HJ = (P5_NH + NT - 1) / NT;
+// the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
+constexpr int P5_GLASTW = (P5_NG - (P5_GJ - 1) * NT + 63) / 64;  // 4 of 8
+constexpr int P5_HLASTW = (P5_NH - (P5_HJ - 1) * NT + 63) / 64;  // 1 of 8
+constexpr int P5_GBUF = P5_NG + 64;      // + a pad slot per lane for the idle jobs' stores (branch-free)
+constexpr int P5_HROW = TS;              // u16 per H row
+constexpr int P5_HBUF = (P5_GH + 1) * P5_HROW;  // + the pad row idle tap jobs store to
+constexpr int p5_lds_bytes() { return 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2 + 256 * 8; }
+
+struct P5Raw {
+    uint32_t v[P5_GJ][3];
+};
+
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int KC = 5, R = 2;
+    uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][P5_GBUF]
+    uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * P5_GBUF * 4);          // [2][P5_HBUF]
+    double* atab = reinterpret_cast<double*>(smem + 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2);
+    const int tid = threadIdx.x, ln = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int s = blockIdx.y;
+    const int ti = swizzle_tile(blockIdx.x, a.ntiles);
+    const int h = a.h, w = a.w, S = a.S;
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const int x0 = tx * TS, y0 = ty * TS;
+    const size_t plane = (size_t)h * w;
+    const size_t fbytes = plane * 3;
+    const bool hk = a.has_keep[s] != 0;
+    const uint8_t* keep = a.keep + (size_t)s * plane;
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+
+    // ---- per-thread job plans (frame invariant)
+    uint32_t goff[P5_GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
+    uint32_t gdst[P5_GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
+#pragma unroll
+    for (int i = 0; i < P5_GJ; i++) {
+        const int j = tid + NT * i;
+        const int gr = j / P5_GQ, gq = j - gr * P5_GQ;
+        const int x = x0 - 4 + 4 * gq;
+        const bool live = j < P5_NG && x >= 0 && x + 4 <= w;
+        const int y = reflect101(y0 - R + gr, h);
+        goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
+        gdst[i] = j < P5_NG ? (uint32_t)j : (uint32_t)(P5_NG + ln);
+    }
+    uint32_t hsrc[P5_HJ], hdst[P5_HJ];
+#pragma unroll
+    for (int i = 0; i < P5_HJ; i++) {
+        const int j = tid + NT * i;
+        const bool live = j < P5_NH;
+        const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
+        hsrc[i] = (uint32_t)(hr * P5_GQ + hq);
+        hdst[i] = (uint32_t)((live ? hr : P5_GH) * P5_HROW + 4 * hq);
+    }
+    // REFLECT_101 quads: left of column 0 (tile x0 = 0, tap quad 0 reads gray quad 0 = columns -4..-1:
+    // bytes 2, 3 = gray(2), gray(1) from quad 1) and the quad starting at column w (bytes 0, 1 =
+    // gray(w-2), gray(w-3) from the quad before it); further quads feed only columns past the image
+    const bool edge_tile = x0 == 0 || x0 + TS + 4 > w;  // workgroup-uniform
+    const int vq = (w - x0 + 4) / 4;  // gray quad index of the quad starting at column w
+    uint32_t hfix[P5_HJ];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
+#pragma unroll
+    for (int i = 0; i < P5_HJ; i++) {
+        const int hq = (int)(hsrc[i] % P5_GQ);
+        hfix[i] = (x0 == 0 && hq == 0 ? 1u : 0u) | (hq + 1 == vq ? 2u : 0u) | (hq + 2 == vq ? 4u : 0u);
+    }
+
+    // background of the wave's 8 rows x 64 columns -> registers (as k_pix)
+    double bg[RPWV];
+    ChainCtx cc;
+    {
+        const double* bgi = a.bg_in + (size_t)s * plane;
+        const int x = x0 + ln;
+        cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
+        cc.rowvalid = 0;
+        cc.keep_lo = cc.keep_hi = 0;
+        cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;
+#pragma unroll
+        for (int j = 0; j < RPWV; j++) {
+            const int y = y0 + RPWV * wv + j;
+            const bool in = x < w && y < h;
+            if (y < h) cc.rowvalid |= 1u << j;
+            bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
+            const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
+            if (j < 4) cc.keep_lo |= kb << (8 * j);
+            else cc.keep_hi |= kb << (8 * (j - 4));
+        }
+        const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
+        cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
+        cc.tbmask = x < w ? cc.rowvalid : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
+    asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
+
+    uint32_t cpk[2];
+    cpk[0] = tap4<KC>(0);
+    cpk[1] = tap4<KC>(1);
+    P5Raw rw;
+    auto load = [&](size_t f) __attribute__((always_inline)) {
+        const uint8_t* src = a.src + f * fbytes;
+#pragma unroll
+        for (int i = 0; i < P5_GJ; i++) {
+            if (i == P5_GJ - 1 && wv >= P5_GLASTW) break;
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(src + goff[i]);
+            rw.v[i][0] = p[0];
+            rw.v[i][1] = p[1];
+            rw.v[i][2] = p[2];
+        }
+    };
+    auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < P5_GJ; i++) {
+            if (i == P5_GJ - 1 && wv >= P5_GLASTW) break;
+            gb[gdst[i]] = gray4(rw.v[i][0], rw.v[i][1], rw.v[i][2]);
+        }
+    };
+    auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < P5_HJ; i++) {
+            if (i == P5_HJ - 1 && wv >= P5_HLASTW) break;
+            // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
+            uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
+            if (edge_tile) {
+                if (hfix[i] & 1) qv[0] = __builtin_amdgcn_perm(qv[1], qv[1], 0x01020000u);
+                if (hfix[i] & 2) qv[1] = __builtin_amdgcn_perm(qv[0], qv[0], 0x00000102u);
+                if (hfix[i] & 4) qv[2] = __builtin_amdgcn_perm(qv[1], qv[1], 0x00000102u);
+            }
+            // outputs x0+4q+k, k = 0..3: taps over gray columns x0+4q+k-2 .. +2 = bytes k+2 .. k+6 of qv
+            const uint32_t h0 = htap<0, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h1 = htap<1, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h2 = htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h3 = htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
+            *reinterpret_cast<uint2*>(Hb + hdst[i]) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+        }
+    };
+    const Geo g(R);
+    const int t0 = a.t_begin, t1 = a.t_end;
+#ifndef FM_P5_ORDER
+#define FM_P5_ORDER 1
+#endif
+    // profiling-only stage ablation (dev build, FM_DEBUG_SKIP; results invalid): 1 gray, 2 chain,
+    // 4 loads, 8 taps; 0 in normal use
+    const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
+#if FM_P5_ORDER == 0
+    // gray of frame t+1 before the frame's barrier, taps after it
+    load((size_t)t0 * S + s);
+    __syncthreads();  // atab
+    gray_stage(gray);
+    if (t0 + 1 < t1) load((size_t)(t0 + 1) * S + s);
+    lds_barrier();
+    tap_stage(gray, Hs);
+#else
+    // all work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame t+3
+    // into the registers gray(t+2) just consumed (one iteration in flight)
+    load((size_t)t0 * S + s);
+    gray_stage(gray);
+    if (t0 + 1 < t1) load((size_t)(t0 + 1) * S + s);
+    __syncthreads();  // atab, gray(t0)
+    tap_stage(gray, Hs);
+    if (t0 + 1 < t1) {
+        gray_stage(gray + P5_GBUF);
+        if (t0 + 2 < t1) load((size_t)(t0 + 2) * S + s);
+    }
+#endif
+
+    auto frame_loop = [&](auto keepc, auto tailc, const ChainCtx ccv) __attribute__((always_inline)) {
+        constexpr bool KEEP = decltype(keepc)::value != 0, TAIL = decltype(tailc)::value != 0;
+        for (int t = t0; t < t1; t++) {
+            const int b = (t - t0) & 1;
+            const size_t f = (size_t)t * S + s;
+#if FM_P5_ORDER == 0
+            if (t + 1 < t1) {
+                gray_stage(gray + (b ^ 1) * P5_GBUF);
+                if (t + 2 < t1) load(f + 2 * S);
+            }
+#endif
+            lds_barrier();
+            uint32_t colbits = 0, fl = 0;
+            ChainCtx ccf = ccv;
+            ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+            int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv;
+            asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+            // chain_rows indexes H as [row][RSH = 64]: the same row-major u16 layout
+            if (!(skip & 2))
+                chain_rows<KC, false, false, KEEP, TAIL>(a, Hs + b * P5_HBUF, atab, g, bg, wvf, ln, x0f, y0f, f, ccf,
+                                                         false, colbits, fl);
+            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
+#if FM_P5_ORDER != 0
+            if (t + 2 < t1) {
+                if (!(skip & 1)) gray_stage(gray + b * P5_GBUF);
+                if (t + 3 < t1 && !(skip & 4)) load(f + 3 * S);
+            }
+#endif
+        }
+    };
+    if (!cc.vec) frame_loop(IntC<1>{}, IntC<1>{}, cc);
+    else if (cc.hk) frame_loop(IntC<1>{}, IntC<0>{}, cc);
+    else frame_loop(IntC<0>{}, IntC<0>{}, cc);
+
+    double* bgo = a.bg_out + (size_t)s * plane;
+    const int x = x0 + ln;
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) {
+        const int y = y0 + RPWV * wv + j;
+        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+    }
+}
+
 }  // namespace px
 
 int pix_lds_bytes(int ksize) { return px::Geo(ksize >> 1).bytes; }
@@ -642,6 +887,11 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
                   : a.ksize == 21 ? taps_match<21>(a) : false;
     if (!ok) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
+    if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
+        px::p5_lds_bytes() <= 64 * 1024) {
+        hipLaunchKernelGGL(px::k_pix5, grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        return hipGetLastError();
+    }
 #define FM_PIX_LAUNCH(K, P, I)                                                                                  \
     do {                                                                                                        \
         (void)hipFuncSetAttribute((const void*)px::k_pix<K, P, I>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
