@@ -52,7 +52,6 @@ struct BatchSlot {
     int32_t* d_regrep = nullptr;    // [F][ntiles] empty tile -> region representative
     int32_t* d_ncr = nullptr;       // [F][2]
     int32_t* d_heavy = nullptr;     // [F * ntiles] heavy-tile list
-    uint8_t* d_hscratch = nullptr;  // [nheavy][kHeavyScratch] heavy-tile labelling scratch
     int32_t* d_count = nullptr;     // [2F+2]
     int32_t* h_count = nullptr;     // pinned [F]
     int32_t* h_overflow = nullptr;  // pinned [F]
@@ -104,7 +103,7 @@ struct fm_ctx {
     size_t rec_all_cap = 0;
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
-    int ntx = 0, nty = 0, ntiles = 0, nnodes = 0, nheavy = 0;  // nnodes, nheavy: per batch slot
+    int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;  // nnodes: per batch slot
     int nquota = 0;                                             // nodes of each frame's quota
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
     float *d_xwt = nullptr, *d_ywt = nullptr;
@@ -516,7 +515,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         const size_t nn = tf + tf * kNodesPerTileFrame + std::max(tf * kNodesShared, (size_t)c->ntiles * kTileMaxRuns);
         if (nn >= (size_t)INT32_MAX) return fail(nullptr, FM_ENOTSUP, "batch too large for 32-bit node ids (%zu)", nn);
         c->nnodes = (int)nn;
-        c->nheavy = kHeavyWaves;
     }
     for (int i = 0; i < c->nslots; i++) {
         BatchSlot& b = c->slots[i];
@@ -524,8 +522,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if ((rc = dalloc(cp, &b.d_count, 3 * frames + 2))) return rc;
         if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
         if (c->use_fused) {
-            if ((rc = dalloc(cp, &b.d_hscratch, (size_t)c->nheavy * kHeavyScratch)) ||
-                (rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) ||
+            if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_tiles, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_tflag, frames * c->ntiles * 8)) || (rc = dalloc(cp, &b.d_candf, frames * c->ntiles)) ||
                 (rc = dalloc(cp, &b.d_clist, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_rlist, frames * c->ntiles)) ||
@@ -629,7 +626,7 @@ void fm_destroy(fm_ctx* c) {
         }
     for (auto& b : c->slots) {
         dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
-        dfree(b.d_nodes); dfree(b.d_hscratch); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
+        dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
         dfree(b.d_clist); dfree(b.d_rlist); dfree(b.d_regrep); dfree(b.d_ncr);
         for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init, (void*)b.h_stats})
             if (hp) (void)hipHostFree(hp);
@@ -775,9 +772,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.ncr = B.d_ncr;
         fa.nodes = B.d_nodes;
         fa.count = B.d_count;
-        fa.hscratch = B.d_hscratch;
         fa.heavy = B.d_heavy;
-        fa.nheavy = c->nheavy;
         fa.rec = B.d_rec;
         fa.h_count = B.dh_count;
         fa.h_overflow = B.dh_overflow;

@@ -22,7 +22,7 @@
 //                (fm.py:266), run-length labelling in LDS (256 runs), a tile
 //                record (edge labels) and one node per component.
 //   k_tile_heavy tiles with more runs (a dense texture of blobs): persistent waves,
-//                global-memory scratch of kTileMaxRuns runs each, no LDS.
+//                kTileMaxRuns runs each in 46 KB of LDS.
 //   k_merge      one wave per candidate: unions along its edges with candidate
 //                neighbours (right / below) and empty regions (all sides).
 //   k_fold       one wave per candidate tile (lanes = its components) or region:
@@ -40,9 +40,15 @@ namespace cc {
 
 constexpr int TS = 64;
 constexpr int MAXR = kTileMaxRuns;
-constexpr int LIGHT = 256;      // runs held by the light pass
+#ifndef FM_CCL_LIGHT
+#define FM_CCL_LIGHT 256
+#endif
+constexpr int LIGHT = FM_CCL_LIGHT;  // runs held by the light pass
 constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k_merge
-constexpr int GW = 32;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
+#ifndef FM_CCL_GW
+#define FM_CCL_GW 8  // measured: 8 > 16 > 32 > 4 (r02: 266k vs 262k vs 251k vs 257k frames/s at the bench default)
+#endif
+constexpr int GW = FM_CCL_GW;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
 constexpr int RG = 512;         // k_regions threads
 constexpr int MAX_REGION_TILES = 8192;
 constexpr uint32_t REF_OUTER = 0x80000000u;
@@ -230,27 +236,6 @@ __device__ __forceinline__ int run_at(int base, uint64_t starts, int p) {
         if (a.dbg_ts && ln == 0) a.dbg_ts[((size_t)f * a.ntiles + ti) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 
-// Scratch access: all in LDS for the light pass; for a heavy tile the union-find parents
-// and the run pairs (hit every hook/shortcut round) stay in LDS, the per-run arrays live
-// in global memory (G: agent-scope loads of everything updated by atomics, so no load
-// can see a stale L1 line; plain stores are made visible to the other lanes by waiting
-// on vmcnt)
-template <bool G>
-__device__ __forceinline__ int sld(int* p) {
-    if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <bool G>
-__device__ __forceinline__ int srd(const int* p) {
-    if constexpr (G) return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-template <bool G>
-__device__ __forceinline__ void sfence() {
-    if constexpr (G) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
 enum : int { TCCL_OK = 0, TCCL_RUNS = 1, TCCL_NODES = 2 };
 
 // the tile's node ids: n consecutive ids from its frame's quota (one counter per frame, so
@@ -274,7 +259,7 @@ __device__ __forceinline__ int take_nodes(const FusedArgs& a, size_t f, int n, i
 }
 
 // TCCL_RUNS (nothing written) if the tile has more than CAP runs
-template <int CAP, bool G>
+template <int CAP>
 __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc) {
     int* par = sc.par;
     int* amin = sc.amin;
@@ -394,7 +379,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             id2++;
         }
     }
-    sfence<G>();
+    lds_fence();
     FM_STAMP(5);
     // Shiloach-Vishkin style rounds: hook the larger of the two parents under the
     // smaller (atomicMin, so parents only decrease), then shortcut par[i] = par[par[i]];
@@ -410,7 +395,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
                 ch = true;
             }
         }
-        sfence<G>();
+        lds_fence();
         for (int i = ln; i < total; i += 64) {
             const int pi = lload(&par[i]);
             const int ppi = lload(&par[pi]);
@@ -419,7 +404,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
                 ch = true;
             }
         }
-        sfence<G>();
+        lds_fence();
         if (__ballot(ch) == 0) break;
     }
     FM_STAMP(6);
@@ -435,7 +420,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             }
         }
     }
-    sfence<G>();
+    lds_fence();
     FM_STAMP(7);
     // ordinals of the roots in raster order
     int myr = 0;
@@ -458,7 +443,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
         for (int i = base; i < base + nr; i++)
             if ((par[i]) == i) ord[i] = (uint16_t)kk++;
     }
-    sfence<G>();
+    lds_fence();
     if (FM_OOB(a, (long long)nb + nroots <= (long long)a.nnodes, 3)) return TCCL_NODES;
     NodeRec* NR = a.nodes + nb;
     for (int i = base; i < base + nr; i++) {
@@ -477,11 +462,11 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             else ref = (uint32_t)ord[(par[i - 1])];  // the background run left of this run
             nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
             nrec.flags = 1u;
-            nrec.minx = x0 + srd<G>(&amin[i]);
-            nrec.maxx = x0 + srd<G>(&amax[i]);
-            nrec.maxy = y0 + srd<G>(&ay[i]);
+            nrec.minx = x0 + amin[i];
+            nrec.maxx = x0 + amax[i];
+            nrec.maxy = y0 + ay[i];
         } else {
-            nrec.flags = srd<G>(&amin[i]) ? 2u : 0u;
+            nrec.flags = amin[i] ? 2u : 0u;
         }
         NR[ord[i]] = nrec;
     }
@@ -594,23 +579,6 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     }
 }
 
-// global part of heavy-tile slot i's scratch (kHeavyScratch bytes); par, pairs and rb are LDS
-__device__ __forceinline__ Scratch heavy_scratch(const FusedArgs& a, int i, int* par, uint32_t* pairs, int* rb) {
-    uint8_t* p = a.hscratch + (size_t)i * kHeavyScratch;
-    Scratch sc;
-    sc.par = par;
-    sc.pairs = pairs;
-    sc.rb = rb;
-    sc.amin = (int*)p;
-    sc.amax = sc.amin + MAXR;
-    sc.ay = sc.amax + MAXR;
-    sc.ord = (uint16_t*)(sc.ay + MAXR);
-    sc.rx0 = (uint8_t*)(sc.ord + MAXR);
-    sc.rx1 = sc.rx0 + MAXR;
-    sc.rf = sc.rx1 + MAXR;
-    return sc;
-}
-static_assert(4 * 3 * MAXR + 2 * MAXR + 3 * MAXR <= kHeavyScratch, "heavy scratch too small");
 
 // grid (GW, F); each wave labels candidates of the frame's list with a stride, in LDS
 // (LIGHT runs); a tile with more runs (a dense texture of small blobs) goes to the
@@ -641,7 +609,7 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
         }
         FM_STAMP(2);
         if (a.dbg_skip & 64) continue;  // profiling ablation (results invalid)
-        const int r = tile_ccl<LIGHT, false>(a, f, ti, ln, m, sc);
+        const int r = tile_ccl<LIGHT>(a, f, ti, ln, m, sc);
         if (ln == 0) {
             if (r == TCCL_RUNS) {
                 const int hi = atomicAdd(&a.count[2 * F + 1], 1);
@@ -652,25 +620,28 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
     }
 }
 
-// heavy pass: NHW persistent waves drain the heavy list (kTileMaxRuns runs per tile), union-
-// find parents and run pairs in 19.5 KB of LDS (small enough to sit beside the pixel
-// kernel's workgroups), the other per-run arrays in a global scratch slot per wave
+// heavy pass: NHW persistent waves drain the heavy list (kTileMaxRuns runs per tile), all scratch
+// in 46 KB of LDS: beside k_pix5's two ~30 KB workgroups a CU has room for it (measured 3.5 %
+// faster end to end than keeping the per-run arrays in global memory, which k_pix's ~52 KB
+// workgroups needed)
 constexpr int NHW = kHeavyWaves;
 __global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
-    __shared__ int par[MAXR];
+    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
+    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
+    __shared__ uint16_t ord[MAXR];
     __shared__ uint32_t pairs[2 * MAXR];
     __shared__ int rb[68];
     const size_t F = (size_t)a.T * a.S;
     const int n = a.count[2 * F + 1];
     const int ln = threadIdx.x;
     if (FM_OOB(a, n <= (int)(F * a.ntiles), 2)) return;
+    const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         if (FM_OOB(a, item >= 0 && item < (int)(F * a.ntiles), 4)) continue;
         const size_t f = item / a.ntiles;
         const int ti = (int)(item - (long long)f * a.ntiles);
-        const int r = tile_ccl<MAXR, true>(a, f, ti, ln, a.dbits[(f * a.ntiles + ti) * 64 + ln],
-                                           heavy_scratch(a, blockIdx.x, par, pairs, rb));
+        const int r = tile_ccl<MAXR>(a, f, ti, ln, a.dbits[(f * a.ntiles + ti) * 64 + ln], sc);
         if (r != TCCL_OK && ln == 0) a.count[F + f] = 1;
     }
 }

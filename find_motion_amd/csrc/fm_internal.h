@@ -37,8 +37,7 @@ inline const char* dev_env(const char* name) {
 constexpr int kMaxK = 255;        // largest Gaussian size handled by the tiled kernel
 constexpr int kCclBlock = 32;     // CCL block edge (pixels)
 constexpr int kTileMaxRuns = 1600; // runs per 64x64 tile of a dilated mask (<= 24 per row => 1536)
-constexpr int kHeavyScratch = 27264; // bytes of global labelling scratch per heavy-pass wave (fm_ccl.hip)
-constexpr int kHeavyWaves = 64;       // k_tile_heavy persistent waves, one scratch slot each
+constexpr int kHeavyWaves = 64;       // k_tile_heavy persistent waves (fm_ccl.hip)
 constexpr int kNodesPerTileFrame = 32; // union-find nodes each frame owns per tile (its quota)
 constexpr int kNodesShared = 16;       // + a shared overflow pool of this many per tile-frame (at least one
                                        //   worst-case frame), taken from only by frames past their quota
@@ -134,7 +133,6 @@ struct FusedArgs {
     int32_t* h_stats;            // mapped host [2]: nodes taken from the shared pool, heavy tiles (written by
                                  // k_counts; diagnostics)
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
-    uint8_t* hscratch;           // [nheavy][kHeavyScratch] k_tile_heavy's labelling scratch
     int32_t* rec;                // [F][cap][5]
     int32_t* h_count;            // mapped host [F]: external contours per frame (written by k_fold_emit)
     int32_t* h_overflow;         // mapped host [F]: frame needs the pixel-level fallback
@@ -142,7 +140,6 @@ struct FusedArgs {
     int t_begin, t_end;          // k_pix: frames of the batch this launch processes
     int ntx, nty, ntiles, nnodes, cap, cvt_simd;
     int nquota;                  // nodes per frame quota
-    int nheavy;                  // heavy-tile scratch slots (= k_tile_heavy's waves)
     int tflag_waves;             // words per tile-frame in tflag: 1 (k_fused, atomicOr) or 8 (k_pix, one per wave)
     int dbg_skip;                // profiling-only stage ablation (FM_DEBUG_SKIP); 0 in normal use
     uint64_t* dbg_ts;            // profiling-only s_memtime stamps [F][ntiles][16] (FM_TS); nullptr in normal use
