@@ -162,6 +162,32 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+// the value of lane ln ^ J, without LDS: v_permlane32_swap / v_permlane16_swap for 32 / 16, DPP
+// row_ror:8 for 8, row_half_mirror then a reversed quad_perm for 4, quad_perm for 2 and 1
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v, int ln) {
+    if constexpr (J == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return ln < 32 ? r[1] : r[0];
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (ln & 16) ? r[0] : r[1];
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);
+    } else if constexpr (J == 4) {
+        const int m = __builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);
+        return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, true);
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
+    } else {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+    }
+}
+template <int J>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v, int ln) {
+    return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32), ln) << 32) | lane_xor<J>((uint32_t)v, ln);
+}
+
 // 64x64 bit transpose across the wave: lane k holds word k; afterwards lane r holds the
 // word whose bit c is bit r of the old word c
 __device__ __forceinline__ uint64_t transpose64(uint64_t w, int ln) {
@@ -170,7 +196,8 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t w, int ln) {
 #pragma unroll
     for (int s = 0; s < 6; s++) {
         const int j = 32 >> s;
-        const uint64_t p = shfl64(w, ln ^ j);
+        const uint64_t p = j == 32 ? lane_xor64<32>(w, ln) : j == 16 ? lane_xor64<16>(w, ln) : j == 8 ? lane_xor64<8>(w, ln)
+                         : j == 4 ? lane_xor64<4>(w, ln) : j == 2 ? lane_xor64<2>(w, ln) : lane_xor64<1>(w, ln);
         if (ln & j) w ^= ((p >> j) ^ w) & masks[s];
         else w ^= (((w >> j) ^ p) & masks[s]) << j;
     }
@@ -182,12 +209,13 @@ __device__ __forceinline__ uint64_t dilate_tile(const FusedArgs& a, size_t f, in
     const int tx = ti % a.ntx, ty = ti / a.ntx;
     const uint64_t* B = a.bits + f * (size_t)a.ntiles * 64;
     const bool hl = tx > 0, hr = tx + 1 < a.ntx;
+    // columns of the neighbours: lanes 62, 63 hold the left tile's columns 62, 63, lanes 0, 1 the
+    // right tile's columns 0, 1 (every lane loads its side column unconditionally -- its own tile's
+    // where there is none -- so all six loads are in flight together)
+    const int st = (ln >= 62 && hl) ? ti - 1 : (ln <= 1 && hr) ? ti + 1 : ti;
     const uint64_t v = vdil(B, a, ti, ty, ln);
-    // columns of the neighbours: lanes 62, 63 hold the left tile's columns 62, 63,
-    // lanes 0, 1 the right tile's columns 0, 1
-    uint64_t e = 0;
-    if (ln >= 62 && hl) e = vdil(B, a, ti - 1, ty, ln);
-    if (ln <= 1 && hr) e = vdil(B, a, ti + 1, ty, ln);
+    uint64_t e = vdil(B, a, st, ty, ln);
+    if (st == ti) e = 0;
     // neighbour columns by DPP wave shifts (wave_shr:1: lane i <- i-1; wave_shl:1: lane i <- i+1),
     // the four neighbour-tile columns by readlane
     const uint64_t vm1 = dpp64<0x138>(v), vm2 = dpp64<0x138>(vm1);
