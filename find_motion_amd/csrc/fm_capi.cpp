@@ -475,6 +475,12 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if (dev_env("FM_PIX_PRIO_OFF")) hi = lo;
         HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
     }
+    int ccl_qmode = 0;
+    if (const char* e = dev_env("FM_CCL_QMODE")) ccl_qmode = std::atoi(e);
+    c->nccl = 2;
+    if (const char* e = dev_env("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
+    if (ccl_qmode == 2)  // contour streams take hardware queues before the rarely used aux / input streams
+        for (int i = 0; i < c->nccl; i++) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
     if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
@@ -496,8 +502,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     // contour-pass streams shared round-robin by the slots: few streams, because the
     // runtime multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order,
     // and a contour kernel queued ahead of a pixel kernel on a shared queue stalls it
-    c->nccl = 2;
-    if (const char* e = dev_env("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
     for (int i = 0; i < 2; i++)
         if ((rc = dalloc(cp, &c->d_bg[i], S * c->work_plane))) return rc;
     if ((rc = dalloc(cp, &c->d_keep, S * c->work_plane)) || (rc = dalloc(cp, &c->d_has_keep, S)) ||
@@ -544,7 +548,15 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_overflow, b.h_overflow, 0));
         if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * 8 * sizeof(uint32_t)));
         HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
-        if (i < c->nccl) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
+        if (i < c->nccl && ccl_qmode != 2) {
+            if (ccl_qmode == 1) {
+                int lo = 0, hi = 0;
+                HIP_TRY(cp, hipDeviceGetStreamPriorityRange(&lo, &hi));
+                HIP_TRY(cp, hipStreamCreateWithPriority(&c->ccl_streams[i], hipStreamNonBlocking, hi));
+            } else {
+                HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
+            }
+        }
         b.ccl_stream = c->ccl_streams[i % c->nccl];
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));

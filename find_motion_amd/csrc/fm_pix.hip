@@ -663,8 +663,9 @@ constexpr int P5_HROW = TS;              // u16 per H row
 constexpr int P5_HBUF = (P5_GH + 1) * P5_HROW;  // + the pad row idle tap jobs store to
 constexpr int p5_lds_bytes() { return 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2 + 256 * 8; }
 
+typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
 struct P5Raw {
-    uint32_t v[P5_GJ][3];
+    u32x3_t v[P5_GJ];  // one 96-bit value per job: one register triple the allocator keeps whole
 };
 
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
@@ -752,22 +753,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     cpk[0] = tap4<KC>(0);
     cpk[1] = tap4<KC>(1);
     P5Raw rw;
+    // Every wave issues every job's load, idle jobs included (they read the frame's first
+    // 12 B): a load under a branch makes its registers a phi of the loaded and the old
+    // value, and the copies the compiler then inserts at the loop back-edge wait for the
+    // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const uint8_t* src = a.src + f * fbytes;
 #pragma unroll
         for (int i = 0; i < P5_GJ; i++) {
-            if (i == P5_GJ - 1 && wv >= P5_GLASTW) break;
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(src + goff[i]);
-            rw.v[i][0] = p[0];
-            rw.v[i][1] = p[1];
-            rw.v[i][2] = p[2];
+            __builtin_memcpy(&rw.v[i], src + goff[i], 12);  // global_load_dwordx3 (4-B aligned)
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < P5_GJ; i++) {
             if (i == P5_GJ - 1 && wv >= P5_GLASTW) break;
-            gb[gdst[i]] = gray4(rw.v[i][0], rw.v[i][1], rw.v[i][2]);
+            gb[gdst[i]] = gray4(rw.v[i].x, rw.v[i].y, rw.v[i].z);
         }
     };
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
@@ -791,70 +792,52 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     };
     const Geo g(R);
     const int t0 = a.t_begin, t1 = a.t_end;
-#ifndef FM_P5_ORDER
-#define FM_P5_ORDER 1
-#endif
     // profiling-only stage ablation (dev build, FM_DEBUG_SKIP; results invalid): 1 gray, 2 chain,
     // 4 loads, 8 taps; 0 in normal use
     const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
-#if FM_P5_ORDER == 0
-    // gray of frame t+1 before the frame's barrier, taps after it
-    load((size_t)t0 * S + s);
-    __syncthreads();  // atab
-    gray_stage(gray);
-    if (t0 + 1 < t1) load((size_t)(t0 + 1) * S + s);
-    lds_barrier();
-    tap_stage(gray, Hs);
-#else
-    // all work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame t+3
-    // into the registers gray(t+2) just consumed (one iteration in flight)
+    // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
+    // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
+    // unconditional, frame indices clamped to the batch (see load).
     load((size_t)t0 * S + s);
     gray_stage(gray);
-    if (t0 + 1 < t1) load((size_t)(t0 + 1) * S + s);
+    load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
-    if (t0 + 1 < t1) {
-        gray_stage(gray + P5_GBUF);
-        if (t0 + 2 < t1) load((size_t)(t0 + 2) * S + s);
-    }
-#endif
+    if (t0 + 1 < t1) gray_stage(gray + P5_GBUF);
+    load((size_t)min(t0 + 2, t1 - 1) * S + s);
 
-    auto frame_loop = [&](auto keepc, auto tailc, const ChainCtx ccv) __attribute__((always_inline)) {
-        constexpr bool KEEP = decltype(keepc)::value != 0, TAIL = decltype(tailc)::value != 0;
-        for (int t = t0; t < t1; t++) {
-            const int b = (t - t0) & 1;
-            const size_t f = (size_t)t * S + s;
-#if FM_P5_ORDER == 0
-            if (t + 1 < t1) {
-                gray_stage(gray + (b ^ 1) * P5_GBUF);
-                if (t + 2 < t1) load(f + 2 * S);
-            }
-#endif
-            lds_barrier();
-            uint32_t colbits = 0, fl = 0;
-            ChainCtx ccf = ccv;
-            ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
-            int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv;
-            asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-            // chain_rows indexes H as [row][RSH = 64]: the same row-major u16 layout
-            if (!(skip & 2))
-                chain_rows<KC, false, false, KEEP, TAIL>(a, Hs + b * P5_HBUF, atab, g, bg, wvf, ln, x0f, y0f, f, ccf,
-                                                         false, colbits, fl);
-            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
-            if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
-#if FM_P5_ORDER != 0
-            if (t + 2 < t1) {
-                if (!(skip & 1)) gray_stage(gray + b * P5_GBUF);
-                if (t + 3 < t1 && !(skip & 4)) load(f + 3 * S);
-            }
-#endif
+    // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
+    // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
+    // Three loop copies would give the in-flight loads different registers in each, and the
+    // wait pass would then wait for them at the top of every frame.
+    const int var0 = __builtin_amdgcn_readfirstlane(!cc.vec ? 2 : cc.hk ? 1 : 0);
+    for (int t = t0; t < t1; t++) {
+        const int b = (t - t0) & 1;
+        const size_t f = (size_t)t * S + s;
+        lds_barrier();
+        uint32_t colbits = 0, fl = 0;
+        ChainCtx ccf = cc;
+        ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+        int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
+        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf), "+s"(var));
+        asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+        // chain_rows indexes H as [row][RSH = 64]: the same row-major u16 layout
+        const uint16_t* Hb = Hs + b * P5_HBUF;
+        if (!(skip & 2)) {
+            if (var == 0)
+                chain_rows<KC, false, false, false, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+            else if (var == 1)
+                chain_rows<KC, false, false, true, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+            else
+                chain_rows<KC, false, false, true, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
         }
-    };
-    if (!cc.vec) frame_loop(IntC<1>{}, IntC<1>{}, cc);
-    else if (cc.hk) frame_loop(IntC<1>{}, IntC<0>{}, cc);
-    else frame_loop(IntC<0>{}, IntC<0>{}, cc);
+        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
+        if (t + 2 < t1 && !(skip & 1)) gray_stage(gray + b * P5_GBUF);
+        // unconditional (see load): past the batch's last frame it re-reads that frame
+        if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
+    }
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
