@@ -793,8 +793,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     const Geo g(R);
     const int t0 = a.t_begin, t1 = a.t_end;
     // profiling-only stage ablation (dev build, FM_DEBUG_SKIP; results invalid): 1 gray, 2 chain,
-    // 4 loads, 8 taps; 0 in normal use
+    // 4 loads, 8 taps.  A constant 0 in the product build: a runtime skip path around the loads or
+    // gray leaves loads unwaited on it, and the wait pass then stalls every frame on the stores
+#ifdef FM_DEV_SWITCHES
     const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
+#else
+    constexpr int skip = 0;
+#endif
     // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
     // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
     // unconditional, frame indices clamped to the batch (see load).
@@ -831,10 +836,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             else
                 chain_rows<KC, false, false, true, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
         }
+        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
+        // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
+        // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
+        // makes every frame wait for the stores below before the next loads
+        if (!(skip & 1)) gray_stage(gray + b * P5_GBUF);
+        // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
+        // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
+        // the prefetch would be waited for with it
         reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
         if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
-        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
-        if (t + 2 < t1 && !(skip & 1)) gray_stage(gray + b * P5_GBUF);
         // unconditional (see load): past the batch's last frame it re-reads that frame
         if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
     }
