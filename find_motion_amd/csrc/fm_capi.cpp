@@ -475,9 +475,15 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if (dev_env("FM_PIX_PRIO_OFF")) hi = lo;
         HIP_TRY(cp, hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, hi));
     }
-    int ccl_qmode = 0;
+#ifndef FM_CCL_QMODE_DEFAULT
+#define FM_CCL_QMODE_DEFAULT 2  // contour streams take their own hardware queues (A/B: +3 %)
+#endif
+#ifndef FM_NCCL_DEFAULT
+#define FM_NCCL_DEFAULT 3
+#endif
+    int ccl_qmode = FM_CCL_QMODE_DEFAULT;
     if (const char* e = dev_env("FM_CCL_QMODE")) ccl_qmode = std::atoi(e);
-    c->nccl = 2;
+    c->nccl = FM_NCCL_DEFAULT;
     if (const char* e = dev_env("FM_CCL_STREAMS")) c->nccl = std::max(1, std::min(kSlots, std::atoi(e)));
     if (ccl_qmode == 2)  // contour streams take hardware queues before the rarely used aux / input streams
         for (int i = 0; i < c->nccl; i++) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));

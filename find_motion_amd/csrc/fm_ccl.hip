@@ -50,6 +50,15 @@ constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k
 #endif
 constexpr int GW = FM_CCL_GW;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
 constexpr int RG = 512;         // k_regions threads
+#ifndef FM_CCL_PRIO
+#define FM_CCL_PRIO 2  // contour waves win issue over the pixel kernel's (A/B: +4 %)
+#endif
+#ifndef FM_HEAVY_PRIO
+#define FM_HEAVY_PRIO 3
+#endif
+#ifndef FM_MERGE_PRIO
+#define FM_MERGE_PRIO 2
+#endif
 constexpr int MAX_REGION_TILES = 8192;
 constexpr uint32_t REF_OUTER = 0x80000000u;
 constexpr uint32_t REF_EDGE = 0x40000000u;
@@ -624,6 +633,7 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
     const int nc = a.ncr[2 * f];
     const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
     if (FM_OOB(a, nc >= 0 && nc <= a.ntiles, 1)) return;
+    if (FM_CCL_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_PRIO);
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int ti = a.clist[f * a.ntiles + k];
         if (FM_OOB(a, ti >= 0 && ti < a.ntiles, 1)) continue;
@@ -653,7 +663,10 @@ __global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
 // faster end to end than keeping the per-run arrays in global memory, which k_pix's ~52 KB
 // workgroups needed)
 constexpr int NHW = kHeavyWaves;
-__global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
+#ifndef FM_HEAVY_WPE
+#define FM_HEAVY_WPE 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FM_HEAVY_WPE))) void k_tile_heavy(FusedArgs a) {
     __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
     __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
     __shared__ uint16_t ord[MAXR];
@@ -664,6 +677,7 @@ __global__ __launch_bounds__(64) void k_tile_heavy(FusedArgs a) {
     const int ln = threadIdx.x;
     if (FM_OOB(a, n <= (int)(F * a.ntiles), 2)) return;
     const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
+    if (FM_HEAVY_PRIO) __builtin_amdgcn_s_setprio(FM_HEAVY_PRIO);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         if (FM_OOB(a, item >= 0 && item < (int)(F * a.ntiles), 4)) continue;
@@ -696,6 +710,7 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     if (a.count[F + f]) return;
+    if (FM_MERGE_PRIO) __builtin_amdgcn_s_setprio(FM_MERGE_PRIO);
     const int ntx = a.ntx, nt = a.ntiles;
     const uint8_t* cf = a.candf + f * nt;
     const int32_t* rr = a.regrep + f * nt;
