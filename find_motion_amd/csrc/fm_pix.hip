@@ -795,10 +795,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     // profiling-only stage ablation (dev build, FM_DEBUG_SKIP; results invalid): 1 gray, 2 chain,
     // 4 loads, 8 taps.  A constant 0 in the product build: a runtime skip path around the loads or
     // gray leaves loads unwaited on it, and the wait pass then stalls every frame on the stores
+#ifndef FM_P5_SKIP
+#define FM_P5_SKIP 0  // compile-time stage ablation (tools/ablate_p5c.sh)
+#endif
 #ifdef FM_DEV_SWITCHES
     const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
 #else
-    constexpr int skip = 0;
+    constexpr int skip = FM_P5_SKIP;
 #endif
     // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
     // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
