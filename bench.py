@@ -49,17 +49,19 @@ def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
     return None
 
 
-def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None]:
+def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | None]:
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/traffic.json,
-    written by tools/traffic.py from FETCH_SIZE / WRITE_SIZE passes of this same workload), or None."""
+    written by tools/traffic.py from FETCH_SIZE / WRITE_SIZE passes of this same workload), and the SQ
+    counter ratios of those passes (what bounds the kernel), or None."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     if t.get("workload") != cfg["workload"] or kernel not in t.get("kernels", {}):
-        return None, None
-    return int(t["kernels"][kernel]["traffic_bytes"]), t.get("source")
+        return None, None, None
+    k = t["kernels"][kernel]
+    return int(k["traffic_bytes"]), t.get("source"), k.get("sq")
 
 
 def cpu_model() -> str:
@@ -275,12 +277,21 @@ def main() -> None:
         nbytes = algorithmic_bytes(dom, cfg)
         if nbytes is not None and avg_s > 0:
             ach = nbytes / avg_s / 1e9
-            traffic, tsrc = pmc_traffic(dom, cfg)
+            traffic, tsrc, sq = pmc_traffic(dom, cfg)
+            # "bound" is the roofline the kernel is priced against (byte/integer stencils + an f64
+            # recurrence: no contraction, no MFMA).  What actually limits it is read from the SQ
+            # counters of the committed profile: "limiter" below.
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3)}
             if traffic is not None:
                 roof["traffic_source"] = f"{tsrc}: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 16-B read correction)"
+            if sq:
+                roof["limiter"] = (f"issue and latency, not HBM bandwidth: of SQ_WAVE_CYCLES, {sq['wait_inst_any_frac']:.0%} "
+                                   f"issue stalls (SQ_WAIT_INST_ANY), {sq['wait_any_frac']:.0%} parked on s_waitcnt / the "
+                                   f"frame barrier (SQ_WAIT_ANY), {sq['active_inst_any_frac']:.0%} issuing; "
+                                   f"{sq['valu_insts'] / 1e6:.1f}M VALU, {sq['salu_insts'] / 1e6:.1f}M SALU, "
+                                   f"{sq['lds_insts'] / 1e6:.1f}M LDS wave-instructions per launch ({tsrc})")
 
     # measured device copy peak (for reference beside the spec)
     try:

@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"k_pix": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit", "k_fold": "fold", "k_emit": "emit",
+SHORT = {"k_pix": "pix", "k_pix5": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit", "k_fold": "fold", "k_emit": "emit",
          "k_regions": "regions", "k_resize_area": "resize_area", "k_pixel": "pixel"}
 
 
@@ -38,7 +38,7 @@ def main(prof, bench_log, tag):
                 if "k_pix<" in k and ", true>" in k:  # the init-frame variant is a one-off
                     continue
                 s = short(k)
-                if s and row["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+                if s:
                     acc[s][row["Counter_Name"]].append(float(row["Counter_Value"]))
     line = [l for l in open(bench_log).read().splitlines() if l.startswith("{")][-1]
     workload = json.loads(line)["config"]["workload"]
@@ -50,6 +50,20 @@ def main(prof, bench_log, tag):
         write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
         out["kernels"][k] = {"fetch_size_bytes": round(fetch), "write_size_bytes": round(write),
                              "traffic_bytes": round(2 * fetch + write), "dispatches": len(cs["FETCH_SIZE"])}
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        if m.get("SQ_WAVE_CYCLES"):
+            # what bounds the kernel, from the SQ counters of the same passes (per dispatch means):
+            # WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue stalls) + ACTIVE_INST_ANY
+            # = WAVE_CYCLES (MI355X_MICROARCH.md, rocprofv3 PMC slots)
+            wc = m["SQ_WAVE_CYCLES"]
+            out["kernels"][k]["sq"] = {
+                "wait_any_frac": round(m.get("SQ_WAIT_ANY", 0) / wc, 3),
+                "wait_inst_any_frac": round(m.get("SQ_WAIT_INST_ANY", 0) / wc, 3),
+                "active_inst_any_frac": round(m.get("SQ_ACTIVE_INST_ANY", 0) / wc, 3),
+                "valu_insts": round(m.get("SQ_INSTS_VALU", 0)), "salu_insts": round(m.get("SQ_INSTS_SALU", 0)),
+                "lds_insts": round(m.get("SQ_INSTS_LDS", 0)),
+                "lds_bank_conflict_per_active": round(m.get("SQ_LDS_BANK_CONFLICT", 0) / max(m.get("SQ_ACTIVE_INST_LDS", 1), 1), 3),
+                "waves": round(m.get("SQ_WAVES", 0))}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
