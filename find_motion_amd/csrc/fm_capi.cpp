@@ -811,6 +811,7 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
         fa.alpha = c->p.avg;
         fa.beta = 1.0 - c->p.avg;
         fa.acc_vec_end = npx - npx % 16;
+        fa.any_keep = std::any_of(c->has_keep.begin(), c->has_keep.end(), [](uint8_t k) { return k != 0; }) ? 1 : 0;
         fa.dbg_skip = c->dbg_skip;
         fa.dbg_ts = c->d_ts;
         fa.dbg_pts = c->d_pts;

@@ -147,6 +147,7 @@ struct FusedArgs {
     int32_t* dbg_err;            // mapped host word: FM_OOB violation bits (checked build only)
     double alpha, beta;
     long long acc_vec_end;
+    int any_keep;                // some stream of the context has a keep-mask (k_pix5 variant choice)
     int32_t coef[kMaxK];
 };
 

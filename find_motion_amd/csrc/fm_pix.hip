@@ -668,6 +668,11 @@ struct P5Raw {
     u32x3_t v[P5_GJ];  // one 96-bit value per job: one register triple the allocator keeps whole
 };
 
+// KEEP: some stream has a keep-mask (streams without one get all-keep bytes); TAIL: the image has
+// accumulateWeighted's scalar tail (h*w % 16 != 0), so some waves take the per-pixel test.  Fixed
+// per launch, so the common kernel has a single chain path: a per-wave 3-way branch inside the
+// frame loop made the background registers a phi and cost 8 v_mov_b64 per frame.
+template <bool KEEP, bool TAIL>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int KC = 5, R = 2;
@@ -818,7 +823,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
-    const int var0 = __builtin_amdgcn_readfirstlane(!cc.vec ? 2 : cc.hk ? 1 : 0);
+    const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
@@ -827,17 +832,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         ChainCtx ccf = cc;
         ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
         int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
-        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf), "+s"(var));
+        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+        var = __builtin_amdgcn_readfirstlane(var);
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
         // chain_rows indexes H as [row][RSH = 64]: the same row-major u16 layout
         const uint16_t* Hb = Hs + b * P5_HBUF;
         if (!(skip & 2)) {
-            if (var == 0)
-                chain_rows<KC, false, false, false, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
-            else if (var == 1)
-                chain_rows<KC, false, false, true, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+            if (!TAIL || var == 0)
+                chain_rows<KC, false, false, KEEP, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
             else
-                chain_rows<KC, false, false, true, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+                chain_rows<KC, false, false, KEEP, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
         }
         if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
         // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
@@ -886,7 +890,11 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
     dim3 grid(a.ntiles, a.S);
     if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
         px::p5_lds_bytes() <= 64 * 1024) {
-        hipLaunchKernelGGL(px::k_pix5, grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
+        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        else hipLaunchKernelGGL((px::k_pix5<false, false>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
         return hipGetLastError();
     }
 #define FM_PIX_LAUNCH(K, P, I)                                                                                  \
