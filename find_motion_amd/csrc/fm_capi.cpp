@@ -597,8 +597,9 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     if (const char* e = dev_env("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
     c->serial = dev_env("FM_SERIAL") != nullptr;
     if (dev_env("FM_PTS") && c->use_pix) {
-        if ((rc = dalloc(cp, &c->d_pts, (size_t)S * c->ntiles * 4))) return rc;
-        HIP_TRY(cp, hipMemset(c->d_pts, 0, (size_t)S * c->ntiles * 4 * sizeof(uint64_t)));
+        // [S][ntiles][4] workgroup stamps, then [S][ntiles][8 waves][4] k_pix5 phase cycles
+        if ((rc = dalloc(cp, &c->d_pts, (size_t)S * c->ntiles * 36))) return rc;
+        HIP_TRY(cp, hipMemset(c->d_pts, 0, (size_t)S * c->ntiles * 36 * sizeof(uint64_t)));
     }
     if (dev_env("FM_TS") && c->use_fused) {
         if ((rc = dalloc(cp, &c->d_ts, frames * c->ntiles * 16))) return rc;
@@ -615,7 +616,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 void fm_destroy(fm_ctx* c) {
     if (!c) return;
     if (c->d_pts) {  // profiling: per-workgroup (hw_id, xcc_id, realtime start/end, memtime start/end) of the last k_pix
-        const size_t n = (size_t)c->p.n_streams * c->ntiles * 4;
+        const size_t n = (size_t)c->p.n_streams * c->ntiles * 36;
         std::vector<uint64_t> v(n);
         if (hipDeviceSynchronize() == hipSuccess &&
             hipMemcpy(v.data(), c->d_pts, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess) {

@@ -652,11 +652,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
 constexpr int P5_GH = TS + 4;            // gray rows y0-2 .. y0+65
 constexpr int P5_GQ = 18;                // gray quads per row: columns x0-4 .. x0+67
 constexpr int P5_NG = P5_GH * P5_GQ;     // gray jobs per frame
-constexpr int P5_GJ = (P5_NG + NT - 1) / NT;
+// Gray jobs go to waves in whole wave-slots of 64 jobs.  Waves 4..7 lose issue arbitration to
+// waves 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves 0..3 spent
+// ~30 % of their cycles in the barrier), so waves 0..3 take P5_GFAST slots each and waves 4..7 the
+// rest; the partial last slot goes to wave 3.
+#ifndef FM_P5_GFAST
+#define FM_P5_GFAST 4  // (A/B: 4 >= 3 > 5)
+#endif
+constexpr int P5_GSLOTS = (P5_NG + 63) / 64;                                   // 20
+constexpr int P5_GFAST = FM_P5_GFAST;
+constexpr int P5_GSLOW = (P5_GSLOTS - 4 * P5_GFAST + 3) / 4;
+constexpr int P5_GJ = P5_GFAST > P5_GSLOW ? P5_GFAST : P5_GSLOW;                 // load rounds per wave
+static_assert(P5_GSLOW >= 0 && 4 * (P5_GFAST + P5_GSLOW) >= P5_GSLOTS, "gray slots");
 constexpr int P5_NH = P5_GH * (TS / 4);  // tap jobs per frame
 constexpr int P5_HJ = (P5_NH + NT - 1) / NT;
 // the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
-constexpr int P5_GLASTW = (P5_NG - (P5_GJ - 1) * NT + 63) / 64;  // 4 of 8
 constexpr int P5_HLASTW = (P5_NH - (P5_HJ - 1) * NT + 63) / 64;  // 1 of 8
 constexpr int P5_GBUF = P5_NG + 64;      // + a pad slot per lane for the idle jobs' stores (branch-free)
 constexpr int P5_HROW = TS;              // u16 per H row
@@ -691,13 +701,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
     if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+#ifdef FM_DEV_SWITCHES
+    // profiling only (FM_PTS, dev build): [hw_id | xcc_id << 32, realtime start, realtime end, memtime cycles]
+    uint64_t* pts = (a.dbg_pts && tid == 0) ? a.dbg_pts + ((size_t)s * a.ntiles + ti) * 4 : nullptr;
+    uint64_t rt0 = 0, mt0 = 0;
+    if (pts) {
+        pts[0] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        mt0 = __builtin_amdgcn_s_memtime();
+    }
+#endif
 
     // ---- per-thread job plans (frame invariant)
     uint32_t goff[P5_GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
     uint32_t gdst[P5_GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
+    const int gjobs = wv < 4 ? P5_GFAST : P5_GSLOW;  // this wave's gray slots (wave-uniform)
 #pragma unroll
     for (int i = 0; i < P5_GJ; i++) {
-        const int j = tid + NT * i;
+        const int slot = wv >= 4 ? (wv - 4) * P5_GSLOW + i : 4 * P5_GSLOW + wv * P5_GFAST + i;
+        const int j = i < gjobs ? slot * 64 + ln : P5_NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / P5_GQ, gq = j - gr * P5_GQ;
         const int x = x0 - 4 + 4 * gq;
         const bool live = j < P5_NG && x >= 0 && x + 4 <= w;
@@ -772,7 +794,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < P5_GJ; i++) {
-            if (i == P5_GJ - 1 && wv >= P5_GLASTW) break;
+            if (i >= gjobs) break;  // wave-uniform
             gb[gdst[i]] = gray4(rw.v[i].x, rw.v[i].y, rw.v[i].z);
         }
     };
@@ -803,7 +825,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #ifndef FM_P5_SKIP
 #define FM_P5_SKIP 0  // compile-time stage ablation (tools/ablate_p5c.sh)
 #endif
-#ifdef FM_DEV_SWITCHES
+#ifdef FM_DEV_SKIP  // runtime FM_DEBUG_SKIP (changes the code shape; tools/ablate_p5c.sh does it at compile time)
     const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
 #else
     constexpr int skip = FM_P5_SKIP;
@@ -824,10 +846,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
+#ifndef FM_P5_PRIO
+#define FM_P5_PRIO 0  // issue priority of the pixel waves against the contour pass's (fm_ccl.hip FM_*_PRIO)
+#endif
+    if (FM_P5_PRIO) __builtin_amdgcn_s_setprio(FM_P5_PRIO);
+#ifdef FM_DEV_SWITCHES
+    // profiling (FM_PTS, dev build): per-wave cycles in the frame barrier, chain, taps, gray+stores+loads
+    uint64_t* phw = a.dbg_pts ? a.dbg_pts + (size_t)a.S * a.ntiles * 4 + (((size_t)s * a.ntiles + ti) * NW + wv) * 4 : nullptr;
+    uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, tA = __builtin_amdgcn_s_memtime(), tB;
+#define P5_PH(acc) do { if (phw) { tB = __builtin_amdgcn_s_memtime(); acc += tB - tA; tA = tB; } } while (0)
+#else
+#define P5_PH(acc) do { } while (0)
+#endif
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
+        P5_PH(ph3);
         lds_barrier();
+        P5_PH(ph0);
         uint32_t colbits = 0, fl = 0;
         ChainCtx ccf = cc;
         ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
@@ -843,7 +879,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             else
                 chain_rows<KC, false, false, KEEP, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
         }
+        P5_PH(ph1);
         if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
+        P5_PH(ph2);
         // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
         // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
         // makes every frame wait for the stores below before the next loads
@@ -856,6 +894,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         // unconditional (see load): past the batch's last frame it re-reads that frame
         if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
     }
+#ifdef FM_DEV_SWITCHES
+    P5_PH(ph3);
+    if (phw && ln == 0) {
+        phw[0] = ph0;
+        phw[1] = ph1;
+        phw[2] = ph2;
+        phw[3] = ph3;
+    }
+#endif
+#undef P5_PH
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
@@ -864,6 +912,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         const int y = y0 + RPWV * wv + j;
         if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
+#ifdef FM_DEV_SWITCHES
+    if (pts) {
+        const uint64_t rt = __builtin_amdgcn_s_memrealtime(), mt = __builtin_amdgcn_s_memtime();
+        pts[1] = rt0;
+        pts[2] = rt;
+        pts[3] = mt - mt0;
+    }
+#endif
 }
 
 }  // namespace px

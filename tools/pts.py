@@ -11,7 +11,16 @@ import numpy as np
 
 
 def main(path, T=32):
-    v = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
+    raw = np.fromfile(path, dtype=np.uint64)
+    nwg = raw.size // 36
+    ph = raw[nwg * 4:].reshape(nwg, 8, 4).astype(np.float64) if raw.size == nwg * 36 else None
+    v = raw[:nwg * 4].reshape(-1, 4) if ph is not None else raw.reshape(-1, 4)
+    if ph is not None and ph.sum() > 0:
+        tot = ph.sum(axis=2)
+        print("k_pix5 per-wave phase cycles per launch (mean over workgroups; waves 0..7):")
+        for k, name in enumerate(["barrier", "chain", "taps", "gray+st+ld"]):
+            print(f"  {name:11s} " + " ".join(f"{x:9.0f}" for x in ph[:, :, k].mean(axis=0)))
+        print("  total       " + " ".join(f"{x:9.0f}" for x in tot.mean(axis=0)))
     v = v[v[:, 1] > 0]
     hw = (v[:, 0] & 0xFFFFFFFF).astype(np.int64)
     xcc = (v[:, 0] >> np.uint64(32)).astype(np.int64) & 0xF
