@@ -665,7 +665,15 @@ constexpr int P5_GSLOW = (P5_GSLOTS - 4 * P5_GFAST + 3) / 4;
 constexpr int P5_GJ = P5_GFAST > P5_GSLOW ? P5_GFAST : P5_GSLOW;                 // load rounds per wave
 static_assert(P5_GSLOW >= 0 && 4 * (P5_GFAST + P5_GSLOW) >= P5_GSLOTS, "gray slots");
 constexpr int P5_NH = P5_GH * (TS / 4);  // tap jobs per frame
-constexpr int P5_HJ = (P5_NH + NT - 1) / NT;
+// tap jobs likewise (FM_P5_HFAST slots to each of waves 0..3); 0 keeps the round-robin deal
+#ifndef FM_P5_HFAST
+#define FM_P5_HFAST 0
+#endif
+constexpr int P5_HSLOTS = (P5_NH + 63) / 64;                                   // 17
+constexpr int P5_HFAST = FM_P5_HFAST;
+constexpr int P5_HSLOW = P5_HFAST ? (P5_HSLOTS - 4 * P5_HFAST + 3) / 4 : 0;
+constexpr int P5_HJ = P5_HFAST ? (P5_HFAST > P5_HSLOW ? P5_HFAST : P5_HSLOW) : (P5_NH + NT - 1) / NT;
+static_assert(!P5_HFAST || (P5_HSLOW >= 0 && 4 * (P5_HFAST + P5_HSLOW) >= P5_HSLOTS), "tap slots");
 // the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
 constexpr int P5_HLASTW = (P5_NH - (P5_HJ - 1) * NT + 63) / 64;  // 1 of 8
 constexpr int P5_GBUF = P5_NG + 64;      // + a pad slot per lane for the idle jobs' stores (branch-free)
@@ -728,9 +736,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         gdst[i] = j < P5_NG ? (uint32_t)j : (uint32_t)(P5_NG + ln);
     }
     uint32_t hsrc[P5_HJ], hdst[P5_HJ];
+    const int hjobs = P5_HFAST ? (wv < 4 ? P5_HFAST : P5_HSLOW) : P5_HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
     for (int i = 0; i < P5_HJ; i++) {
-        const int j = tid + NT * i;
+        const int hslot = wv >= 4 ? (wv - 4) * P5_HSLOW + i : 4 * P5_HSLOW + wv * P5_HFAST + i;
+        const int j = P5_HFAST ? (i < hjobs ? hslot * 64 + ln : P5_NH) : tid + NT * i;
         const bool live = j < P5_NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
         hsrc[i] = (uint32_t)(hr * P5_GQ + hq);
@@ -801,7 +811,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < P5_HJ; i++) {
-            if (i == P5_HJ - 1 && wv >= P5_HLASTW) break;
+            if (P5_HFAST ? i >= hjobs : (i == P5_HJ - 1 && wv >= P5_HLASTW)) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
             if (edge_tile) {
