@@ -12,6 +12,7 @@ from ._native import (  # noqa: F401
     CascadeClassifier,
     Contour,
     FMError,
+    MJpegDecoder,
     MotionEngine,
     NativeLibraryMissing,
     rasterize_masks,

@@ -29,6 +29,8 @@ EXPORTED = (
     "fm_host_alloc", "fm_host_free", "fm_last_fallbacks", "fm_last_ccl_stats",
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
+    "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
+    "fm_submit_jpeg",
 )
 
 
@@ -114,9 +116,18 @@ def load() -> C.CDLL:
     L.fm_haar_detect_frames.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
     L.fm_haar_last_ms.argtypes = [vp]
     L.fm_haar_last_ms.restype = C.c_double
+    L.fm_mjpeg_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
+    L.fm_mjpeg_destroy.argtypes = [vp]
+    L.fm_mjpeg_destroy.restype = None
+    L.fm_mjpeg_last_error.argtypes = [vp]
+    L.fm_mjpeg_last_error.restype = C.c_char_p
+    L.fm_mjpeg_decode.argtypes = [vp, vp, vp, i32, vp, i32]
+    L.fm_mjpeg_last_ms.argtypes = [vp]
+    L.fm_mjpeg_last_ms.restype = C.c_double
+    L.fm_submit_jpeg.argtypes = [vp, vp, vp, vp, i32]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
-                        "fm_haar_last_ms"):
+                        "fm_haar_last_ms", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_last_ms"):
             getattr(L, name).restype = i32
     _lib = L
     return L
@@ -283,6 +294,18 @@ class MotionEngine:
         self._check(self._L.fm_submit(self._h, C.c_void_p(ptr), n_frames, 1))
         self._inflight.append((n_frames, None))
 
+    def submit_jpeg(self, decoder: "MJpegDecoder", jpegs) -> None:
+        """Compressed frames (the decode side, fm.py:497-506): jpegs = n_frames x n_streams JPEG byte
+        strings in [t][s] order (a flat sequence), decoded on the GPU into the batch, then processed
+        as submit().  The byte strings may be dropped once this returns."""
+        n = len(jpegs)
+        if n % self.n_streams:
+            raise ValueError(f"{n} JPEGs is not a multiple of n_streams={self.n_streams}")
+        ptrs, sizes, keep = _jpeg_arrays(jpegs)
+        self._check(self._L.fm_submit_jpeg(self._h, decoder._h, _ptr(ptrs), _ptr(sizes), n // self.n_streams))
+        del keep
+        self._inflight.append((n // self.n_streams, None))
+
     def wait(self) -> None:
         """Complete the oldest batch in flight; its results become readable."""
         self._check(self._L.fm_wait(self._h))
@@ -429,6 +452,65 @@ class CascadeClassifier:
     def close(self):
         if self._h:
             load().fm_haar_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _jpeg_arrays(jpegs):
+    """(pointer array, size array, keep-alive list) for a sequence of JPEG byte strings."""
+    keep = [np.frombuffer(j, np.uint8) if not isinstance(j, np.ndarray) else np.ascontiguousarray(j, np.uint8)
+            for j in jpegs]
+    ptrs = np.array([k.ctypes.data for k in keep], np.uint64)
+    sizes = np.array([k.size for k in keep], np.uint64)
+    return ptrs, sizes, keep
+
+
+class MJpegDecoder:
+    """The decode side on the GPU: baseline JPEG frames of an MJPEG stream ->
+    BGR u8 frames as cv2.VideoCapture.read returns them (fm.py:497-506), libjpeg-turbo's default
+    decode reproduced bit for bit (jpeg_idct_islow, fancy upsampling, integer YCbCr tables)."""
+
+    def __init__(self, width: int, height: int, max_frames: int = 64, device: int = 0):
+        L = load()
+        h = C.c_void_p()
+        rc = L.fm_mjpeg_create(int(device), int(width), int(height), int(max_frames), C.byref(h))
+        self._h = h
+        if rc != FM_OK:
+            msg = L.fm_mjpeg_last_error(h).decode() if h else ""
+            L.fm_mjpeg_destroy(h)
+            self._h = None
+            raise FMError(rc, f"fm_mjpeg_create: {msg}")
+        self.width, self.height, self.max_frames = int(width), int(height), int(max_frames)
+
+    def decode(self, jpegs) -> np.ndarray:
+        """JPEG byte strings -> BGR u8 [n, H, W, 3] (host)."""
+        L = load()
+        ptrs, sizes, keep = _jpeg_arrays(jpegs)
+        out = np.empty((len(keep), self.height, self.width, 3), np.uint8)
+        rc = L.fm_mjpeg_decode(self._h, _ptr(ptrs), _ptr(sizes), len(keep), _ptr(out), 0)
+        if rc != FM_OK:
+            raise FMError(rc, f"fm_mjpeg_decode: {L.fm_mjpeg_last_error(self._h).decode()}")
+        return out
+
+    def decode_device(self, jpegs, ptr: int) -> None:
+        """JPEG byte strings -> BGR frames at device address ptr (synchronous)."""
+        L = load()
+        ptrs, sizes, keep = _jpeg_arrays(jpegs)
+        rc = L.fm_mjpeg_decode(self._h, _ptr(ptrs), _ptr(sizes), len(keep), C.c_void_p(ptr), 1)
+        if rc != FM_OK:
+            raise FMError(rc, f"fm_mjpeg_decode: {L.fm_mjpeg_last_error(self._h).decode()}")
+
+    def last_ms(self) -> float:
+        return float(load().fm_mjpeg_last_ms(self._h))
+
+    def close(self):
+        if self._h:
+            load().fm_mjpeg_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -716,11 +716,14 @@ int fm_set_hip_stream(fm_ctx* c, void* s) {
     return FM_OK;
 }
 
-int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
+// fm_submit / fm_submit_jpeg: frames from host memory (copied), device memory, or JPEGs decoded
+// on the input stream into the batch's device buffer (dec != nullptr)
+static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, fm_mjpeg* dec,
+                       const uint8_t* const* jpegs, const size_t* sizes) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
     if ((int)c->inflight.size() >= c->nslots)
         return fail(c, FM_ESTATE, "%d batch(es) already in flight: call fm_wait first", (int)c->inflight.size());
-    if (!frames || n < 1 || n > c->p.max_batch)
+    if ((!frames && !dec) || n < 1 || n > c->p.max_batch)
         return fail(c, FM_EINVAL, "n_frames %d outside [1, max_batch=%d] or null frames", n, c->p.max_batch);
     HIP_TRY(c, hipSetDevice(c->p.device));
     const int si = c->next_slot;
@@ -733,7 +736,16 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     // work image is small); the pixel stream waits for it below
     hipStream_t rs = c->rs_stream ? c->rs_stream : ps;
     const uint8_t* src = frames;
-    if (!on_device) {
+    if (dec) {  // the decode side (§8(f)-3): JPEGs -> BGR frames in the batch's device buffer
+        if (!B.d_in) {
+            int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
+            if (rc) return rc;
+        }
+        if (int rc = fm_mjpeg_enqueue(dec, jpegs, sizes, (int)F, B.d_in, rs))
+            return fail(c, rc, "JPEG decode: %s", fm_mjpeg_last_error(dec));
+        src = B.d_in;
+        on_device = 0;  // (the input stream ran: the pixel stream waits for it below)
+    } else if (!on_device) {
         if (!B.d_in) {
             int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
             if (rc) return rc;
@@ -901,6 +913,16 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     c->inflight.push_back(si);
     c->next_slot = (si + 1) % c->nslots;
     return FM_OK;
+}
+
+int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
+    return submit_impl(c, frames, n, on_device, nullptr, nullptr, nullptr);
+}
+
+int fm_submit_jpeg(fm_ctx* c, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (!dec || !jpegs || !sizes) return fail(c, FM_EINVAL, "null decoder or JPEG arrays");
+    return submit_impl(c, nullptr, n, 0, dec, jpegs, sizes);
 }
 
 int fm_wait(fm_ctx* c) {

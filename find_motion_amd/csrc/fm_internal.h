@@ -207,3 +207,7 @@ struct KernelTimer {
 };
 
 }  // namespace fm
+
+// decode side (fm_jpeg.hip): queue the decode of n JPEGs into BGR frames at device address out on
+// stream st; FM_* status, the message in fm_mjpeg_last_error
+int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* sizes, int n, uint8_t* out, hipStream_t st);

@@ -219,6 +219,39 @@ int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);
 /* Device time of the last fm_haar_detect's kernels (HIP events), ms. */
 double fm_haar_last_ms(const fm_haar* det);
 
+/* ---- Decode side: MJPEG frames decoded on the GPU ------
+ * Replaces cv2.VideoCapture.read (find_motion.py:413, :497-506) for MJPEG
+ * video, where every frame is one baseline JPEG.  The decode is libjpeg-
+ * turbo's default one (what OpenCV and Pillow call): jpeg_idct_islow, fancy
+ * upsampling, integer YCbCr->RGB tables, BGR u8 HWC out as cap.read() returns.
+ * Supported: 8-bit baseline / extended-sequential Huffman JPEG, grayscale or
+ * YCbCr with Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2, restart intervals
+ * optional (each interval is decoded by its own lane; without them one lane
+ * decodes one frame).  The host only parses marker segments and copies the
+ * entropy-coded bytes (stuffing and RSTn removed); Huffman decoding, IDCT,
+ * upsampling and colour conversion run on the device.  Every frame of one
+ * call must share frame 0's size, sampling and Huffman tables (an MJPEG
+ * stream repeats them); quantization tables may differ per frame. */
+typedef struct fm_mjpeg fm_mjpeg;
+/* A decoder for width x height frames, up to max_frames per call.  *out is set
+ * even on failure (fm_mjpeg_last_error says why); release with fm_mjpeg_destroy. */
+int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg** out);
+void fm_mjpeg_destroy(fm_mjpeg* dec);
+const char* fm_mjpeg_last_error(const fm_mjpeg* dec);
+/* Decode n JPEGs (host memory: jpegs[i], sizes[i] bytes) into [n][H][W][3] BGR
+ * frames at out: device memory when out_on_device, else host memory.
+ * Synchronous. */
+int fm_mjpeg_decode(fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n, uint8_t* out,
+                    int out_on_device);
+/* Device time of the last fm_mjpeg_decode's kernels (HIP events), ms. */
+double fm_mjpeg_last_ms(const fm_mjpeg* dec);
+/* fm_submit from compressed frames: n_frames x n_streams JPEGs in [t][s]
+ * order, decoded by dec (created for this context's src_w x src_h) on the
+ * context's input stream into the batch's device buffer, then processed as
+ * fm_submit (frames, n_frames, on_device = 1) would.  The host buffers may be
+ * reused when the call returns. */
+int fm_submit_jpeg(fm_ctx* ctx, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n_frames);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,101 @@
+"""Decode side on the GPU: fm_mjpeg_* / fm_submit_jpeg against Pillow's libjpeg-turbo.
+
+The reference gets frames from cv2.VideoCapture.read (fm.py:413, 497-506); on MJPEG video that is a
+libjpeg(-turbo) default decode per frame.  Every case here is bit-exact against Pillow's decode of the same
+bytes (the CPU restatement oracle/jpeg.py is pinned to it in tests/test_jpeg_host.py), and the whole path
+from JPEG bytes to contours equals the path from the reference-decoded frames."""
+import numpy as np
+import pytest
+
+from find_motion_amd import FMError, MJpegDecoder, MotionEngine
+from find_motion_amd.synthetic import SyntheticVideo
+from jpeg_cases import ENCODINGS, Image, encode, image, reference_decode
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(Image is None, reason="Pillow not importable")]
+
+
+@pytest.mark.parametrize("name,kw", ENCODINGS)
+@pytest.mark.parametrize("H,W", [(16, 16), (37, 53), (8, 9), (61, 33), (9, 2), (5, 4), (1, 1)])
+def test_decoder_equals_libjpeg(name, kw, H, W):
+    frames = [encode(image(H, W, kind, seed=s), **kw) for s, kind in enumerate(["noise", "smooth", "smooth"])]
+    dec = MJpegDecoder(W, H, max_frames=4)
+    got = dec.decode(frames)
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f)), (name, H, W, i)
+    dec.close()
+
+
+def test_grayscale_frames_come_out_bgr():
+    frames = [encode(image(37, 53, "smooth", seed=s)[..., 1], quality=75) for s in range(3)]
+    dec = MJpegDecoder(53, 37, max_frames=3)
+    got = dec.decode(frames)
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f))
+
+
+@pytest.mark.parametrize("kw", [dict(quality=75), dict(quality=90, restart_marker_rows=1),
+                                dict(quality=60, subsampling=1)])
+def test_1080p_synthetic_video(kw):
+    v = SyntheticVideo(1920, 1080, 0)
+    frames = [encode(v.frame(t), **kw) for t in (0, 1, 95, 96)]
+    dec = MJpegDecoder(1920, 1080, max_frames=8)
+    got = dec.decode(frames)
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f)), i
+    # a second call reuses the (re-zeroed) coefficient buffer
+    got2 = dec.decode(frames[::-1])
+    for i, f in enumerate(frames[::-1]):
+        assert np.array_equal(got2[i], reference_decode(f)), i
+    assert dec.last_ms() > 0
+
+
+def test_decode_into_device_memory():
+    torch = pytest.importorskip("torch")
+    frames = [encode(image(64, 96, "smooth", seed=s), quality=80) for s in range(4)]
+    dec = MJpegDecoder(96, 64, max_frames=4)
+    out = torch.zeros((4, 64, 96, 3), dtype=torch.uint8, device="cuda")
+    dec.decode_device(frames, out.data_ptr())
+    got = out.cpu().numpy()
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f))
+
+
+def test_refusals():
+    dec = MJpegDecoder(16, 16, max_frames=2)
+    with pytest.raises(FMError):  # progressive
+        dec.decode([encode(image(16, 16, "smooth"), quality=75, progressive=True)])
+    with pytest.raises(FMError):  # size differs from the decoder's
+        dec.decode([encode(image(16, 24, "smooth"), quality=75)])
+    with pytest.raises(FMError):  # more frames than max_frames
+        dec.decode([encode(image(16, 16, "smooth"), quality=75)] * 3)
+    with pytest.raises(FMError):  # not a JPEG
+        dec.decode([b"\x00" * 64])
+    dec.close()
+    dec = MJpegDecoder(16, 16, max_frames=2)
+    with pytest.raises(FMError):  # per-frame optimized Huffman tables differ within one call
+        dec.decode([encode(image(16, 16, "noise", seed=s), quality=75, optimize=True) for s in range(2)])
+
+
+def test_submit_jpeg_equals_submit_of_decoded_frames():
+    """The path from compressed frames (fm_submit_jpeg) == fm_submit of the libjpeg-decoded frames."""
+    W, H, S, T = 320, 240, 2, 4
+    vids = [SyntheticVideo(W, H, s) for s in range(S)]
+    kw = dict(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    a, b = MotionEngine(**kw), MotionEngine(**kw)
+    dec = MJpegDecoder(W, H, max_frames=T * S)
+    for bi in range(3):
+        jp = [encode(vids[s].frame(bi * T + t), quality=85) for t in range(T) for s in range(S)]
+        frames = np.stack([reference_decode(j) for j in jp]).reshape(T, S, H, W, 3)
+        a.submit_jpeg(dec, jp)
+        b.submit(frames)
+        a.wait()
+        b.wait()
+        assert np.array_equal(a.counts(), b.counts())
+        for t in range(T):
+            for s in range(S):
+                assert [c.bbox for c in a.contours(t, s)] == [c.bbox for c in b.contours(t, s)]
+                assert np.array_equal(a.mask(t, s), b.mask(t, s))
+    for s in range(S):
+        assert np.array_equal(a.background(s), b.background(s))
+    a.close()
+    b.close()

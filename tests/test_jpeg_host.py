@@ -1,0 +1,57 @@
+"""Decode side, CPU: the restatement oracle/jpeg.py against Pillow's libjpeg-turbo.
+
+libjpeg-turbo's default decode is what cv2.VideoCapture.read / imdecode run on MJPEG frames (fm.py:497-506);
+Pillow bundles it, so the restatement of jdhuff / jidctint (islow) / jdsample (fancy upsampling) / jdcolor
+is pinned bit for bit here, on every sampling layout, odd sizes (partial MCUs, one-column chroma), restart
+intervals and grayscale.  The committed fixtures (tests/golden/jpeg_cases.npz, tests/golden/make_golden_jpeg.py)
+keep the same check on a machine whose Pillow differs."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import jpeg
+from jpeg_cases import ENCODINGS, Image, encode, image, reference_decode
+
+pytestmark = pytest.mark.skipif(Image is None, reason="Pillow not importable")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "jpeg_cases.npz")
+
+
+def _bgr(a):
+    return np.repeat(a[..., None], 3, axis=2) if a.ndim == 2 else a
+
+
+@pytest.mark.parametrize("name,kw", ENCODINGS)
+@pytest.mark.parametrize("H,W", [(16, 16), (37, 53), (8, 9), (24, 40), (61, 33), (9, 2), (5, 4), (3, 7), (1, 1)])
+@pytest.mark.parametrize("kind", ["noise", "smooth"])
+def test_restatement_equals_libjpeg(name, kw, H, W, kind):
+    data = encode(image(H, W, kind), **kw)
+    assert np.array_equal(_bgr(jpeg.decode(data)), reference_decode(data))
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (37, 53)])
+def test_grayscale(H, W):
+    data = encode(image(H, W, "smooth")[..., 1], quality=75)
+    assert np.array_equal(_bgr(jpeg.decode(data)), reference_decode(data))
+
+
+def test_parse_reports_layout_and_restart_interval():
+    j = jpeg.parse(encode(image(32, 48, "smooth"), quality=80, restart_marker_blocks=3))
+    assert (j["frame"]["H"], j["frame"]["W"]) == (32, 48)
+    assert [(c["h"], c["v"]) for c in j["frame"]["comps"]] == [(2, 2), (1, 1), (1, 1)]
+    assert j["dri"] > 0
+    assert set(j["ht"]) == {(0, 0), (1, 0), (0, 1), (1, 1)}
+
+
+def test_progressive_is_refused():
+    data = encode(image(16, 16, "smooth"), quality=75, progressive=True)
+    with pytest.raises(jpeg.JpegError):
+        jpeg.parse(data)
+
+
+def test_golden_fixtures():
+    z = np.load(GOLDEN)
+    n = int(z["n"])
+    for i in range(n):
+        data = z[f"jpeg{i}"].tobytes()
+        assert np.array_equal(_bgr(jpeg.decode(data)), z[f"bgr{i}"]), i
