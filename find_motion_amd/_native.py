@@ -30,7 +30,7 @@ EXPORTED = (
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
-    "fm_submit_jpeg",
+    "fm_submit_jpeg", "fm_read_frame",
 )
 
 
@@ -125,6 +125,7 @@ def load() -> C.CDLL:
     L.fm_mjpeg_last_ms.argtypes = [vp]
     L.fm_mjpeg_last_ms.restype = C.c_double
     L.fm_submit_jpeg.argtypes = [vp, vp, vp, vp, i32]
+    L.fm_read_frame.argtypes = [vp, i32, i32, vp]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
                         "fm_haar_last_ms", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_last_ms"):
@@ -194,6 +195,7 @@ class MotionEngine:
         self.max_inflight = self._L.fm_max_inflight(h)
         self.n_streams = n_streams
         self.src_shape = (src_h, src_w, 3)
+        self.device = int(device)
         self.max_batch = max_batch
         self.max_contours = max_contours
         self.last_batch = 0
@@ -346,6 +348,12 @@ class MotionEngine:
     def mask(self, frame: int, stream: int) -> np.ndarray:
         out = np.empty(self.work_shape, np.uint8)
         self._check(self._L.fm_read_mask(self._h, frame, stream, _ptr(out)))
+        return out
+
+    def read_frame(self, frame: int, stream: int) -> np.ndarray:
+        """The source frame (BGR) of (frame, stream) of the last waited batch, from the device."""
+        out = np.empty(self.src_shape, np.uint8)
+        self._check(self._L.fm_read_frame(self._h, frame, stream, _ptr(out)))
         return out
 
     def plane(self, which: int, frame: int, stream: int) -> np.ndarray:

@@ -67,6 +67,7 @@ struct BatchSlot {
     int n = 0;                      // frames in flight in this slot (0 = none)
     FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
     uint64_t gen = 0;               // submits into this slot
+    const uint8_t* src = nullptr;   // the batch's source frames [T][S][H][W][3] on the device (fm_read_frame)
 };
 
 struct fm_ctx {
@@ -909,6 +910,7 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
     }
     for (int s = 0; s < S; s++) c->bg_init[s] = 1;
     B.n = n;
+    B.src = src;
     B.gen++;
     c->inflight.push_back(si);
     c->next_slot = (si + 1) % c->nslots;
@@ -1074,6 +1076,18 @@ int fm_read_plane(fm_ctx* c, int plane, int frame, int stream, uint8_t* out) {
     const size_t Fcur = (size_t)c->ready * c->p.n_streams;
     HIP_TRY(c, hipMemcpyAsync(out, B.d_planes + ((size_t)plane * Fcur + f) * c->work_plane, c->work_plane,
                               hipMemcpyDeviceToHost, c->aux_stream));
+    HIP_TRY(c, hipStreamSynchronize(c->aux_stream));
+    return FM_OK;
+}
+
+int fm_read_frame(fm_ctx* c, int frame, int stream, uint8_t* out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    if (int rc = check_frame(c, frame, stream, true)) return rc;
+    const BatchSlot& B = c->slots[c->ready_slot];
+    if (!B.src) return fail(c, FM_ESTATE, "no source frames for the last waited batch");
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    HIP_TRY(c, hipMemcpyAsync(out, B.src + ((size_t)frame * c->p.n_streams + stream) * c->src_frame_bytes,
+                              c->src_frame_bytes, hipMemcpyDeviceToHost, c->aux_stream));
     HIP_TRY(c, hipStreamSynchronize(c->aux_stream));
     return FM_OK;
 }

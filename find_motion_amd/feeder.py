@@ -18,6 +18,12 @@ So decode (host), H2D copies and the pixel kernel / contour pass of later
 batches all overlap the state machines of the batch being consumed.  Frame
 order per stream, and therefore every decision, is unchanged: batches are
 waited in submission order and consumed frame by frame.
+
+JPEG mode (every capture has read_jpeg(), i.e. MJPEG sources, SURVEY.md
+§8(f)-3): the decoder thread only reads the compressed frames; the engine
+decodes them on the GPU (fm_submit_jpeg) in front of the hot path, so only
+compressed bytes cross PCIe.  Batch.frames then holds JPEG byte strings and
+Batch.buf is None.
 """
 from __future__ import annotations
 
@@ -39,6 +45,7 @@ class Batch:
     buf: np.ndarray
     frames: list
     T: int
+    jpegs: list = None  # JPEG mode: the T x S compressed frames in [t][s] order, ended streams padded
 
 
 class BatchFeeder:
@@ -49,11 +56,23 @@ class BatchFeeder:
     StreamGroup always did); the iteration ends when every stream has ended.
     """
 
-    def __init__(self, engine, caps: list, batch: int, depth: int | None = None, buffers: list | None = None):
+    def __init__(self, engine, caps: list, batch: int, depth: int | None = None, buffers: list | None = None,
+                 jpeg: bool | None = None):
         self.engine = engine
         self.caps = list(caps)
         self.T = int(batch)
         self.depth = max(1, min(depth or engine.max_inflight, engine.max_inflight))
+        # JPEG mode needs every capture to hand out compressed frames (None: when they all can)
+        can = bool(self.caps) and all(hasattr(c, "read_jpeg") for c in self.caps)
+        self.jpeg = can if jpeg is None else bool(jpeg)
+        if self.jpeg and not can:
+            raise ValueError("JPEG mode needs captures with read_jpeg()")
+        self.decoder = None
+        if self.jpeg:
+            from ._native import MJpegDecoder
+            sw, sh = engine.src_shape[1], engine.src_shape[0]
+            self.decoder = MJpegDecoder(sw, sh, max_frames=self.T * len(self.caps), device=engine.device)
+            buffers = []
         # depth batches in flight + one being decoded + one being consumed; page-locking is slow
         # (~0.3 s per GB), so callers that run several feeders pass the same buffers to each
         self.buffers = buffers if buffers is not None else self.make_buffers(engine, self.T, self.depth)
@@ -84,7 +103,7 @@ class BatchFeeder:
                 got = [[] for _ in range(S)]
                 for s, cap in enumerate(self.caps):
                     while live[s] and len(got[s]) < self.T:
-                        ok, fr = cap.read()
+                        ok, fr = cap.read_jpeg() if self.jpeg else cap.read()
                         if not ok:
                             live[s] = False
                             break
@@ -92,6 +111,15 @@ class BatchFeeder:
                 T = max(len(g) for g in got)
                 if T == 0:
                     break
+                if self.jpeg:
+                    jp = []
+                    for t in range(T):
+                        for s in range(S):
+                            if t < len(got[s]):
+                                last[s] = got[s][t]
+                            jp.append(last[s] if last[s] is not None else got[0][0])  # padding
+                    self._full.put(Batch(None, got, T, jp))
+                    continue
                 buf = self._free.get()
                 if buf is None or self._stop.is_set():
                     break
@@ -126,14 +154,18 @@ class BatchFeeder:
                     if b is None:
                         done = True
                         break
-                    eng.submit(b.buf[:b.T])
+                    if b.jpegs is not None:
+                        eng.submit_jpeg(self.decoder, b.jpegs)
+                    else:
+                        eng.submit(b.buf[:b.T])
                     inflight.append(b)
                 if not inflight:
                     break
                 b = inflight.popleft()
                 eng.wait()
                 yield b
-                self._free.put(b.buf)
+                if b.buf is not None:
+                    self._free.put(b.buf)
         finally:
             self._stop.set()
             while inflight:  # an abandoned iteration: finish what was submitted
@@ -142,5 +174,8 @@ class BatchFeeder:
             self._free.put(None)  # a decoder blocked on a free buffer wakes and stops
             self._thread.join(timeout=30)
             self._copiers.shutdown(wait=True)
+            if self.decoder is not None:
+                self.decoder.close()
+                self.decoder = None
         if self._error is not None:
             raise self._error

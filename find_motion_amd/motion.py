@@ -25,6 +25,12 @@ VideoFrame:
   access.  The mask polygons are rasterised once per video (they are static)
   and applied inside the kernel, so mask_off_areas() has nothing left to do.
 
+MJPEG sources (videoio.MjpegAviCapture) are decoded on the GPU in front of
+the hot path (fm_submit_jpeg): frame.raw is then fetched
+from the device on first access (a frame the state machine writes, shows or
+runs a cascade on), and an MJPG output receives the source's JPEG bytes
+unchanged instead of a re-encode.
+
 Extra keyword arguments (not in the reference): device (HIP ordinal),
 batch (frames decoded ahead and processed per kernel launch; the per-frame
 results and the decisions are identical for any batch -- only ref_frame is
@@ -46,7 +52,8 @@ from collections import deque
 import numpy as np
 
 from . import videoio
-from ._native import PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, CascadeClassifier, MotionEngine, rasterize_masks
+from ._native import (PLANE_BLUR, PLANE_DELTA, PLANE_GRAY, CascadeClassifier, MJpegDecoder, MotionEngine,
+                      rasterize_masks)
 from .feeder import BatchFeeder
 
 log = logging.getLogger("find_motion_amd")
@@ -105,10 +112,14 @@ class VideoFrame:
 
     _LAZY = ("gray", "blur", "frame_delta", "thresh")
 
-    def __init__(self, frame, show: bool = False) -> None:
-        self.raw = frame
+    def __init__(self, frame, show: bool = False, jpeg: bytes = None) -> None:
+        self._raw = frame
+        self.jpeg = jpeg  # MJPEG input: the compressed source frame (raw is decoded on the GPU)
+        self._load = None  # MJPEG input: fetches raw on first access (VideoMotion.bind_results)
+        self._show = show
         # fm.py:236 always copies raw; the copy is only drawn on (show), so it is made only then
-        self.frame = frame.copy() if show else frame
+        if frame is not None:
+            self.frame = frame.copy() if show else frame
         self.in_cache = False
         self.contours: list = []
         self.resized = None
@@ -116,6 +127,28 @@ class VideoFrame:
         self._vals: dict = {}
         self.processed = False
         self.index = -1  # position in the source (set when the engine processes the frame)
+
+    @property
+    def raw(self):
+        r = self._raw
+        if r is None:
+            if self._load is None:
+                raise AttributeError("raw")
+            r = self._raw = self._load()
+        return r
+
+    @raw.setter
+    def raw(self, value):
+        self._raw = value
+
+    def __getattr__(self, name):
+        # frame of an MJPEG input, made from raw on first access like fm.py:236
+        d = self.__dict__
+        if name == "frame" and d.get("_load") is not None:
+            f = self.raw.copy() if d.get("_show") else self.raw
+            d["frame"] = f
+            return f
+        raise AttributeError(name)
 
     def _get(self, name):
         if name in self._vals:
@@ -156,8 +189,7 @@ class VideoFrame:
         self._bound = None
         if self.in_cache:
             return
-        if "raw" in self.__dict__:
-            del self.raw
+        self._raw = self._load = self.jpeg = None
 
 
 class VideoMotion:
@@ -239,6 +271,7 @@ class VideoMotion:
         self._capture = capture
         self._ahead: typing.Deque[VideoFrame] = deque()
         self.frames_read = 0
+        self._jpeg_dec = None  # one-frame GPU decoder for raw frames of batches already overwritten
         self.written_indices: typing.List[int] = []  # source frame indices written, in write order
         self._calc_min_area()
         self._make_gaussian()
@@ -353,14 +386,31 @@ class VideoMotion:
             b = next(self._pipe, None)
             if b is None:
                 return False
-            vfs = [VideoFrame(r, self.show) for r in b.frames[0]]
+            vfs = self.make_frames(b, 0)
             self.bind_results(vfs, eng, 0)
             self._ahead.extend(vfs)
         self.current_frame = self._ahead.popleft()
         return True
 
+    def make_frames(self, b, stream: int) -> list:
+        """VideoFrames of stream `stream` of a waited feeder batch (JPEG batches: raw fetched lazily)."""
+        if b.jpegs is not None:
+            return [VideoFrame(None, self.show, jpeg=j) for j in b.frames[stream]]
+        return [VideoFrame(r, self.show) for r in b.frames[stream]]
+
+    def _raw_loader(self, eng, gen: int, t: int, s: int, jpeg: bytes):
+        def load():
+            if eng.generation == gen:  # the batch's decoded frame is still in the engine's input slot
+                return eng.read_frame(t, s)
+            if self._jpeg_dec is None:
+                self._jpeg_dec = MJpegDecoder(self.frame_width, self.frame_height, 1, device=self.device)
+            return self._jpeg_dec.decode([jpeg])[0]
+        return load
+
     def bind_results(self, vfs, eng, stream: int) -> None:
         for t, vf in enumerate(vfs):
+            if vf.jpeg is not None and vf._raw is None:
+                vf._load = self._raw_loader(eng, eng.generation, t, stream, vf.jpeg)
             vf._bound = _Bound(eng, eng.generation, t, stream)
             vf.contours = eng.contours(t, stream)
             vf.processed = True
@@ -378,29 +428,39 @@ class VideoMotion:
         else:
             self.outfile_name = os.path.join(self.outdir, os.path.basename(outname)) + "_motion.avi"
         self.outfile = videoio.open_writer(self.outfile_name, self.codec, self.fps,
-                                           (self.frame_width, self.frame_height))
+                                           (self.frame_width, self.frame_height),
+                                           jpeg=hasattr(self.cap, "read_jpeg"))
 
     def output_frame(self, frame: VideoFrame = None) -> None:
         """fm.py:509-530"""
         frame = self.current_frame if frame is None else frame
         if self.show and videoio.cv2 is not None:
             videoio.cv2.imshow("frame", frame.frame)
-        self._write(frame.raw, getattr(frame, "index", -1))
+        self._write_frame(frame)
 
     def output_raw_frame(self, frame: np.ndarray = None, index: int = -1) -> None:
         """fm.py:533-546"""
         self._write(frame, index)
 
-    def _write(self, raw, index):
+    def _write_frame(self, frame: VideoFrame) -> None:
+        self._write(lambda: frame.raw, getattr(frame, "index", -1), getattr(frame, "jpeg", None))
+
+    def _put(self, raw, jpeg) -> None:
+        if jpeg is not None and hasattr(self.outfile, "write_jpeg"):
+            self.outfile.write_jpeg(jpeg)  # MJPEG in, MJPG out: the source's bytes, no re-encode
+        else:
+            self.outfile.write(raw() if callable(raw) else raw)
+
+    def _write(self, raw, index, jpeg=None):
         if not self.wrote_frames:
             self._make_outfile()
             self.wrote_frames = True
         try:
-            self.outfile.write(raw)
+            self._put(raw, jpeg)
         except Exception as e:  # noqa: BLE001 (fm.py:527-530)
             self.log.warning("Having to create output file due to exception: {}".format(e))
             self._make_outfile()
-            self.outfile.write(raw)
+            self._put(raw, jpeg)
         self.written_indices.append(index)
 
     # -- the hot path (fm.py:487-494, 619-636, 638-662) ------------------------
@@ -455,7 +515,7 @@ class VideoMotion:
                 self.movement_decay = self.cache_frames
                 for frame in self.frame_cache:
                     if frame is not None:
-                        self.output_raw_frame(frame.raw, getattr(frame, "index", -1))
+                        self._write_frame(frame)  # output_raw_frame(frame.raw), fm.py:557
                         if self.cleanup_flag:
                             frame.in_cache = False
                             frame.cleanup()
@@ -573,6 +633,9 @@ class VideoMotion:
         if self._own_engine and self._engine is not None:
             self._engine.close()
             self._engine = None
+        if self._jpeg_dec is not None:
+            self._jpeg_dec.close()
+            self._jpeg_dec = None
 
     # -- main loop (fm.py:852-904) ---------------------------------------------
     def step(self) -> None:
@@ -664,7 +727,7 @@ class StreamGroup:
             for s, v in enumerate(self.videos):
                 if not b.frames[s]:
                     continue
-                vfs = [VideoFrame(r, v.show) for r in b.frames[s]]
+                vfs = v.make_frames(b, s)
                 v.bind_results(vfs, self.engine, s)
                 for vf in vfs:
                     v.current_frame = vf

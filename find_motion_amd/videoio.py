@@ -10,6 +10,13 @@ available:
 * otherwise (this image has no cv2): uncompressed RIFF AVI (BI_RGB, 24-bit
   BGR, bottom-up rows), read and written here -- the container OpenCV itself
   writes for fourcc 'DIB ' and reads through FFmpeg's rawvideo decoder;
+* MJPEG AVI (fourcc 'MJPG', one baseline JPEG per '00dc' chunk), read here
+  whether or not cv2 exists: MjpegAviCapture.read_jpeg() hands the compressed
+  frames to the GPU decoder (find_motion_amd.MJpegDecoder / fm_submit_jpeg,
+  SURVEY.md §8(f)-3), so only compressed bytes cross PCIe; read() decodes
+  on the GPU too.  MjpegAviWriter writes such files: the 'MJPG' output of an
+  MJPEG input keeps the source's JPEG bytes (write_jpeg); write() encodes a
+  BGR frame with Pillow;
 * in-memory sources for tests, benchmarks and embedding: ArrayCapture over a
   [N][H][W][3] uint8 array and SyntheticCapture over the deterministic
   synthetic video of find_motion_amd.synthetic.
@@ -261,6 +268,141 @@ class RawAviCapture:
         self._mm = None
 
 
+FOURCC_MJPG = b"MJPG"
+
+
+class MjpegAviCapture(RawAviCapture):
+    """MJPEG AVI reader: read_jpeg() -> (ok, JPEG bytes) for the GPU decoder; read() -> (ok, BGR frame),
+    decoded on the GPU (a one-frame MJpegDecoder on `device`, created on first use)."""
+
+    def __init__(self, path: str, device: int = 0):
+        self._device = int(device)
+        self._dec = None
+        super().__init__(path)
+
+    def _walk(self, f, start, end, depth):
+        pos = start
+        while pos + 8 <= end:
+            f.seek(pos)
+            ck, ln = struct.unpack("<4sI", f.read(8))
+            body = pos + 8
+            if ck == b"LIST":
+                kind = f.read(4)
+                if kind in (b"hdrl", b"strl", b"movi", b"rec ") and depth < 4:
+                    self._walk(f, body + 4, min(body + ln, end), depth + 1)
+            elif ck == b"avih":
+                vals = struct.unpack("<10I", f.read(40))
+                if vals[0]:
+                    self.fps = 1e6 / vals[0]
+            elif ck == b"strf" and not self.w:
+                bi = struct.unpack("<IiiHH4s", f.read(20))
+                if bi[5] != FOURCC_MJPG:
+                    raise ValueError(f"not an MJPEG AVI (compression {bi[5]!r})")
+                self.w, self.h = bi[1], abs(bi[2])
+            elif ck[2:] == b"dc" and ln > 0:
+                self._offsets.append((body, ln))
+            pos = body + ln + (ln & 1)
+
+    def read_jpeg(self):
+        if not self._open or self._i >= len(self._offsets):
+            return False, None
+        off, ln = self._offsets[self._i]
+        self._i += 1
+        return True, bytes(self._mm[off: off + ln])
+
+    def read(self):
+        ok, j = self.read_jpeg()
+        if not ok:
+            return False, None
+        if self._dec is None:
+            from ._native import MJpegDecoder
+            self._dec = MJpegDecoder(self.w, self.h, max_frames=1, device=self._device)
+        return True, self._dec.decode([j])[0]
+
+    def release(self) -> None:
+        super().release()
+        if self._dec is not None:
+            self._dec.close()
+            self._dec = None
+
+
+class MjpegAviWriter(RawAviWriter):
+    """MJPEG AVI writer: frames encoded by Pillow (libjpeg-turbo) at `quality` (default 95, OpenCV's MJPG
+    default), one '00dc' chunk per frame."""
+
+    def __init__(self, path: str, fps: float, size, quality: int = 95, **jpeg_kw):
+        self.quality = int(quality)
+        self.jpeg_kw = jpeg_kw
+        self.sizes = []
+        super().__init__(path, fps, size)
+
+    def _write_headers(self):
+        f = self.f
+        f.write(b"RIFF" + struct.pack("<I", 0) + b"AVI ")
+        mx = self.w * self.h * 3
+        hdrl = bytearray()
+        avih = struct.pack("<IIIIIIIIII16x", 1000000 // self.fps, mx * self.fps, 0, 0x10, 0, 0, 1, mx, self.w, self.h)
+        hdrl += b"avih" + struct.pack("<I", len(avih)) + avih
+        strh = struct.pack("<4s4sIHHIIIIIIIIhhhh", b"vids", FOURCC_MJPG, 0, 0, 0, 0, 1, self.fps, 0, 0, mx,
+                           0xFFFFFFFF, 0, 0, 0, self.w, self.h)
+        strf = struct.pack("<IiiHH4sIiiII", 40, self.w, self.h, 1, 24, FOURCC_MJPG, mx, 0, 0, 0, 0)
+        strl = b"strl" + b"strh" + struct.pack("<I", len(strh)) + strh + b"strf" + struct.pack("<I", len(strf)) + strf
+        hdrl += b"LIST" + struct.pack("<I", len(strl)) + strl
+        f.write(b"LIST" + struct.pack("<I", len(hdrl) + 4) + b"hdrl" + hdrl)
+        self._avih_frames_at = 12 + 8 + 4 + 8 + 16
+        self._strh_len_at = 12 + 8 + 4 + 8 + len(avih) + 8 + 4 + 8 + 32
+        self._movi_at = f.tell()
+        f.write(b"LIST" + struct.pack("<I", 0) + b"movi")
+
+    def write_jpeg(self, data: bytes) -> None:
+        off = self.f.tell() - (self._movi_at + 8)
+        self.f.write(b"00dc" + struct.pack("<I", len(data)) + data + (b"\0" if len(data) & 1 else b""))
+        self.index.append(off)
+        self.sizes.append(len(data))
+        self.n += 1
+
+    def write(self, frame: np.ndarray) -> None:
+        import io
+
+        from PIL import Image
+        frame = np.asarray(frame, dtype=np.uint8)
+        if frame.shape != (self.h, self.w, 3):
+            raise ValueError(f"frame shape {frame.shape} != ({self.h}, {self.w}, 3)")
+        b = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(frame[..., ::-1])).save(b, "JPEG", quality=self.quality, **self.jpeg_kw)
+        self.write_jpeg(b.getvalue())
+
+    def release(self) -> None:
+        if self.f is None:
+            return
+        f = self.f
+        movi_end = f.tell()
+        f.write(b"idx1" + struct.pack("<I", 16 * len(self.index)))
+        for off, ln in zip(self.index, self.sizes):
+            f.write(b"00dc" + struct.pack("<III", 0x10, off, ln))
+        end = f.tell()
+        f.seek(4)
+        f.write(struct.pack("<I", end - 8))
+        f.seek(self._movi_at + 4)
+        f.write(struct.pack("<I", movi_end - self._movi_at - 8))
+        f.seek(self._avih_frames_at)
+        f.write(struct.pack("<I", self.n))
+        f.seek(self._strh_len_at)
+        f.write(struct.pack("<I", self.n))
+        f.close()
+        self.f = None
+
+
+def is_mjpeg_avi(path) -> bool:
+    """An AVI whose video stream is MJPG (read by MjpegAviCapture, decoded on the GPU)."""
+    try:
+        with open(path, "rb") as f:
+            head = f.read(4096)
+    except (OSError, TypeError):
+        return False
+    return head[:4] == b"RIFF" and head[8:12] == b"AVI " and FOURCC_MJPG in head
+
+
 def open_capture(source):
     """cv2.VideoCapture(source) when OpenCV exists (fm.py:413); otherwise the readers above.
 
@@ -277,6 +419,8 @@ def open_capture(source):
         return SyntheticCapture(w, h, int(parts[2]), int(parts[3]) if len(parts) > 3 else 0)
     if isinstance(source, str) and source.endswith(".npy"):
         return ArrayCapture(np.load(source, mmap_mode="r", allow_pickle=False))
+    if isinstance(source, str) and is_mjpeg_avi(source):
+        return MjpegAviCapture(source)  # compressed frames to the GPU decoder (§8(f)-3)
     if cv2 is not None:
         return cv2.VideoCapture(source)
     if isinstance(source, int):
@@ -284,8 +428,12 @@ def open_capture(source):
     return RawAviCapture(str(source))
 
 
-def open_writer(path: str, codec: str, fps: float, size):
-    """cv2.VideoWriter(path, fourcc(codec), fps, size) (fm.py:468-470), else an uncompressed AVI."""
+def open_writer(path: str, codec: str, fps: float, size, jpeg: bool = False):
+    """cv2.VideoWriter(path, fourcc(codec), fps, size) (fm.py:468-470), else an uncompressed AVI.
+    jpeg: the frames come from an MJPEG source -- an 'MJPG' output is then an MjpegAviWriter that
+    stores the source's JPEG bytes as they are (write_jpeg), with or without cv2."""
+    if jpeg and codec == "MJPG":
+        return MjpegAviWriter(path, fps, size)
     if cv2 is not None:
         return cv2.VideoWriter(path, cv2.VideoWriter_fourcc(*codec), fps, size)
     if codec not in ("DIB ", "RGB ", "raw ", None):

@@ -251,6 +251,11 @@ double fm_mjpeg_last_ms(const fm_mjpeg* dec);
  * fm_submit (frames, n_frames, on_device = 1) would.  The host buffers may be
  * reused when the call returns. */
 int fm_submit_jpeg(fm_ctx* ctx, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n_frames);
+/* The source frame (BGR u8 [H][W][3], cap.read()'s frame.raw, fm.py:501) of (frame, stream) of the
+ * last waited batch, copied to host memory: what the host needs of a batch submitted with
+ * fm_submit_jpeg only for the frames it writes (fm.py:535-546) or shows.  Valid until the next
+ * fm_wait; for fm_submit(on_device = 1) the caller's buffer must still hold the frames. */
+int fm_read_frame(fm_ctx* ctx, int frame, int stream, uint8_t* out);
 
 #ifdef __cplusplus
 }

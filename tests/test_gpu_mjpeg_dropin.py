@@ -1,0 +1,107 @@
+"""The drop-in on MJPEG input (SURVEY.md §8(f)-3 wired into §8(b)): an MJPEG AVI read by
+videoio.MjpegAviCapture is decoded on the GPU in front of the hot path (BatchFeeder JPEG mode ->
+fm_submit_jpeg).  Decisions must equal the oracle's on the libjpeg-turbo-decoded frames
+(cv2.VideoCapture's frames, fm.py:497-506), raw frames fetched lazily (fm_read_frame, or the
+one-frame decoder once the batch is gone) must equal those decoded frames, and an MJPG output
+must hold the source's JPEG bytes of exactly the written frames."""
+import numpy as np
+import pytest
+
+import oracle
+from find_motion_amd import MotionEngine, motion, videoio
+from find_motion_amd.synthetic import SyntheticVideo
+from jpeg_cases import encode, reference_decode
+from oracle.decision import written_indices
+
+pytestmark = pytest.mark.gpu
+
+
+def _mjpeg_avi(path, W, H, n, seed, **kw):
+    vid = SyntheticVideo(W, H, seed)
+    jp = [encode(vid.frame(i), **kw) for i in range(n)]
+    w = videoio.MjpegAviWriter(str(path), 30, (W, H))
+    for j in jp:
+        w.write_jpeg(j)
+    w.release()
+    return jp
+
+
+def _oracle_written(jp, W, H, box, ksize=5, threshold=12):
+    st = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=box, ksize=ksize, thresh=threshold))
+    counts = [st.step(reference_decode(j))["count"] for j in jp]
+    return written_indices(counts, min_time=0.1, cache_time=0.3)
+
+
+def _read_all(cap):
+    out = []
+    while True:
+        ok, f = cap.read_jpeg() if hasattr(cap, "read_jpeg") else cap.read()
+        if not ok:
+            return out
+        out.append(f)
+
+
+@pytest.mark.parametrize("batch", [1, 8])
+def test_video_motion_on_mjpeg_avi(tmp_path, batch):
+    W, H, n = 480, 270, 48
+    src = tmp_path / "v.avi"
+    jp = _mjpeg_avi(src, W, H, n, 0, quality=85)
+    vm = motion.VideoMotion(filename=str(src), box_size=100, threshold=12, cache_time=0.3, min_time=0.1,
+                            batch=batch, outdir=str(tmp_path))
+    assert isinstance(vm.cap, videoio.MjpegAviCapture)
+    vm.find_motion()
+    want = _oracle_written(jp, W, H, 100)
+    assert want and vm.written_indices == want
+    got = _read_all(videoio.MjpegAviCapture(vm.outfile_name))
+    assert got == [jp[i] for i in want]  # MJPG out: the source's bytes, no re-encode
+
+
+def test_lazy_raw_frames_written_uncompressed(tmp_path):
+    """Codec 'DIB ': every written frame is decoded -- from the engine's input slot while its batch is
+    current, by the one-frame decoder for cached frames of batches already overwritten."""
+    W, H, n = 320, 240, 40
+    src = tmp_path / "v.avi"
+    jp = _mjpeg_avi(src, W, H, n, 1, quality=90, restart_marker_rows=2)
+    vm = motion.VideoMotion(filename=str(src), box_size=100, threshold=12, cache_time=0.3, min_time=0.1,
+                            batch=8, outdir=str(tmp_path), codec="DIB ")
+    vm.find_motion()
+    want = _oracle_written(jp, W, H, 100)
+    assert want and vm.written_indices == want
+    got = _read_all(videoio.RawAviCapture(vm.outfile_name))
+    assert len(got) == len(want)
+    for g, i in zip(got, want):
+        assert np.array_equal(g, reference_decode(jp[i])), i
+
+
+def test_stream_group_on_mjpeg(tmp_path):
+    W, H, n, S = 320, 180, 24, 3
+    srcs = [tmp_path / f"s{s}.avi" for s in range(S)]
+    jps = [_mjpeg_avi(p, W, H, n, s, quality=80, subsampling=1) for s, p in enumerate(srcs)]
+    grp = motion.StreamGroup([str(p) for p in srcs], batch=6, box_size=320, blur_scale=64, threshold=12,
+                             cache_time=0.3, min_time=0.1, outdir=str(tmp_path))
+    grp.find_motion()
+    for s, v in enumerate(grp.videos):
+        assert v.written_indices == _oracle_written(jps[s], W, H, 320), s
+
+
+def test_read_frame_after_submit_and_submit_jpeg():
+    W, H, S, T = 160, 96, 2, 3
+    vids = [SyntheticVideo(W, H, s) for s in range(S)]
+    kw = dict(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    eng = MotionEngine(**kw)
+    frames = np.stack([np.stack([vids[s].frame(t) for s in range(S)]) for t in range(T)])
+    eng.submit(frames)
+    eng.wait()
+    for t in range(T):
+        for s in range(S):
+            assert np.array_equal(eng.read_frame(t, s), frames[t, s])
+    from find_motion_amd import MJpegDecoder
+    dec = MJpegDecoder(W, H, max_frames=T * S)
+    jp = [encode(vids[s].frame(T + t), quality=70) for t in range(T) for s in range(S)]
+    eng.submit_jpeg(dec, jp)
+    eng.wait()
+    for t in range(T):
+        for s in range(S):
+            assert np.array_equal(eng.read_frame(t, s), reference_decode(jp[t * S + s]))
+    dec.close()
+    eng.close()

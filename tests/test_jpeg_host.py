@@ -55,3 +55,37 @@ def test_golden_fixtures():
     for i in range(n):
         data = z[f"jpeg{i}"].tobytes()
         assert np.array_equal(_bgr(jpeg.decode(data)), z[f"bgr{i}"]), i
+
+
+def test_mjpeg_avi_round_trip(tmp_path):
+    """videoio.MjpegAviWriter -> MjpegAviCapture: chunk bytes, count, size and rate survive; open_capture
+    picks the MJPEG reader (the GPU decode path) and open_writer(jpeg=True) the passthrough writer."""
+    from find_motion_amd import videoio
+    W, H = 72, 40
+    jp = [encode(image(H, W, "smooth", seed=s), quality=70 + s) for s in range(5)]  # odd and even lengths
+    p = str(tmp_path / "m.avi")
+    w = videoio.open_writer(p, "MJPG", 25, (W, H), jpeg=True)
+    assert isinstance(w, videoio.MjpegAviWriter)
+    for j in jp[:4]:
+        w.write_jpeg(j)
+    w.write(reference_decode(jp[4]))  # a BGR frame, Pillow-encoded
+    w.release()
+    assert videoio.is_mjpeg_avi(p) and not videoio.is_mjpeg_avi(str(tmp_path / "none.avi"))
+    cap = videoio.open_capture(p)
+    assert isinstance(cap, videoio.MjpegAviCapture)
+    assert (cap.get(videoio.CAP_PROP_FRAME_COUNT), cap.get(videoio.CAP_PROP_FRAME_WIDTH),
+            cap.get(videoio.CAP_PROP_FRAME_HEIGHT)) == (5, W, H)
+    assert abs(cap.fps - 25) < 0.01
+    got = []
+    while True:
+        ok, j = cap.read_jpeg()
+        if not ok:
+            break
+        got.append(j)
+    assert got[:4] == jp[:4] and len(got) == 5
+    assert reference_decode(got[4]).shape == (H, W, 3)
+    cap.release()
+    raw = str(tmp_path / "r.avi")
+    videoio.RawAviWriter(raw, 25, (W, H)).release()
+    assert not videoio.is_mjpeg_avi(raw)
+    assert not videoio.MjpegAviCapture(raw).isOpened()  # cv2-like: a capture that failed to open
