@@ -7,15 +7,17 @@
 //   host    marker segments (DQT, DHT, SOF0/1, DRI, SOS) parsed per frame; the entropy-coded bytes
 //           copied into one pinned buffer with byte stuffing and RSTn markers removed, one segment
 //           per restart interval (the whole scan without DRI);
-//   k_jpeg_huff   one lane per segment: Huffman decode (9-bit lookahead tables in LDS, canonical slow
-//           path past 9 bits), DC prediction, zigzag -> natural order; quantized coefficients scattered
-//           (non-zeros only) into a zeroed int16 coefficient buffer [frame][component][block][64];
+//   k_jpeg_huff   self-synchronizing parallel Huffman decode: each segment cut into chunks of CB bits,
+//           one lane per chunk, entry states speculated and fixed up through a chained look-back
+//           (see the kernel); 9-bit lookahead tables in LDS, canonical slow path past 9 bits, DC
+//           prediction; quantized coefficients written in zigzag order, int16 [frame][comp][block][64];
 //   k_jpeg_idct   8 lanes per block: dequantize + jpeg_idct_islow (jidctint.c: CONST_BITS 13,
 //           PASS1_BITS 2, zero-column / zero-row shortcuts, IDCT range-limit table) into component
-//           planes; the block's coefficients are zeroed again for the next call;
-//   k_jpeg_color  one thread per 4 output pixels: fancy upsampling (jdsample.c h2v1/h2v2 with the
-//           edge-replicated context rows of jdmainct.c) and ycc_rgb_convert (jdcolor.c tables) ->
-//           BGR u8 HWC, the cv2.VideoCapture layout, straight into the caller's frame buffer.
+//           planes;
+//   k_jpeg_color  one workgroup per output row, chroma rows staged in LDS, 8 pixels per thread: fancy
+//           upsampling (jdsample.c h2v1/h2v2 with the edge-replicated context rows of jdmainct.c) and
+//           ycc_rgb_convert (jdcolor.c tables) -> BGR u8 HWC, the cv2.VideoCapture layout, straight
+//           into the caller's frame buffer.
 // Supported: 8-bit baseline / extended-sequential Huffman, grayscale or 3-component YCbCr with
 // Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2; restart intervals optional.  Anything else: FM_ENOTSUP.
 #include <algorithm>
@@ -31,9 +33,14 @@ namespace fm {
 namespace jp {
 
 constexpr int kMaxComp = 3;
+constexpr int kLook = 10;                 // lookahead bits of the fast Huffman table
+constexpr uint32_t kFull = 1u << 5;       // fast-table flag: code and extra bits both within kLook bits
 
 struct HuffDev {              // one table as the decoder reads it (LDS image)
-    uint16_t lut[512];        // 9-bit lookahead: (length << 8) | symbol, 0 = longer code
+    // fast table over the next kLook bits: 0 = a code longer than kLook bits; else bits 0-4 = bits
+    // consumed (code + extra bits when kFull, the code alone otherwise), bits 8-15 = the symbol,
+    // bits 16-31 = the extended value (HUFF_EXTEND of the extra bits; kFull only)
+    uint32_t lut[1 << kLook];
     int32_t maxcode[18];      // largest code of each length (-1: none), [17] sentinel
     int32_t valoff[18];       // index into vals of code c of length l: valoff[l] + c
     uint8_t vals[256];
@@ -52,6 +59,8 @@ struct JpegGeom {
     long long frame_blocks;   // coefficient blocks per frame (all components)
     long long frame_plane;    // sample-plane bytes per frame (all components)
     CompDev comp[kMaxComp];
+    int bpm;                  // blocks per MCU (1 for a one-component scan)
+    int8_t ucomp[10], udv[10], udh[10];  // block u of an MCU: component and offset in the MCU's block grid
 };
 
 struct Seg {
@@ -61,123 +70,357 @@ struct Seg {
     int32_t mcu0, nmcu;       // MCUs the segment holds
 };
 
+// look-back record of a tile of 64 chunks (published by its last lane)
+struct TileState {
+    uint32_t flag;            // 1 once the fields below are valid
+    uint32_t p;               // exit bit position of the tile's last chunk (segment-relative)
+    int32_t uk;               // exit state: block u of the MCU * 64 + coefficient index k
+    int32_t cnt;              // blocks started from the segment start through the tile (inclusive)
+    int32_t dc[kMaxComp];     // DC predictors after the tile (sums of differences since the segment start)
+    int32_t pad;
+};
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
-__constant__ uint8_t c_zigzag[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-                                     12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-                                     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-                                     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
-                                     // k past 63 (corrupt runs): a harmless slot, as libjpeg's
-                                     // jpeg_natural_order extra entries
-                                     63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
-
+// MSB-first bit reader that knows its position (bits consumed since the segment start).  The word
+// after the accumulator's bits is loaded one refill ahead, so a refill does not wait on memory.
 struct BitReader {
-    const uint32_t* w;
+    const uint32_t* w;        // next word to fetch
     const uint32_t* lim;
     uint64_t acc;
     int nb;
-    __device__ __forceinline__ void init(const uint8_t* base, uint32_t off, const uint8_t* end) {
-        w = reinterpret_cast<const uint32_t*>(base + (off & ~3u));
-        lim = reinterpret_cast<const uint32_t*>(end);
-        acc = 0;
-        nb = 0;
-        refill();
-        const int skip = (int)(off & 3u) * 8;
-        acc <<= skip;
-        nb -= skip;
-        refill();
+    uint32_t pos;
+    uint32_t nxt;
+    __device__ __forceinline__ uint32_t fetch() {
+        const uint32_t v = *(w < lim ? w : lim - 1);
+        const uint32_t r = w < lim ? v : 0u;
+        w++;
+        return r;
     }
-    __device__ __forceinline__ void refill() {
-        while (nb <= 32) {
-            const uint32_t v = w < lim ? bswap32(*w) : 0u;
-            w++;
-            acc |= (uint64_t)v << (32 - nb);
+    // start at bit p of the segment whose data begins at byte off of the stream
+    __device__ __forceinline__ void init(const uint8_t* stream, uint32_t off, uint32_t p, const uint8_t* end) {
+        const uint32_t b = off + (p >> 3);
+        w = reinterpret_cast<const uint32_t*>(stream + (b & ~3u));
+        lim = reinterpret_cast<const uint32_t*>(end);
+        const uint32_t w0 = fetch(), w1 = fetch();
+        acc = (uint64_t)bswap32(w0) << 32 | bswap32(w1);
+        nxt = fetch();
+        const int sk = (int)(b & 3u) * 8 + (int)(p & 7u);
+        acc <<= sk;
+        nb = 64 - sk;
+        pos = p;
+    }
+    __device__ __forceinline__ void refill() {  // afterwards more than 32 bits are buffered
+        if (nb <= 32) {
+            acc |= (uint64_t)bswap32(nxt) << (32 - nb);
             nb += 32;
+            nxt = fetch();
         }
     }
     __device__ __forceinline__ uint32_t peek(int n) const { return (uint32_t)(acc >> (64 - n)); }
     __device__ __forceinline__ void skip(int n) {
         acc <<= n;
         nb -= n;
+        pos += (uint32_t)n;
     }
     __device__ __forceinline__ int get(int n) {  // n in [0, 16]
-        if (n == 0) return 0;
-        const int v = (int)peek(n);
+        const int v = n ? (int)peek(n) : 0;
         skip(n);
         return v;
     }
 };
 
-__device__ __forceinline__ int huff_decode(BitReader& br, const HuffDev& t) {
-    br.refill();
-    const uint32_t e = t.lut[br.peek(9)];
-    if (e) {
-        br.skip((int)(e >> 8));
-        return (int)(e & 0xFF);
-    }
-    const uint32_t c16 = br.peek(16);
-    for (int l = 10; l <= 16; l++) {
-        const int code = (int)(c16 >> (16 - l));
-        if (code <= t.maxcode[l]) {
-            br.skip(l);
-            return t.vals[(t.valoff[l] + code) & 0xFF];
-        }
-    }
-    br.skip(16);  // not a code: corrupt data (libjpeg warns and returns 0)
-    return 0;
-}
-
 __device__ __forceinline__ int extend(int v, int s) { return (s && v < (1 << (s - 1))) ? v - (1 << s) + 1 : v; }
 
-// one lane per segment; one wave per workgroup (the Huffman tables of this call in LDS)
-__global__ __launch_bounds__(64) void k_jpeg_huff(const uint8_t* __restrict__ stream, uint32_t stream_len,
-                                                   const Seg* __restrict__ segs, int nseg, const HuffDev* __restrict__ tabs,
-                                                   JpegGeom g, int16_t* __restrict__ coef) {
+// a code longer than kLook bits (jdhuff.c jpeg_huff_decode: canonical codes by length) from the next
+// 16 bits: (length << 8) | symbol; length 16 and symbol 0 when no code matches (corrupt data)
+__device__ __forceinline__ int huff_slow(uint32_t c16, const HuffDev& t) {
+#pragma unroll 1
+    for (int l = kLook + 1; l <= 16; l++) {
+        const int code = (int)(c16 >> (16 - l));
+        if (code <= t.maxcode[l]) return l << 8 | t.vals[(t.valoff[l] + code) & 0xFF];
+    }
+    return 16 << 8;
+}
+
+// the per-block tables a lane needs, in LDS
+struct UTab {
+    uint8_t dc[10], ac[10], comp[10];
+};
+
+__device__ __forceinline__ uint64_t pack_state(uint32_t p, int uk) { return (uint64_t)p << 32 | (uint32_t)uk; }
+
+constexpr int kBufStride = 68;  // int16 per lane block buffer (136 B: lanes spread over the LDS banks)
+
+// Decode symbols from state (br.pos, uk) while br.pos < end.  Every symbol is one Huffman code plus
+// its extra bits (jdhuff.c decode_mcu): at k == 0 the DC difference of block u, else one AC
+// run/size (EOB and ZRL included); uk = u * 64 + k.
+// Speculative mode (!WRITE): at the first symbol boundary at or past `mark` the state is recorded as
+// the chunk's entry (p_in, uk_in) and the counters restart: cnt counts DC symbols (blocks started),
+// dc[] sums the DC differences per component from there.
+// WRITE: the entry is exact, cnt = blocks started before it in the segment and dc[] = the DC
+// predictors; coefficients go to the lane's LDS block buffer in zigzag order and each block (or the
+// part of it inside this chunk) is flushed to its place in the coefficient buffer; decoding stops
+// once the segment's `total` blocks are complete.
+template <bool WRITE>
+__device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mark, uint32_t end, const HuffDev* T,
+                                            const UTab& ut, int bpm, int& cnt, int& dc0, int& dc1, int& dc2, uint32_t& p_in,
+                                            int& uk_in, int16_t* buf, int total, const JpegGeom& g, const Seg& sg,
+                                            int16_t* coef) {
+    int u = uk >> 6, k = uk & 63;
+    int kfirst = k;  // first coefficient index of the current block inside this chunk
+    bool marked = WRITE;
+    auto zero_buf = [&]() {
+#pragma unroll
+        for (int i = 0; i < 16; i++) reinterpret_cast<uint2*>(buf)[i] = make_uint2(0, 0);
+    };
+    auto flush = [&](int kb, int ke) {  // coefficients [kb, ke) of block cnt - 1 of the segment
+        const long long n = (long long)sg.mcu0 * bpm + cnt - 1;
+        const int m = (int)(n / bpm), uu = (int)(n - (long long)m * bpm);
+        const int my = m / g.mcux, mx = m - my * g.mcux;
+        const int ci = ut.comp[uu];
+        const CompDev& c = g.comp[ci];
+        const int by = g.interleaved ? my * c.v + g.udv[uu] : my, bx = g.interleaved ? mx * c.h + g.udh[uu] : mx;
+        int16_t* dst = coef + ((size_t)sg.frame * g.frame_blocks + c.coef0 + (long long)by * c.bw + bx) * 64;
+        if (kb == 0 && ke == 64) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint2 a = reinterpret_cast<const uint2*>(buf)[2 * i], b = reinterpret_cast<const uint2*>(buf)[2 * i + 1];
+                reinterpret_cast<uint4*>(dst)[i] = make_uint4(a.x, a.y, b.x, b.y);
+            }
+        } else {
+            for (int i = kb; i < ke; i++) dst[i] = buf[i];
+        }
+    };
+    if (WRITE && k) zero_buf();
+    while (true) {
+        if (!WRITE && !marked && br.pos >= mark) {
+            marked = true;
+            p_in = br.pos;
+            uk_in = u * 64 + k;
+            cnt = 0;
+            dc0 = dc1 = dc2 = 0;
+        }
+        if (br.pos >= end) break;
+        if (WRITE && k == 0 && cnt == total) break;
+        br.refill();
+        const bool isdc = k == 0;
+        const HuffDev& t = T[isdc ? ut.dc[u] : ut.ac[u]];
+        const uint32_t e = t.lut[br.peek(kLook)];
+        int sym, v;
+        if (e & kFull) {
+            br.skip((int)(e & 31));
+            sym = (int)((e >> 8) & 0xFF);
+            v = (int)e >> 16;
+        } else {
+            if (e) {
+                br.skip((int)(e & 31));
+                sym = (int)((e >> 8) & 0xFF);
+            } else {
+                const int ls = huff_slow(br.peek(16), t);
+                br.skip(ls >> 8);
+                sym = ls & 0xFF;
+            }
+            const int sz = isdc ? min(sym, 16) : (sym & 15);
+            v = extend(br.get(sz), sz);
+        }
+        const int r = isdc ? 0 : sym >> 4;
+        const bool val = isdc || (sym & 15);
+        if (isdc) {
+            const int ci = ut.comp[u];
+            // three scalars and selects: an array indexed by ci would live in scratch
+            const int pred = (ci == 0 ? dc0 : ci == 1 ? dc1 : dc2) + v;
+            dc0 = ci == 0 ? pred : dc0;
+            dc1 = ci == 1 ? pred : dc1;
+            dc2 = ci == 2 ? pred : dc2;
+            v = pred;
+            cnt++;
+            if (WRITE) {
+                zero_buf();
+                kfirst = 0;
+            }
+        }
+        if (WRITE && val) buf[min(k + r, 63)] = (int16_t)v;
+        k = (!val && r != 15) ? 64 : k + r + 1;
+        if (k >= 64) {
+            if (WRITE) flush(kfirst, 64);
+            k = 0;
+            u = u + 1 == bpm ? 0 : u + 1;
+        }
+    }
+    if (!WRITE && !marked) {  // a symbol jumped over the whole chunk: it starts (and ends) here
+        p_in = br.pos;
+        uk_in = u * 64 + k;
+        cnt = 0;
+        dc0 = dc1 = dc2 = 0;
+    }
+    if (WRITE && k) flush(kfirst, k);
+    uk = u * 64 + k;
+}
+
+constexpr int kHuffWaves = 4;
+
+// Self-synchronizing parallel Huffman decode (Weissenberger & Schmidt's scheme for JPEG): every
+// segment (a restart interval, or the whole scan) is cut into chunks of CB bits, one lane each,
+// 64 chunks = one tile per wave (tiles taken in order from a counter).
+//   1. speculate: decode from bit start - OV in state (u, k) = (0, 0) up to the chunk start -- Huffman
+//      codes resynchronise, so the state reached there is the true one with high probability -- then
+//      decode the chunk, counting blocks and summing DC differences;
+//   2. fix up: a lane whose entry differs from its predecessor's exit decodes again from that exit
+//      (repeated until no lane changes); the wave's first lane gets its predecessor's exit from the
+//      previous tile's published record (look-back; the chain is exact from each segment's start,
+//      and a tile holding a segment head publishes before it looks back, so waits stay inside one
+//      segment);
+//   3. a segmented scan over the wave gives each chunk its first block index and DC predictors;
+//   4. decode again, writing the coefficients (zigzag order; a block split between chunks is written
+//      in two disjoint coefficient ranges, so nothing needs zeroing beforehand).
+__global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __restrict__ stream, uint32_t stream_len,
+                                                                const Seg* __restrict__ segs, int nseg,
+                                                                const uint32_t* __restrict__ seg_chunk0, int nchunks,
+                                                                const HuffDev* __restrict__ tabs, JpegGeom g, int CB, int OV,
+                                                                TileState* __restrict__ ts, uint32_t* __restrict__ tile_ctr,
+                                                                int16_t* __restrict__ coef) {
     __shared__ HuffDev T[4];
+    __shared__ UTab ut;
+    __shared__ __attribute__((aligned(16))) int16_t bufs[kHuffWaves * 64][kBufStride];
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tabs);
         uint32_t* dst = reinterpret_cast<uint32_t*>(T);
-        for (int i = threadIdx.x; i < (int)(sizeof(T) / 4); i += 64) dst[i] = src[i];
-    }
-    __syncthreads();
-    const int si = blockIdx.x * 64 + threadIdx.x;
-    if (si >= nseg) return;
-    const Seg sg = segs[si];
-    BitReader br;
-    br.init(stream, sg.off, stream + stream_len);
-    int pred[kMaxComp] = {0, 0, 0};
-    int16_t* cf = coef + (size_t)sg.frame * g.frame_blocks * 64;
-    for (int m = sg.mcu0; m < sg.mcu0 + sg.nmcu; m++) {
-        const int my = m / g.mcux, mx = m - my * g.mcux;
-        for (int ci = 0; ci < g.nc; ci++) {
-            const CompDev& c = g.comp[ci];
-            const int nv = g.interleaved ? c.v : 1, nh = g.interleaved ? c.h : 1;
-            for (int v = 0; v < nv; v++) {
-                for (int h = 0; h < nh; h++) {
-                    const int by = g.interleaved ? my * c.v + v : my, bx = g.interleaved ? mx * c.h + h : mx;
-                    int16_t* blk = cf + (size_t)(c.coef0 + (long long)by * c.bw + bx) * 64;
-                    // DC (jdhuff.c decode_mcu: s = HUFF_DECODE; r = GET_BITS(s); s = HUFF_EXTEND(r, s))
-                    const int s0 = huff_decode(br, T[c.dc]);
-                    br.refill();
-                    pred[ci] += extend(br.get(s0), s0);
-                    blk[0] = (int16_t)pred[ci];
-                    const HuffDev& at = T[c.ac];
-                    for (int k = 1; k < 64; k++) {
-                        const int rs = huff_decode(br, at);
-                        const int r = rs >> 4, s = rs & 15;
-                        if (s) {
-                            k += r;
-                            br.refill();
-                            blk[c_zigzag[min(k, 79)]] = (int16_t)extend(br.get(s), s);
-                        } else {
-                            if (r != 15) break;
-                            k += 15;
-                        }
-                    }
-                }
-            }
+        for (int i = threadIdx.x; i < (int)(sizeof(T) / 4); i += blockDim.x) dst[i] = src[i];
+        if (threadIdx.x < 10) {
+            const int u = threadIdx.x < g.bpm ? threadIdx.x : 0;
+            const int ci = g.ucomp[u];
+            ut.comp[threadIdx.x] = (uint8_t)ci;
+            ut.dc[threadIdx.x] = (uint8_t)g.comp[ci].dc;
+            ut.ac[threadIdx.x] = (uint8_t)g.comp[ci].ac;
         }
     }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    int tile = 0;
+    if (lane == 0) tile = (int)atomicAdd(tile_ctr, 1u);
+    tile = __shfl(tile, 0);
+    if (tile * 64 >= nchunks) return;  // the grid's spare waves (whole waves: no barrier follows)
+    const int c = tile * 64 + lane;
+    const bool valid = c < nchunks;
+    // the chunk's segment: last s with seg_chunk0[s] <= c
+    int lo = 0, hi = nseg - 1;
+    const int cc = valid ? c : nchunks - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)seg_chunk0[mid] <= cc) lo = mid; else hi = mid - 1;
+    }
+    const Seg sg = segs[lo];
+    const int j = cc - (int)seg_chunk0[lo];
+    const bool head = j == 0;
+    const uint32_t nbits = sg.len * 8u;
+    const uint32_t cb = (uint32_t)j * (uint32_t)CB;
+    const uint32_t ce = min(cb + (uint32_t)CB, nbits);
+    const uint8_t* send = stream + stream_len;
+    const int bpm = g.bpm;
+    int16_t* buf = bufs[threadIdx.x];
+
+    // 1 + 2: speculate, then fix up until every lane's entry is its predecessor's exit
+    uint64_t want = pack_state(head ? 0u : (cb > (uint32_t)OV ? cb - (uint32_t)OV : 0u), 0);
+    uint32_t mark = head ? 0u : cb;
+    uint64_t st_in = 0, st_out = 0, lb_state = 0;
+    int cnt = 0, dc0 = 0, dc1 = 0, dc2 = 0;
+    int carry_cnt = 0, cd0 = 0, cd1 = 0, cd2 = 0;
+    uint32_t p_in = 0;
+    int uk_in = 0;
+    BitReader br;
+    bool go = true;
+    int phase = 0;  // 0: lane 0 as speculated; 1: lane 0 from the previous tile's record
+    const bool need_lb = __shfl((int)(!head), 0) != 0;
+    int ic, id0, id1, id2, f;
+    auto scan = [&]() {  // segmented inclusive scan of (blocks, DC sums); f = a head at or before the lane
+        ic = cnt;
+        id0 = dc0;
+        id1 = dc1;
+        id2 = dc2;
+        f = head ? 1 : 0;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int pc = __shfl_up(ic, off), p0 = __shfl_up(id0, off), p1 = __shfl_up(id1, off),
+                      p2 = __shfl_up(id2, off), pf = __shfl_up(f, off);
+            if (lane >= off) {
+                if (!f) {
+                    ic += pc;
+                    id0 += p0;
+                    id1 += p1;
+                    id2 += p2;
+                }
+                f |= pf;
+            }
+        }
+    };
+    auto publish = [&]() {
+        TileState* t = ts + tile;
+        t->p = (uint32_t)(st_out >> 32);
+        t->uk = (int)(uint32_t)st_out;
+        t->cnt = ic;
+        t->dc[0] = id0;
+        t->dc[1] = id1;
+        t->dc[2] = id2;
+        __hip_atomic_store(&t->flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    for (int it = 0; it < 256; it++) {  // each pass fixes at least the next lane: <= 2 x 64 passes
+        if (go) {
+            br.init(stream, sg.off, (uint32_t)(want >> 32), send);
+            int uk = (int)(uint32_t)want;
+            run_symbols<false>(br, uk, mark, ce, T, ut, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, buf, 0, g, sg, coef);
+            st_in = pack_state(p_in, uk_in);
+            st_out = pack_state(br.pos, uk);
+        }
+        uint64_t pv = __shfl_up(st_out, 1);
+        if (lane == 0) pv = phase ? lb_state : st_in;
+        const bool mism = valid && !head && pv != st_in;
+        if (__any(mism)) {
+            go = mism;
+            want = pv;
+            mark = (uint32_t)(pv >> 32);
+            continue;
+        }
+        if (phase == 1 || !need_lb) break;
+        // consistent with lane 0's speculation: a tile holding a segment head publishes now
+        scan();
+        if (lane == 63 && valid && f) publish();
+        if (lane == 0) {
+            const TileState* t = ts + tile - 1;
+            while (__hip_atomic_load(&t->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(1);
+            lb_state = pack_state(__hip_atomic_load(&t->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                  __hip_atomic_load(&t->uk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            carry_cnt = __hip_atomic_load(&t->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cd0 = __hip_atomic_load(&t->dc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cd1 = __hip_atomic_load(&t->dc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cd2 = __hip_atomic_load(&t->dc[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        phase = 1;
+        go = false;
+    }
+    // 3. scan with the previous tile's totals for the lanes of lane 0's segment
+    scan();
+    if (need_lb) {
+        carry_cnt = __shfl(carry_cnt, 0);
+        cd0 = __shfl(cd0, 0);
+        cd1 = __shfl(cd1, 0);
+        cd2 = __shfl(cd2, 0);
+        if (!f) {
+            ic += carry_cnt;
+            id0 += cd0;
+            id1 += cd1;
+            id2 += cd2;
+        }
+        if (lane == 63 && valid && !f) publish();
+    } else if (lane == 63 && valid) {
+        publish();
+    }
+    if (!valid) return;
+    // 4. decode once more from the exact entry, writing the coefficients
+    int wcnt = ic - cnt, w0 = id0 - dc0, w1 = id1 - dc1, w2 = id2 - dc2;
+    br.init(stream, sg.off, p_in, send);
+    int wuk = uk_in;
+    run_symbols<true>(br, wuk, 0, ce, T, ut, bpm, wcnt, w0, w1, w2, p_in, uk_in, buf, sg.nmcu * bpm, g, sg, coef);
 }
 
 // jidctint.c constants (CONST_BITS 13)
@@ -221,8 +464,15 @@ __device__ __forceinline__ uint32_t range_idct(int x) {
     return (uint32_t)(v < 128 ? v + 128 : v < 512 ? 255 : v < 896 ? 0 : v - 896);
 }
 
-// 8 lanes per block: lane r runs column r of pass 1, then row r of pass 2
-__global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
+// zigzag position -> natural index, 8 per lane of a block's 8-lane group (the coefficient buffer holds
+// blocks in zigzag order): lane r holds positions 8r .. 8r+7
+__constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040B12u}, {0x211A130Cu, 0x22293028u},
+                               {0x060D141Bu, 0x1C150E07u}, {0x38312A23u, 0x242B3239u}, {0x170F161Du, 0x332C251Eu},
+                               {0x2D343B3Au, 0x2E271F26u}, {0x363D3C35u, 0x3F3E372Fu}};
+
+// 8 lanes per block: lane r loads zigzag positions 8r..8r+7 (16 B) and scatters them to natural order
+// in LDS, runs column r of pass 1, then row r of pass 2
+__global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
                                                     long long nblocks, uint8_t* __restrict__ planes) {
     __shared__ int ws[32][64];
     const long long b = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
@@ -236,12 +486,22 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, c
     const CompDev& c = g.comp[ci];
     const long long ib = rem - c.coef0;
     const int by = (int)(ib / c.bw), bx = (int)(ib - (long long)by * c.bw);
-    int16_t* blk = coef + (size_t)fb * 64;
     const uint16_t* q = qt + ((size_t)frame * kMaxComp + ci) * 64;
+    {
+        const uint4 raw = live ? reinterpret_cast<const uint4*>(coef + (size_t)fb * 64)[r] : make_uint4(0, 0, 0, 0);
+        const uint2 nat = c_zz8[r];
+        const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
+            ws[lb][n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
+        }
+    }
+    __syncthreads();
     // pass 1: column r (jpeg_idct_islow, with the all-zero-AC column shortcut)
     int v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = live ? (int)blk[8 * k + r] * (int)q[8 * k + r] : 0;
+    for (int k = 0; k < 8; k++) v[k] = ws[lb][8 * k + r] * (int)q[8 * k + r];
     if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
 #pragma unroll
         for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = v[0] * 4;
@@ -272,83 +532,125 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, c
     uint8_t* row = planes + (size_t)frame * g.frame_plane + c.plane0 + ((size_t)by * 8 + r) * pw + (size_t)bx * 8;
     reinterpret_cast<uint2*>(row)[0] = make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24,
                                                   px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
-    // leave the coefficient buffer zeroed for the next call (this block's 64 values were read by
-    // the column pass above: their values fed pass 1, so the loads have returned)
-    reinterpret_cast<uint4*>(blk)[r] = make_uint4(0, 0, 0, 0);
 }
 
 __device__ __forceinline__ int clamp255(int x) { return x < 0 ? 0 : x > 255 ? 255 : x; }
 
-// chroma sample (cb or cr) at output pixel (y, x) after fancy upsampling (jdsample.c), from a
-// plane downsampled by (hf, vf) in {1, 2}, real size dw x dh, row pitch pw.  jinit_upsampler uses
-// the fancy filters only when downsampled_width > 2; narrower planes are replicated (h2v1_upsample,
-// h2v2_upsample).
-__device__ __forceinline__ int chroma_at(const uint8_t* p, int pw, int dw, int dh, int hf, int vf, int y, int x) {
-    if (hf == 2 && dw <= 2) return p[(size_t)(y / vf) * pw + (x >> 1)];
-    if (vf == 2) {  // h2v2_fancy_upsample (hf == 2)
-        const int cy = y >> 1;
-        const int fy = (y & 1) ? min(cy + 1, dh - 1) : max(cy - 1, 0);  // the farther context row
-        const uint8_t* n = p + (size_t)cy * pw;
-        const uint8_t* f = p + (size_t)fy * pw;
-        const int cx = x >> 1;
-        const int cs = n[cx] * 3 + f[cx];
-        if ((x & 1) == 0) return cx == 0 ? (cs * 4 + 8) >> 4 : (cs * 3 + n[cx - 1] * 3 + f[cx - 1] + 8) >> 4;
-        return cx == dw - 1 ? (cs * 4 + 7) >> 4 : (cs * 3 + n[cx + 1] * 3 + f[cx + 1] + 7) >> 4;
-    }
-    const uint8_t* n = p + (size_t)y * pw;
-    if (hf == 1) return n[x];
-    const int cx = x >> 1;  // h2v1_fancy_upsample
-    if ((x & 1) == 0) return cx == 0 ? n[0] : (n[cx] * 3 + n[cx - 1] + 1) >> 2;
-    return cx == dw - 1 ? n[cx] : (n[cx] * 3 + n[cx + 1] + 2) >> 2;
+__device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor.c ycc_rgb_convert, BGR
+    const int R = clamp255(Y + ((91881 * cr + 32768) >> 16));
+    const int G = clamp255(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
+    const int B = clamp255(Y + ((116130 * cb + 32768) >> 16));
+    return (uint32_t)B | (uint32_t)G << 8 | (uint32_t)R << 16;
 }
 
-// one thread per 4 output pixels of a row; ycc_rgb_convert (jdcolor.c build_ycc_rgb_table) -> BGR
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g, int n,
+// One workgroup per output row (blockIdx.x) of one frame (blockIdx.y): the chroma rows the row needs
+// (for h2v2 the nearer and the farther context row, jdsample.c) are staged in LDS with dword loads,
+// then each thread converts 8 consecutive pixels (8 Y samples in one load, chroma upsampled from LDS,
+// ycc_rgb_convert) into the BGR row staged in LDS, which is then stored with 16-B stores.
+__global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g,
                                                      uint8_t* __restrict__ out) {
-    const int qpr = (g.W + 3) / 4;  // quads per row
-    const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long total = (long long)n * g.H * qpr;
-    if (id >= total) return;
-    const int frame = (int)(id / ((long long)g.H * qpr));
-    const long long rem = id - (long long)frame * g.H * qpr;
-    const int y = (int)(rem / qpr), x0 = (int)(rem - (long long)y * qpr) * 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // BGR row [W*3, padded to 16], chroma [2][2][cpw]
+    uint8_t* orow = lds;
+    uint8_t* crow = lds + ((g.W * 3 + 15) & ~15);
+    const int y = blockIdx.x, frame = blockIdx.y;
     const uint8_t* fp = planes + (size_t)frame * g.frame_plane;
     const CompDev& cy = g.comp[0];
     const uint8_t* yrow = fp + cy.plane0 + (size_t)y * (cy.bw * 8);
     uint8_t* o = out + ((size_t)frame * g.H + y) * g.W * 3;
-    uint32_t bgr[4];
-    const int nx = min(4, g.W - x0);
-    for (int k = 0; k < 4; k++) {
-        const int x = min(x0 + k, g.W - 1);
-        const int Y = yrow[x];
-        if (g.nc == 1) {
-            bgr[k] = (uint32_t)Y | (uint32_t)Y << 8 | (uint32_t)Y << 16;
-            continue;
+    const bool color = g.nc == 3;
+    int hf = 1, vf = 1, dw = 0, cpw = 0;
+    if (color) {
+        const CompDev& cc = g.comp[1];
+        hf = g.hmax / cc.h;
+        vf = g.vmax / cc.v;
+        dw = (g.W * cc.h + g.hmax - 1) / g.hmax;
+        const int dh = (g.H * cc.v + g.vmax - 1) / g.vmax;
+        cpw = cc.bw * 8;
+        int r0, r1;
+        if (vf == 2) {
+            r0 = y >> 1;
+            r1 = (y & 1) ? min(r0 + 1, dh - 1) : max(r0 - 1, 0);
+        } else {
+            r0 = r1 = y;
         }
-        const CompDev& ccb = g.comp[1];
-        const CompDev& ccr = g.comp[2];
-        const int hf = g.hmax / ccb.h, vf = g.vmax / ccb.v;
-        const int dw = (g.W * ccb.h + g.hmax - 1) / g.hmax, dh = (g.H * ccb.v + g.vmax - 1) / g.vmax;
-        const int cb = chroma_at(fp + ccb.plane0, ccb.bw * 8, dw, dh, hf, vf, y, x) - 128;
-        const int cr = chroma_at(fp + ccr.plane0, ccr.bw * 8, dw, dh, hf, vf, y, x) - 128;
-        const int R = clamp255(Y + ((91881 * cr + 32768) >> 16));
-        const int G = clamp255(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-        const int B = clamp255(Y + ((116130 * cb + 32768) >> 16));
-        bgr[k] = (uint32_t)B | (uint32_t)G << 8 | (uint32_t)R << 16;
+        const int nw = cpw >> 2;  // dwords per row
+        for (int i = threadIdx.x; i < 4 * nw; i += 256) {
+            const int comp = i / (2 * nw), rr = (i / nw) & 1, x4 = i - (i / nw) * nw;
+            const CompDev& c = g.comp[1 + comp];
+            const uint32_t v = reinterpret_cast<const uint32_t*>(fp + c.plane0 + (size_t)(rr ? r1 : r0) * cpw)[x4];
+            reinterpret_cast<uint32_t*>(crow)[i] = v;
+        }
+        __syncthreads();
     }
-    uint8_t* dst = o + (size_t)x0 * 3;
-    if (ALIGNED && nx == 4) {  // 12 B at a 4-B aligned address: three dwords
-        uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-        d32[0] = bgr[0] | bgr[1] << 24;
-        d32[1] = bgr[1] >> 8 | bgr[2] << 16;
-        d32[2] = bgr[2] >> 16 | bgr[3] << 8;
-    } else {
-        for (int k = 0; k < nx; k++) {
-            dst[3 * k] = (uint8_t)bgr[k];
-            dst[3 * k + 1] = (uint8_t)(bgr[k] >> 8);
-            dst[3 * k + 2] = (uint8_t)(bgr[k] >> 16);
+    for (int x0 = threadIdx.x * 8; x0 < g.W; x0 += 256 * 8) {
+        const uint2 yy = *reinterpret_cast<const uint2*>(yrow + x0);
+        uint32_t bgr[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int Y = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 0xFF);
+            if (!color) {
+                bgr[i] = (uint32_t)Y * 0x010101u;
+                continue;
+            }
+            const int x = x0 + i;
+            int cbv, crv;
+#pragma unroll
+            for (int comp = 0; comp < 2; comp++) {
+                const uint8_t* n = crow + (2 * comp) * cpw;
+                const uint8_t* f = n + cpw;
+                int v;
+                if (hf == 1) {
+                    v = n[x];
+                } else if (dw <= 2) {
+                    v = n[x >> 1];  // narrow planes are replicated (h2v1_upsample / h2v2_upsample)
+                } else if (vf == 2) {  // h2v2_fancy_upsample
+                    const int cx = x >> 1;
+                    const int cs = n[cx] * 3 + f[cx];
+                    if ((x & 1) == 0)
+                        v = cx == 0 ? (cs * 4 + 8) >> 4 : (cs * 3 + n[cx - 1] * 3 + f[cx - 1] + 8) >> 4;
+                    else
+                        v = cx == dw - 1 ? (cs * 4 + 7) >> 4 : (cs * 3 + n[cx + 1] * 3 + f[cx + 1] + 7) >> 4;
+                } else {  // h2v1_fancy_upsample
+                    const int cx = x >> 1;
+                    if ((x & 1) == 0)
+                        v = cx == 0 ? n[0] : (n[cx] * 3 + n[cx - 1] + 1) >> 2;
+                    else
+                        v = cx == dw - 1 ? n[cx] : (n[cx] * 3 + n[cx + 1] + 2) >> 2;
+                }
+                if (comp == 0) cbv = v - 128; else crv = v - 128;
+            }
+            bgr[i] = ycc_bgr(Y, cbv, crv);
         }
+        uint8_t* dst = orow + (size_t)x0 * 3;
+        if (x0 + 8 <= g.W) {  // 24 B at a 4-B aligned LDS address
+            uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t* b = bgr + 4 * h;
+                d32[3 * h] = b[0] | b[1] << 24;
+                d32[3 * h + 1] = b[1] >> 8 | b[2] << 16;
+                d32[3 * h + 2] = b[2] >> 16 | b[3] << 8;
+            }
+        } else {
+            const int nx = min(8, g.W - x0);
+            for (int k = 0; k < nx; k++) {
+                dst[3 * k] = (uint8_t)bgr[k];
+                dst[3 * k + 1] = (uint8_t)(bgr[k] >> 8);
+                dst[3 * k + 2] = (uint8_t)(bgr[k] >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    const int nbytes = g.W * 3;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(o) | (uintptr_t)nbytes;
+    if ((al & 15) == 0) {
+        for (int i = threadIdx.x; i < nbytes / 16; i += 256)
+            reinterpret_cast<uint4*>(o)[i] = reinterpret_cast<const uint4*>(orow)[i];
+    } else if ((al & 3) == 0) {
+        for (int i = threadIdx.x; i < nbytes / 4; i += 256)
+            reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(orow)[i];
+    } else {
+        for (int i = threadIdx.x; i < nbytes; i += 256) o[i] = orow[i];
     }
 }
 
@@ -373,6 +675,11 @@ struct fm_mjpeg {
     size_t stream_cap = 0;
     Seg* d_segs = nullptr;
     size_t segs_cap = 0;
+    uint32_t* d_chunk0 = nullptr;      // [nseg + 1] first chunk of each segment
+    size_t chunk0_cap = 0;
+    TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
+    size_t ts_cap = 0;
+    int CB = 1024, OV = 512;           // chunk and speculation lengths in bits (FM_JPEG_CB / FM_JPEG_OV)
     HuffDev* d_tabs = nullptr;         // [n_sets][4]
     int tabs_cap = 0;
     uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
@@ -384,6 +691,8 @@ struct fm_mjpeg {
     size_t h_stream_cap = 0;
     Seg* h_segs = nullptr;
     size_t h_segs_cap = 0;
+    uint32_t* h_chunk0 = nullptr;
+    size_t h_chunk0_cap = 0;
     HuffDev* h_tabs = nullptr;
     uint16_t* h_qt = nullptr;
     float last_ms = 0.f;
@@ -523,15 +832,25 @@ int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) 
     return jfail(d, FM_EINVAL, "frame %d: no scan", idx);
 }
 
-void build_table(const HuffHost& h, HuffDev& t) {
+void build_table(const HuffHost& h, HuffDev& t, bool dc) {
     memset(&t, 0, sizeof t);
     int code = 0, k = 0;
     for (int l = 1; l <= 16; l++) {
         t.valoff[l] = k - code;
         for (int j = 0; j < h.bits[l]; j++) {
-            if (l <= 9) {
-                const int lo = code << (9 - l), hi = (code + 1) << (9 - l);
-                for (int x = lo; x < hi && x < 512; x++) t.lut[x] = (uint16_t)((l << 8) | h.vals[k]);
+            if (l <= kLook) {
+                const int sym = h.vals[k];
+                const int s = dc ? std::min(sym, 16) : (sym & 15);
+                for (int sfx = 0; sfx < (1 << (kLook - l)); sfx++) {
+                    const int idx = (code << (kLook - l)) | sfx;
+                    uint32_t e = (uint32_t)l | (uint32_t)sym << 8;
+                    if (l + s <= kLook) {
+                        const int extra = s ? (sfx >> (kLook - l - s)) & ((1 << s) - 1) : 0;
+                        const int v = (s && extra < (1 << (s - 1))) ? extra - (1 << s) + 1 : extra;
+                        e = (uint32_t)(l + s) | kFull | (uint32_t)sym << 8 | (uint32_t)(uint16_t)(int16_t)v << 16;
+                    }
+                    t.lut[idx] = e;
+                }
             }
             code++;
             k++;
@@ -611,6 +930,19 @@ int setup_geometry(fm_mjpeg* d, const ParsedJpeg& J) {
     }
     g.frame_blocks = blocks;
     g.frame_plane = (plane + 15) & ~15ll;
+    g.bpm = 0;
+    if (g.interleaved) {
+        for (int c = 0; c < J.nc; c++)
+            for (int v = 0; v < J.cv[c]; v++)
+                for (int h = 0; h < J.ch[c]; h++) {
+                    g.ucomp[g.bpm] = (int8_t)c;
+                    g.udv[g.bpm] = (int8_t)v;
+                    g.udh[g.bpm] = (int8_t)h;
+                    g.bpm++;
+                }
+    } else {
+        g.bpm = 1;
+    }
     const size_t nb = (size_t)d->max_frames * blocks * 64;
     JHIP(d, hipMalloc((void**)&d->d_coef, nb * sizeof(int16_t)));
     JHIP(d, hipMemsetAsync(d->d_coef, 0, nb * sizeof(int16_t), d->st));
@@ -641,6 +973,8 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
     JHIP(d, hipEventCreate(&d->e0));
     JHIP(d, hipEventCreate(&d->e1));
     JHIP(d, hipHostMalloc((void**)&d->h_tabs, 4 * sizeof(HuffDev), hipHostMallocDefault));
+    if (const char* e = getenv("FM_JPEG_CB")) d->CB = std::max(64, atoi(e));
+    if (const char* e = getenv("FM_JPEG_OV")) d->OV = std::max(0, atoi(e));
     return FM_OK;
 }
 
@@ -648,9 +982,9 @@ void fm_mjpeg_destroy(fm_mjpeg* d) {
     if (!d) return;
     if (d->st) (void)hipStreamSynchronize(d->st);
     for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef,
-                    (void*)d->d_planes, (void*)d->d_out})
+                    (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)d->h_stream, (void*)d->h_segs, (void*)d->h_tabs, (void*)d->h_qt})
+    for (void* p : {(void*)d->h_stream, (void*)d->h_segs, (void*)d->h_tabs, (void*)d->h_qt, (void*)d->h_chunk0})
         if (p) (void)hipHostFree(p);
     if (d->e0) (void)hipEventDestroy(d->e0);
     if (d->e1) (void)hipEventDestroy(d->e1);
@@ -716,8 +1050,8 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         d->g.comp[c].ac = 2 + (sel[c][1] & 1);
     }
     for (int t = 0; t < 2; t++) {
-        build_table(P[0].ht[0][t], d->h_tabs[t]);
-        build_table(P[0].ht[1][t], d->h_tabs[2 + t]);
+        build_table(P[0].ht[0][t], d->h_tabs[t], true);
+        build_table(P[0].ht[1][t], d->h_tabs[2 + t], false);
     }
     // entropy-coded bytes: stuffing and RSTn removed, one segment per restart interval
     if (int rc = grow_host(d, &d->h_stream, d->h_stream_cap, total + 16)) return rc;
@@ -768,30 +1102,42 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     if (w >= (size_t)UINT32_MAX) return jfail(d, FM_ENOTSUP, "compressed batch too large");
     if (int rc = grow_host(d, &d->h_segs, d->h_segs_cap, segs.size())) return rc;
     memcpy(d->h_segs, segs.data(), segs.size() * sizeof(Seg));
+    // chunks of CB bits per segment (at least one), 64 per tile
+    const int nseg = (int)segs.size();
+    if (int rc = grow_host(d, &d->h_chunk0, d->h_chunk0_cap, (size_t)nseg + 1)) return rc;
+    size_t nchunks = 0;
+    for (int i = 0; i < nseg; i++) {
+        d->h_chunk0[i] = (uint32_t)nchunks;
+        nchunks += std::max<size_t>(1, ((size_t)segs[i].len * 8 + d->CB - 1) / d->CB);
+    }
+    d->h_chunk0[nseg] = (uint32_t)nchunks;
+    if (nchunks >= (size_t)INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "compressed batch too large");
+    const size_t ntiles = (nchunks + 63) / 64;
     if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + 8)) return rc;  // word reads may pass w by 3 B
     if (int rc = grow_dev(d, &d->d_segs, d->segs_cap, segs.size())) return rc;
+    if (int rc = grow_dev(d, &d->d_chunk0, d->chunk0_cap, (size_t)nseg + 1)) return rc;
+    if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + 1)) return rc;
     size_t tcap = d->tabs_cap;
     if (int rc = grow_dev(d, &d->d_tabs, tcap, 4)) return rc;
     d->tabs_cap = (int)tcap;
     JHIP(d, hipMemcpyAsync(d->d_stream, d->h_stream, w, hipMemcpyHostToDevice, st));
     JHIP(d, hipMemcpyAsync(d->d_segs, d->h_segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_chunk0, d->h_chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemsetAsync(d->d_ts, 0, (ntiles + 1) * sizeof(TileState), st));  // flags + the tile counter
     JHIP(d, hipMemcpyAsync(d->d_tabs, d->h_tabs, 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
     JHIP(d, hipMemcpyAsync(d->d_qt, d->h_qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
     if (d->timing) JHIP(d, hipEventRecord(d->e0, st));
-    const int nseg = (int)segs.size();
-    hipLaunchKernelGGL(k_jpeg_huff, dim3((nseg + 63) / 64), dim3(64), 0, st, d->d_stream, (uint32_t)w, d->d_segs, nseg,
-                       d->d_tabs, d->g, d->d_coef);
+    hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((ntiles + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
+                       d->d_stream, (uint32_t)w, d->d_segs, nseg, d->d_chunk0, (int)nchunks, d->d_tabs, d->g, d->CB,
+                       d->OV, d->d_ts, reinterpret_cast<uint32_t*>(d->d_ts + ntiles), d->d_coef);
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
     hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 31) / 32)), dim3(256), 0, st, d->d_coef, d->d_qt, d->g, nb,
                        d->d_planes);
     JHIP(d, hipGetLastError());
-    const long long nq = (long long)n * g.H * ((g.W + 3) / 4);
-    const bool aligned = ((uintptr_t)out & 3) == 0 && (g.W * 3) % 4 == 0;
-    if (aligned)
-        hipLaunchKernelGGL(k_jpeg_color<true>, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, d->d_planes, d->g, n, out);
-    else
-        hipLaunchKernelGGL(k_jpeg_color<false>, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, d->d_planes, d->g, n, out);
+    const size_t lds = (((size_t)g.W * 3 + 15) & ~(size_t)15) + (g.nc == 3 ? 4 * (size_t)g.comp[1].bw * 8 : 0);
+    if (lds > 64 * 1024) return jfail(d, FM_ENOTSUP, "frame width %d too large for the colour kernel", g.W);
+    hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)g.H, (unsigned)n), dim3(256), lds, st, d->d_planes, d->g, out);
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
     return FM_OK;
