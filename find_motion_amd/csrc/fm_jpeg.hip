@@ -33,6 +33,7 @@ namespace fm {
 namespace jp {
 
 constexpr int kMaxComp = 3;
+constexpr int kStreamSlack = 64;          // bytes allocated past the stream buffer's length
 constexpr int kLook = 10;                 // lookahead bits of the fast Huffman table
 constexpr uint32_t kFull = 1u << 5;       // fast-table flag: code and extra bits both within kLook bits
 
@@ -84,24 +85,20 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap
 
 // MSB-first bit reader that knows its position (bits consumed since the segment start).  The word
 // after the accumulator's bits is loaded one refill ahead, so a refill does not wait on memory.
+// Reads run at most 16 bytes past the last segment's padding: the stream buffer has kStreamSlack
+// bytes beyond its length.
 struct BitReader {
     const uint32_t* w;        // next word to fetch
-    const uint32_t* lim;
     uint64_t acc;
     int nb;
     uint32_t pos;
     uint32_t nxt;
-    __device__ __forceinline__ uint32_t fetch() {
-        const uint32_t v = *(w < lim ? w : lim - 1);
-        const uint32_t r = w < lim ? v : 0u;
-        w++;
-        return r;
-    }
+    __device__ __forceinline__ uint32_t fetch() { return *w++; }
     // start at bit p of the segment whose data begins at byte off of the stream
     __device__ __forceinline__ void init(const uint8_t* stream, uint32_t off, uint32_t p, const uint8_t* end) {
         const uint32_t b = off + (p >> 3);
         w = reinterpret_cast<const uint32_t*>(stream + (b & ~3u));
-        lim = reinterpret_cast<const uint32_t*>(end);
+        (void)end;
         const uint32_t w0 = fetch(), w1 = fetch();
         acc = (uint64_t)bswap32(w0) << 32 | bswap32(w1);
         nxt = fetch();
@@ -150,8 +147,6 @@ struct UTab {
 
 __device__ __forceinline__ uint64_t pack_state(uint32_t p, int uk) { return (uint64_t)p << 32 | (uint32_t)uk; }
 
-constexpr int kBufStride = 68;  // int16 per lane block buffer (136 B: lanes spread over the LDS banks)
-
 // Decode symbols from state (br.pos, uk) while br.pos < end.  Every symbol is one Huffman code plus
 // its extra bits (jdhuff.c decode_mcu): at k == 0 the DC difference of block u, else one AC
 // run/size (EOB and ZRL included); uk = u * 64 + k.
@@ -162,37 +157,32 @@ constexpr int kBufStride = 68;  // int16 per lane block buffer (136 B: lanes spr
 // predictors; coefficients go to the lane's LDS block buffer in zigzag order and each block (or the
 // part of it inside this chunk) is flushed to its place in the coefficient buffer; decoding stops
 // once the segment's `total` blocks are complete.
+// the coefficient block (zigzag order) of block n of segment sg
+__device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, const UTab& ut, const Seg& sg, int bpm, int n) {
+    const long long a = (long long)sg.mcu0 * bpm + n;
+    const int m = (int)(a / bpm), uu = (int)(a - (long long)m * bpm);
+    const int my = m / g.mcux, mx = m - my * g.mcux;
+    const CompDev& c = g.comp[ut.comp[uu]];
+    const int by = g.interleaved ? my * c.v + g.udv[uu] : my, bx = g.interleaved ? mx * c.h + g.udh[uu] : mx;
+    return coef + ((size_t)sg.frame * g.frame_blocks + c.coef0 + (long long)by * c.bw + bx) * 64;
+}
+
+// Decode symbols from state (br.pos, uk) while br.pos < end.  Every symbol is one Huffman code plus
+// its extra bits (jdhuff.c decode_mcu): at k == 0 the DC difference of block u, else one AC
+// run/size (EOB and ZRL included); uk = u * 64 + k.
+// Speculative mode (!WRITE): at the first symbol boundary at or past `mark` the state is recorded as
+// the chunk's entry (p_in, uk_in) and the counters restart: cnt counts DC symbols (blocks started),
+// dc0..dc2 sum the DC differences per component from there.
+// WRITE: the entry is exact, cnt = blocks started before it in the segment and dc0..dc2 = the DC
+// predictors; each value is stored at its zigzag position of its block in the (zeroed) coefficient
+// buffer; decoding stops once the segment's `total` blocks are complete.
 template <bool WRITE>
 __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mark, uint32_t end, const HuffDev* T,
                                             const UTab& ut, int bpm, int& cnt, int& dc0, int& dc1, int& dc2, uint32_t& p_in,
-                                            int& uk_in, int16_t* buf, int total, const JpegGeom& g, const Seg& sg,
-                                            int16_t* coef) {
+                                            int& uk_in, int total, const JpegGeom& g, const Seg& sg, int16_t* coef) {
     int u = uk >> 6, k = uk & 63;
-    int kfirst = k;  // first coefficient index of the current block inside this chunk
     bool marked = WRITE;
-    auto zero_buf = [&]() {
-#pragma unroll
-        for (int i = 0; i < 16; i++) reinterpret_cast<uint2*>(buf)[i] = make_uint2(0, 0);
-    };
-    auto flush = [&](int kb, int ke) {  // coefficients [kb, ke) of block cnt - 1 of the segment
-        const long long n = (long long)sg.mcu0 * bpm + cnt - 1;
-        const int m = (int)(n / bpm), uu = (int)(n - (long long)m * bpm);
-        const int my = m / g.mcux, mx = m - my * g.mcux;
-        const int ci = ut.comp[uu];
-        const CompDev& c = g.comp[ci];
-        const int by = g.interleaved ? my * c.v + g.udv[uu] : my, bx = g.interleaved ? mx * c.h + g.udh[uu] : mx;
-        int16_t* dst = coef + ((size_t)sg.frame * g.frame_blocks + c.coef0 + (long long)by * c.bw + bx) * 64;
-        if (kb == 0 && ke == 64) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint2 a = reinterpret_cast<const uint2*>(buf)[2 * i], b = reinterpret_cast<const uint2*>(buf)[2 * i + 1];
-                reinterpret_cast<uint4*>(dst)[i] = make_uint4(a.x, a.y, b.x, b.y);
-            }
-        } else {
-            for (int i = kb; i < ke; i++) dst[i] = buf[i];
-        }
-    };
-    if (WRITE && k) zero_buf();
+    int16_t* blk = (WRITE && k) ? block_ptr(coef, g, ut, sg, bpm, cnt - 1) : coef;
     while (true) {
         if (!WRITE && !marked && br.pos >= mark) {
             marked = true;
@@ -227,23 +217,19 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
         const int r = isdc ? 0 : sym >> 4;
         const bool val = isdc || (sym & 15);
         if (isdc) {
-            const int ci = ut.comp[u];
             // three scalars and selects: an array indexed by ci would live in scratch
+            const int ci = ut.comp[u];
             const int pred = (ci == 0 ? dc0 : ci == 1 ? dc1 : dc2) + v;
             dc0 = ci == 0 ? pred : dc0;
             dc1 = ci == 1 ? pred : dc1;
             dc2 = ci == 2 ? pred : dc2;
             v = pred;
+            if (WRITE) blk = block_ptr(coef, g, ut, sg, bpm, cnt);
             cnt++;
-            if (WRITE) {
-                zero_buf();
-                kfirst = 0;
-            }
         }
-        if (WRITE && val) buf[min(k + r, 63)] = (int16_t)v;
+        if (WRITE && val && v) blk[min(k + r, 63)] = (int16_t)v;
         k = (!val && r != 15) ? 64 : k + r + 1;
         if (k >= 64) {
-            if (WRITE) flush(kfirst, 64);
             k = 0;
             u = u + 1 == bpm ? 0 : u + 1;
         }
@@ -254,7 +240,6 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
         cnt = 0;
         dc0 = dc1 = dc2 = 0;
     }
-    if (WRITE && k) flush(kfirst, k);
     uk = u * 64 + k;
 }
 
@@ -272,8 +257,8 @@ constexpr int kHuffWaves = 4;
 //      and a tile holding a segment head publishes before it looks back, so waits stay inside one
 //      segment);
 //   3. a segmented scan over the wave gives each chunk its first block index and DC predictors;
-//   4. decode again, writing the coefficients (zigzag order; a block split between chunks is written
-//      in two disjoint coefficient ranges, so nothing needs zeroing beforehand).
+//   4. decode again, storing the non-zero quantized coefficients (zigzag order) into the coefficient
+//      buffer, which k_jpeg_idct leaves zeroed behind it.
 __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __restrict__ stream, uint32_t stream_len,
                                                                 const Seg* __restrict__ segs, int nseg,
                                                                 const uint32_t* __restrict__ seg_chunk0, int nchunks,
@@ -282,7 +267,6 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
                                                                 int16_t* __restrict__ coef) {
     __shared__ HuffDev T[4];
     __shared__ UTab ut;
-    __shared__ __attribute__((aligned(16))) int16_t bufs[kHuffWaves * 64][kBufStride];
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tabs);
         uint32_t* dst = reinterpret_cast<uint32_t*>(T);
@@ -318,7 +302,6 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     const uint32_t ce = min(cb + (uint32_t)CB, nbits);
     const uint8_t* send = stream + stream_len;
     const int bpm = g.bpm;
-    int16_t* buf = bufs[threadIdx.x];
 
     // 1 + 2: speculate, then fix up until every lane's entry is its predecessor's exit
     uint64_t want = pack_state(head ? 0u : (cb > (uint32_t)OV ? cb - (uint32_t)OV : 0u), 0);
@@ -368,7 +351,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         if (go) {
             br.init(stream, sg.off, (uint32_t)(want >> 32), send);
             int uk = (int)(uint32_t)want;
-            run_symbols<false>(br, uk, mark, ce, T, ut, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, buf, 0, g, sg, coef);
+            run_symbols<false>(br, uk, mark, ce, T, ut, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, 0, g, sg, coef);
             st_in = pack_state(p_in, uk_in);
             st_out = pack_state(br.pos, uk);
         }
@@ -420,7 +403,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     int wcnt = ic - cnt, w0 = id0 - dc0, w1 = id1 - dc1, w2 = id2 - dc2;
     br.init(stream, sg.off, p_in, send);
     int wuk = uk_in;
-    run_symbols<true>(br, wuk, 0, ce, T, ut, bpm, wcnt, w0, w1, w2, p_in, uk_in, buf, sg.nmcu * bpm, g, sg, coef);
+    run_symbols<true>(br, wuk, 0, ce, T, ut, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef);
 }
 
 // jidctint.c constants (CONST_BITS 13)
@@ -472,7 +455,7 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 
 // 8 lanes per block: lane r loads zigzag positions 8r..8r+7 (16 B) and scatters them to natural order
 // in LDS, runs column r of pass 1, then row r of pass 2
-__global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
+__global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
                                                     long long nblocks, uint8_t* __restrict__ planes) {
     __shared__ int ws[32][64];
     const long long b = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
@@ -489,6 +472,8 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ c
     const uint16_t* q = qt + ((size_t)frame * kMaxComp + ci) * 64;
     {
         const uint4 raw = live ? reinterpret_cast<const uint4*>(coef + (size_t)fb * 64)[r] : make_uint4(0, 0, 0, 0);
+        // leave the block zeroed for the next call's sparse coefficient stores
+        if (live) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
         const uint2 nat = c_zz8[r];
         const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
@@ -1113,7 +1098,7 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     d->h_chunk0[nseg] = (uint32_t)nchunks;
     if (nchunks >= (size_t)INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "compressed batch too large");
     const size_t ntiles = (nchunks + 63) / 64;
-    if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + 8)) return rc;  // word reads may pass w by 3 B
+    if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + kStreamSlack)) return rc;  // look-ahead reads
     if (int rc = grow_dev(d, &d->d_segs, d->segs_cap, segs.size())) return rc;
     if (int rc = grow_dev(d, &d->d_chunk0, d->chunk0_cap, (size_t)nseg + 1)) return rc;
     if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + 1)) return rc;
