@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fm_internal.h"
@@ -34,6 +35,7 @@ namespace jp {
 
 constexpr int kMaxComp = 3;
 constexpr int kStreamSlack = 64;          // bytes allocated past the stream buffer's length
+constexpr int kSegPad = 16;               // zero bytes after each segment's data (look-ahead reads)
 constexpr int kLook = 10;                 // lookahead bits of the fast Huffman table
 constexpr uint32_t kFull = 1u << 5;       // fast-table flag: code and extra bits both within kLook bits
 
@@ -528,114 +530,189 @@ __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor
     return (uint32_t)B | (uint32_t)G << 8 | (uint32_t)R << 16;
 }
 
-// One workgroup per output row (blockIdx.x) of one frame (blockIdx.y): the chroma rows the row needs
-// (for h2v2 the nearer and the farther context row, jdsample.c) are staged in LDS with dword loads,
-// then each thread converts 8 consecutive pixels (8 Y samples in one load, chroma upsampled from LDS,
-// ycc_rgb_convert) into the BGR row staged in LDS, which is then stored with 16-B stores.
-__global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g,
+// One workgroup per band of `rb` output rows (blockIdx.x) of one frame (blockIdx.y).  The band's Y
+// rows and the chroma rows it needs (for h2v2 also the context rows above and below, jdsample.c
+// with jdmainct.c's edge replication) are staged in LDS with 8-byte loads, all in flight together;
+// then row by row each thread converts 8 consecutive pixels (chroma upsampled from LDS,
+// ycc_rgb_convert) into a BGR row in LDS (two of them, alternating), stored with 16-byte stores.
+__global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g, int rb,
                                                      uint8_t* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // BGR row [W*3, padded to 16], chroma [2][2][cpw]
-    uint8_t* orow = lds;
-    uint8_t* crow = lds + ((g.W * 3 + 15) & ~15);
-    const int y = blockIdx.x, frame = blockIdx.y;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int y0 = blockIdx.x * rb, frame = blockIdx.y;
+    const int y1 = min(y0 + rb, g.H);
     const uint8_t* fp = planes + (size_t)frame * g.frame_plane;
     const CompDev& cy = g.comp[0];
-    const uint8_t* yrow = fp + cy.plane0 + (size_t)y * (cy.bw * 8);
-    uint8_t* o = out + ((size_t)frame * g.H + y) * g.W * 3;
+    const int ypw = cy.bw * 8;
+    const int wr = (g.W + 7) & ~7;           // Y bytes staged per row
+    const int orow_sz = (g.W * 3 + 15) & ~15;
+    uint8_t* orow = lds;                     // [2][orow_sz]
+    uint8_t* ys = lds + 2 * orow_sz;         // [rb][wr]
+    uint8_t* cs = ys + rb * wr;              // [2 comps][nr][cpw]
     const bool color = g.nc == 3;
-    int hf = 1, vf = 1, dw = 0, cpw = 0;
+    int hf = 1, vf = 1, dw = 0, dh = 0, cpw = 0, r_lo = 0, nr = 0;
     if (color) {
         const CompDev& cc = g.comp[1];
         hf = g.hmax / cc.h;
         vf = g.vmax / cc.v;
         dw = (g.W * cc.h + g.hmax - 1) / g.hmax;
-        const int dh = (g.H * cc.v + g.vmax - 1) / g.vmax;
+        dh = (g.H * cc.v + g.vmax - 1) / g.vmax;
         cpw = cc.bw * 8;
-        int r0, r1;
+        int r_hi;
         if (vf == 2) {
-            r0 = y >> 1;
-            r1 = (y & 1) ? min(r0 + 1, dh - 1) : max(r0 - 1, 0);
+            r_lo = max((y0 >> 1) - 1, 0);
+            r_hi = min(((y1 - 1) >> 1) + 1, dh - 1);
         } else {
-            r0 = r1 = y;
+            r_lo = y0;
+            r_hi = y1 - 1;
         }
-        const int nw = cpw >> 2;  // dwords per row
-        for (int i = threadIdx.x; i < 4 * nw; i += 256) {
-            const int comp = i / (2 * nw), rr = (i / nw) & 1, x4 = i - (i / nw) * nw;
-            const CompDev& c = g.comp[1 + comp];
-            const uint32_t v = reinterpret_cast<const uint32_t*>(fp + c.plane0 + (size_t)(rr ? r1 : r0) * cpw)[x4];
-            reinterpret_cast<uint32_t*>(crow)[i] = v;
-        }
-        __syncthreads();
+        nr = r_hi - r_lo + 1;
     }
-    for (int x0 = threadIdx.x * 8; x0 < g.W; x0 += 256 * 8) {
-        const uint2 yy = *reinterpret_cast<const uint2*>(yrow + x0);
-        uint32_t bgr[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int Y = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 0xFF);
-            if (!color) {
-                bgr[i] = (uint32_t)Y * 0x010101u;
-                continue;
+    {   // stage: Y rows, then chroma rows (8-byte words)
+        const int yw = wr >> 3, nyw = (y1 - y0) * yw;
+        const int cw = cpw >> 3, ncw = 2 * nr * cw;
+        for (int i = threadIdx.x; i < nyw + ncw; i += 256) {
+            uint2 v;
+            uint8_t* dst;
+            if (i < nyw) {
+                const int r = i / yw, x8 = i - r * yw;
+                v = reinterpret_cast<const uint2*>(fp + cy.plane0 + (size_t)(y0 + r) * ypw)[x8];
+                dst = ys + r * wr + x8 * 8;
+            } else {
+                const int q = i - nyw, comp = q / (nr * cw), rem = q - comp * nr * cw, r = rem / cw, x8 = rem - r * cw;
+                v = reinterpret_cast<const uint2*>(fp + g.comp[1 + comp].plane0 + (size_t)(r_lo + r) * cpw)[x8];
+                dst = cs + (comp * nr + r) * cpw + x8 * 8;
             }
-            const int x = x0 + i;
-            int cbv, crv;
-#pragma unroll
-            for (int comp = 0; comp < 2; comp++) {
-                const uint8_t* n = crow + (2 * comp) * cpw;
-                const uint8_t* f = n + cpw;
-                int v;
-                if (hf == 1) {
-                    v = n[x];
-                } else if (dw <= 2) {
-                    v = n[x >> 1];  // narrow planes are replicated (h2v1_upsample / h2v2_upsample)
-                } else if (vf == 2) {  // h2v2_fancy_upsample
-                    const int cx = x >> 1;
-                    const int cs = n[cx] * 3 + f[cx];
-                    if ((x & 1) == 0)
-                        v = cx == 0 ? (cs * 4 + 8) >> 4 : (cs * 3 + n[cx - 1] * 3 + f[cx - 1] + 8) >> 4;
-                    else
-                        v = cx == dw - 1 ? (cs * 4 + 7) >> 4 : (cs * 3 + n[cx + 1] * 3 + f[cx + 1] + 7) >> 4;
-                } else {  // h2v1_fancy_upsample
-                    const int cx = x >> 1;
-                    if ((x & 1) == 0)
-                        v = cx == 0 ? n[0] : (n[cx] * 3 + n[cx - 1] + 1) >> 2;
-                    else
-                        v = cx == dw - 1 ? n[cx] : (n[cx] * 3 + n[cx + 1] + 2) >> 2;
-                }
-                if (comp == 0) cbv = v - 128; else crv = v - 128;
-            }
-            bgr[i] = ycc_bgr(Y, cbv, crv);
-        }
-        uint8_t* dst = orow + (size_t)x0 * 3;
-        if (x0 + 8 <= g.W) {  // 24 B at a 4-B aligned LDS address
-            uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t* b = bgr + 4 * h;
-                d32[3 * h] = b[0] | b[1] << 24;
-                d32[3 * h + 1] = b[1] >> 8 | b[2] << 16;
-                d32[3 * h + 2] = b[2] >> 16 | b[3] << 8;
-            }
-        } else {
-            const int nx = min(8, g.W - x0);
-            for (int k = 0; k < nx; k++) {
-                dst[3 * k] = (uint8_t)bgr[k];
-                dst[3 * k + 1] = (uint8_t)(bgr[k] >> 8);
-                dst[3 * k + 2] = (uint8_t)(bgr[k] >> 16);
-            }
+            *reinterpret_cast<uint2*>(dst) = v;
         }
     }
     __syncthreads();
     const int nbytes = g.W * 3;
-    const uintptr_t al = reinterpret_cast<uintptr_t>(o) | (uintptr_t)nbytes;
-    if ((al & 15) == 0) {
-        for (int i = threadIdx.x; i < nbytes / 16; i += 256)
-            reinterpret_cast<uint4*>(o)[i] = reinterpret_cast<const uint4*>(orow)[i];
-    } else if ((al & 3) == 0) {
-        for (int i = threadIdx.x; i < nbytes / 4; i += 256)
-            reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(orow)[i];
-    } else {
-        for (int i = threadIdx.x; i < nbytes; i += 256) o[i] = orow[i];
+    for (int y = y0; y < y1; y++) {
+        uint8_t* ob = orow + ((y - y0) & 1) * orow_sz;
+        const uint8_t* yrow = ys + (y - y0) * wr;
+        const uint8_t *n0 = nullptr, *f0 = nullptr;
+        if (color) {
+            int rn, rf;
+            if (vf == 2) {
+                rn = y >> 1;
+                rf = (y & 1) ? min(rn + 1, dh - 1) : max(rn - 1, 0);  // the farther context row
+            } else {
+                rn = rf = y;
+            }
+            n0 = cs + (rn - r_lo) * cpw;
+            f0 = cs + (rf - r_lo) * cpw;
+        }
+        for (int x0 = threadIdx.x * 8; x0 < g.W; x0 += 256 * 8) {
+            const uint2 yy = *reinterpret_cast<const uint2*>(yrow + x0);
+            uint32_t bgr[8];
+            if (color && hf == 2 && dw > 2) {
+                // fancy h2v1 / h2v2 over chroma columns cx0-1 .. cx0+4, read as three LDS words per row
+                const int cx0 = x0 >> 1;
+                int up[2][8];
+#pragma unroll
+                for (int comp = 0; comp < 2; comp++) {
+                    int cs[6];
+#pragma unroll
+                    for (int rr = 0; rr < 2; rr++) {
+                        const uint8_t* row = (rr ? f0 : n0) + comp * nr * cpw;
+                        const uint32_t a = cx0 ? *reinterpret_cast<const uint32_t*>(row + cx0 - 4) : 0u;
+                        const uint32_t b = *reinterpret_cast<const uint32_t*>(row + cx0);
+                        const uint32_t c = *reinterpret_cast<const uint32_t*>(row + cx0 + 4);
+                        const int v6[6] = {(int)(a >> 24), (int)(b & 255), (int)((b >> 8) & 255), (int)((b >> 16) & 255),
+                                           (int)(b >> 24), (int)(c & 255)};
+#pragma unroll
+                        for (int q = 0; q < 6; q++) {
+                            if (vf == 2) cs[q] = rr ? cs[q] + v6[q] : v6[q] * 3;  // 3 * nearer + farther
+                            else if (!rr) cs[q] = v6[q];
+                        }
+                    }
+#pragma unroll
+                    for (int m = 0; m < 4; m++) {
+                        const int cx = cx0 + m;
+                        const int cc = cs[m + 1], cl = cs[m], cr = cs[m + 2];
+                        if (vf == 2) {
+                            up[comp][2 * m] = cx == 0 ? (cc * 4 + 8) >> 4 : (cc * 3 + cl + 8) >> 4;
+                            up[comp][2 * m + 1] = cx == dw - 1 ? (cc * 4 + 7) >> 4 : (cc * 3 + cr + 7) >> 4;
+                        } else {
+                            up[comp][2 * m] = cx == 0 ? cc : (cc * 3 + cl + 1) >> 2;
+                            up[comp][2 * m + 1] = cx == dw - 1 ? cc : (cc * 3 + cr + 2) >> 2;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int Y = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 0xFF);
+                    bgr[i] = ycc_bgr(Y, up[0][i] - 128, up[1][i] - 128);
+                }
+            } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int Y = (int)(((i < 4 ? yy.x : yy.y) >> (8 * (i & 3))) & 0xFF);
+                if (!color) {
+                    bgr[i] = (uint32_t)Y * 0x010101u;
+                    continue;
+                }
+                const int x = x0 + i;
+                int cbv = 0, crv = 0;
+#pragma unroll
+                for (int comp = 0; comp < 2; comp++) {
+                    const uint8_t* n = n0 + comp * nr * cpw;
+                    const uint8_t* f = f0 + comp * nr * cpw;
+                    int v;
+                    if (hf == 1) {
+                        v = n[x];
+                    } else if (dw <= 2) {
+                        v = n[x >> 1];  // narrow planes are replicated (h2v1_upsample / h2v2_upsample)
+                    } else if (vf == 2) {  // h2v2_fancy_upsample
+                        const int cx = x >> 1;
+                        const int c0 = n[cx] * 3 + f[cx];
+                        if ((x & 1) == 0)
+                            v = cx == 0 ? (c0 * 4 + 8) >> 4 : (c0 * 3 + n[cx - 1] * 3 + f[cx - 1] + 8) >> 4;
+                        else
+                            v = cx == dw - 1 ? (c0 * 4 + 7) >> 4 : (c0 * 3 + n[cx + 1] * 3 + f[cx + 1] + 7) >> 4;
+                    } else {  // h2v1_fancy_upsample
+                        const int cx = x >> 1;
+                        if ((x & 1) == 0)
+                            v = cx == 0 ? n[0] : (n[cx] * 3 + n[cx - 1] + 1) >> 2;
+                        else
+                            v = cx == dw - 1 ? n[cx] : (n[cx] * 3 + n[cx + 1] + 2) >> 2;
+                    }
+                    if (comp == 0) cbv = v - 128; else crv = v - 128;
+                }
+                bgr[i] = ycc_bgr(Y, cbv, crv);
+            }
+            }
+            uint8_t* dst = ob + (size_t)x0 * 3;
+            if (x0 + 8 <= g.W) {  // 24 B at a 4-B aligned LDS address
+                uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t* b = bgr + 4 * h;
+                    d32[3 * h] = b[0] | b[1] << 24;
+                    d32[3 * h + 1] = b[1] >> 8 | b[2] << 16;
+                    d32[3 * h + 2] = b[2] >> 16 | b[3] << 8;
+                }
+            } else {
+                const int nx = min(8, g.W - x0);
+                for (int k = 0; k < nx; k++) {
+                    dst[3 * k] = (uint8_t)bgr[k];
+                    dst[3 * k + 1] = (uint8_t)(bgr[k] >> 8);
+                    dst[3 * k + 2] = (uint8_t)(bgr[k] >> 16);
+                }
+            }
+        }
+        __syncthreads();  // (also: every thread is past its stores of the row two back, from this buffer)
+        uint8_t* o = out + ((size_t)frame * g.H + y) * nbytes;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(o) | (uintptr_t)nbytes;
+        if ((al & 15) == 0) {
+            for (int i = threadIdx.x; i < nbytes / 16; i += 256)
+                reinterpret_cast<uint4*>(o)[i] = reinterpret_cast<const uint4*>(ob)[i];
+        } else if ((al & 3) == 0) {
+            for (int i = threadIdx.x; i < nbytes / 4; i += 256)
+                reinterpret_cast<uint32_t*>(o)[i] = reinterpret_cast<const uint32_t*>(ob)[i];
+        } else {
+            for (int i = threadIdx.x; i < nbytes; i += 256) o[i] = ob[i];
+        }
     }
 }
 
@@ -671,15 +748,23 @@ struct fm_mjpeg {
     int16_t* d_coef = nullptr;         // [max_frames][frame_blocks][64]
     uint8_t* d_planes = nullptr;       // [max_frames][frame_plane]
     uint8_t* d_out = nullptr;          // device BGR when the caller wants host output
-    // pinned host staging (reused; the previous call's transfers are finished before refilling)
-    uint8_t* h_stream = nullptr;
-    size_t h_stream_cap = 0;
-    Seg* h_segs = nullptr;
-    size_t h_segs_cap = 0;
-    uint32_t* h_chunk0 = nullptr;
-    size_t h_chunk0_cap = 0;
-    HuffDev* h_tabs = nullptr;
-    uint16_t* h_qt = nullptr;
+    // pinned host staging, two sets used in turn: a call refills the set whose uploads (two calls
+    // back) are done, so host parsing overlaps the previous call's transfers and kernels
+    struct HostSet {
+        uint8_t* stream = nullptr;
+        size_t stream_cap = 0;
+        Seg* segs = nullptr;
+        size_t segs_cap = 0;
+        uint32_t* chunk0 = nullptr;
+        size_t chunk0_cap = 0;
+        HuffDev* tabs = nullptr;
+        uint16_t* qt = nullptr;
+        hipEvent_t done = nullptr;  // the set's uploads are finished
+        bool used = false;
+    } hs[2];
+    int cur = 0;
+    hipStream_t last_st = nullptr;     // stream of the previous call, and its kernels' completion
+    hipEvent_t last_ev = nullptr;
     float last_ms = 0.f;
     bool timing = false;
 };
@@ -701,6 +786,34 @@ int jfail(fm_mjpeg* d, int code, const char* fmt, ...) {
         hipError_t _e = (expr);                                                                     \
         if (_e != hipSuccess) return jfail(d, FM_EHIP, "%s: %s", #expr, hipGetErrorString(_e));     \
     } while (0)
+
+int pfail(std::string& err, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+}
+
+// fn(i) for i in [0, n) on up to 8 host threads (frames are independent)
+template <typename F>
+void parallel_for(int n, F&& fn) {
+    const int nt = std::max(1, std::min({8, (int)std::thread::hardware_concurrency(), n / 8}));
+    if (nt == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int t = 1; t < nt; t++)
+        th.emplace_back([&, t]() {
+            for (int i = t; i < n; i += nt) fn(i);
+        });
+    for (int i = 0; i < n; i += nt) fn(i);
+    for (auto& x : th) x.join();
+}
 
 struct HuffHost {
     uint8_t bits[17] = {};
@@ -725,20 +838,20 @@ const int kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,
                       41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
                       30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) {
-    if (n < 4 || p[0] != 0xFF || p[1] != 0xD8) return jfail(d, FM_EINVAL, "frame %d: no SOI", idx);
+int parse_jpeg(std::string& err, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) {
+    if (n < 4 || p[0] != 0xFF || p[1] != 0xD8) return pfail(err, FM_EINVAL, "frame %d: no SOI", idx);
     size_t i = 2;
     bool sof = false;
     while (i + 4 <= n) {
-        if (p[i] != 0xFF) return jfail(d, FM_EINVAL, "frame %d: marker expected at byte %zu", idx, i);
+        if (p[i] != 0xFF) return pfail(err, FM_EINVAL, "frame %d: marker expected at byte %zu", idx, i);
         while (i < n && p[i] == 0xFF) i++;
         if (i >= n) break;
         const int m = p[i++];
         if (m == 0xD9) break;
         if (m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
-        if (i + 2 > n) return jfail(d, FM_EINVAL, "frame %d: truncated marker", idx);
+        if (i + 2 > n) return pfail(err, FM_EINVAL, "frame %d: truncated marker", idx);
         const size_t len = ((size_t)p[i] << 8) | p[i + 1];
-        if (len < 2 || i + len > n) return jfail(d, FM_EINVAL, "frame %d: bad segment length", idx);
+        if (len < 2 || i + len > n) return pfail(err, FM_EINVAL, "frame %d: bad segment length", idx);
         const uint8_t* s = p + i + 2;
         const size_t sl = len - 2;
         if (m == 0xDB) {
@@ -746,7 +859,7 @@ int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) 
             while (q < sl) {
                 const int pq = s[q] >> 4, tq = s[q] & 15;
                 q++;
-                if (tq > 3 || q + (pq ? 128 : 64) > sl) return jfail(d, FM_EINVAL, "frame %d: bad DQT", idx);
+                if (tq > 3 || q + (pq ? 128 : 64) > sl) return pfail(err, FM_EINVAL, "frame %d: bad DQT", idx);
                 for (int k = 0; k < 64; k++) J.qt[tq][kZig[k]] = pq ? (uint16_t)((s[q + 2 * k] << 8) | s[q + 2 * k + 1]) : s[q + k];
                 J.qt_present[tq] = true;
                 q += pq ? 128 : 64;
@@ -755,26 +868,26 @@ int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) 
             size_t q = 0;
             while (q < sl) {
                 const int tc = s[q] >> 4, th = s[q] & 15;
-                if (tc > 1 || th > 3 || q + 17 > sl) return jfail(d, FM_EINVAL, "frame %d: bad DHT", idx);
+                if (tc > 1 || th > 3 || q + 17 > sl) return pfail(err, FM_EINVAL, "frame %d: bad DHT", idx);
                 HuffHost& t = J.ht[tc][th];
                 int cnt = 0;
                 for (int l = 1; l <= 16; l++) {
                     t.bits[l] = s[q + l];
                     cnt += s[q + l];
                 }
-                if (cnt > 256 || q + 17 + cnt > sl) return jfail(d, FM_EINVAL, "frame %d: bad DHT counts", idx);
+                if (cnt > 256 || q + 17 + cnt > sl) return pfail(err, FM_EINVAL, "frame %d: bad DHT counts", idx);
                 memcpy(t.vals, s + q + 17, cnt);
                 t.n = cnt;
                 t.present = true;
                 q += 17 + cnt;
             }
         } else if (m == 0xC0 || m == 0xC1) {
-            if (sl < 6 || s[0] != 8) return jfail(d, FM_ENOTSUP, "frame %d: only 8-bit samples", idx);
+            if (sl < 6 || s[0] != 8) return pfail(err, FM_ENOTSUP, "frame %d: only 8-bit samples", idx);
             J.H = (s[1] << 8) | s[2];
             J.W = (s[3] << 8) | s[4];
             J.nc = s[5];
             if ((J.nc != 1 && J.nc != 3) || sl < 6 + 3 * (size_t)J.nc)
-                return jfail(d, FM_ENOTSUP, "frame %d: %d components (1 or 3 supported)", idx, J.nc);
+                return pfail(err, FM_ENOTSUP, "frame %d: %d components (1 or 3 supported)", idx, J.nc);
             for (int c = 0; c < J.nc; c++) {
                 J.cid[c] = s[6 + 3 * c];
                 J.ch[c] = s[7 + 3 * c] >> 4;
@@ -783,16 +896,16 @@ int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) 
             }
             sof = true;
         } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-            return jfail(d, FM_ENOTSUP, "frame %d: SOF%d (progressive / lossless / arithmetic) not supported", idx,
+            return pfail(err, FM_ENOTSUP, "frame %d: SOF%d (progressive / lossless / arithmetic) not supported", idx,
                          m - 0xC0);
         } else if (m == 0xDD) {
-            if (sl < 2) return jfail(d, FM_EINVAL, "frame %d: bad DRI", idx);
+            if (sl < 2) return pfail(err, FM_EINVAL, "frame %d: bad DRI", idx);
             J.dri = (s[0] << 8) | s[1];
         } else if (m == 0xDA) {
-            if (!sof) return jfail(d, FM_EINVAL, "frame %d: SOS before SOF", idx);
+            if (!sof) return pfail(err, FM_EINVAL, "frame %d: SOS before SOF", idx);
             J.ns = s[0];
             if (J.ns != J.nc || sl < 1 + 2 * (size_t)J.ns + 3)
-                return jfail(d, FM_ENOTSUP, "frame %d: non-interleaved multi-scan JPEG not supported", idx);
+                return pfail(err, FM_ENOTSUP, "frame %d: non-interleaved multi-scan JPEG not supported", idx);
             for (int k = 0; k < J.ns; k++) {
                 J.sid[k] = s[1 + 2 * k];
                 J.std_[k] = s[2 + 2 * k] >> 4;
@@ -814,7 +927,7 @@ int parse_jpeg(fm_mjpeg* d, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) 
         }
         i += len;
     }
-    return jfail(d, FM_EINVAL, "frame %d: no scan", idx);
+    return pfail(err, FM_EINVAL, "frame %d: no scan", idx);
 }
 
 void build_table(const HuffHost& h, HuffDev& t, bool dc) {
@@ -933,7 +1046,8 @@ int setup_geometry(fm_mjpeg* d, const ParsedJpeg& J) {
     JHIP(d, hipMemsetAsync(d->d_coef, 0, nb * sizeof(int16_t), d->st));
     JHIP(d, hipMalloc((void**)&d->d_planes, (size_t)d->max_frames * g.frame_plane));
     JHIP(d, hipMalloc((void**)&d->d_qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t)));
-    JHIP(d, hipHostMalloc((void**)&d->h_qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t), hipHostMallocDefault));
+    for (auto& H : d->hs)
+        JHIP(d, hipHostMalloc((void**)&H.qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t), hipHostMallocDefault));
     JHIP(d, hipStreamSynchronize(d->st));
     d->have_geom = true;
     return FM_OK;
@@ -957,7 +1071,11 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
     JHIP(d, hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking));
     JHIP(d, hipEventCreate(&d->e0));
     JHIP(d, hipEventCreate(&d->e1));
-    JHIP(d, hipHostMalloc((void**)&d->h_tabs, 4 * sizeof(HuffDev), hipHostMallocDefault));
+    for (auto& H : d->hs) {
+        JHIP(d, hipHostMalloc((void**)&H.tabs, 4 * sizeof(HuffDev), hipHostMallocDefault));
+        JHIP(d, hipEventCreateWithFlags(&H.done, hipEventDisableTiming));
+    }
+    JHIP(d, hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
     if (const char* e = getenv("FM_JPEG_CB")) d->CB = std::max(64, atoi(e));
     if (const char* e = getenv("FM_JPEG_OV")) d->OV = std::max(0, atoi(e));
     return FM_OK;
@@ -969,8 +1087,12 @@ void fm_mjpeg_destroy(fm_mjpeg* d) {
     for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef,
                     (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)d->h_stream, (void*)d->h_segs, (void*)d->h_tabs, (void*)d->h_qt, (void*)d->h_chunk0})
-        if (p) (void)hipHostFree(p);
+    for (auto& H : d->hs) {
+        for (void* p : {(void*)H.stream, (void*)H.segs, (void*)H.tabs, (void*)H.qt, (void*)H.chunk0})
+            if (p) (void)hipHostFree(p);
+        if (H.done) (void)hipEventDestroy(H.done);
+    }
+    if (d->last_ev) (void)hipEventDestroy(d->last_ev);
     if (d->e0) (void)hipEventDestroy(d->e0);
     if (d->e1) (void)hipEventDestroy(d->e1);
     if (d->st) (void)hipStreamDestroy(d->st);
@@ -991,15 +1113,22 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         return jfail(d, FM_EINVAL, "n %d outside [1, max_frames=%d] or null buffers", n, d->max_frames);
     JHIP(d, hipSetDevice(d->device));
     if (!st) st = d->st;
-    // the previous call's uploads must be done before the pinned staging is refilled
-    JHIP(d, hipStreamSynchronize(st));
-    if (st != d->st) JHIP(d, hipStreamSynchronize(d->st));
+    // the staging set's previous uploads must be done before it is refilled; the device buffers are
+    // reused in stream order (a call on another stream than the previous one waits for its kernels)
+    auto& H = d->hs[d->cur];
+    if (H.used) JHIP(d, hipEventSynchronize(H.done));
+    if (d->last_st && d->last_st != st) JHIP(d, hipStreamWaitEvent(st, d->last_ev, 0));
     std::vector<ParsedJpeg> P(n);
-    size_t total = 0;
-    for (int i = 0; i < n; i++) {
+    for (int i = 0; i < n; i++)
         if (!jpegs[i]) return jfail(d, FM_EINVAL, "frame %d: null", i);
-        if (int rc = parse_jpeg(d, i, jpegs[i], sizes[i], P[i])) return rc;
-        total += P[i].scan_end - P[i].scan_begin + 8 * (P[i].nrst + 1);  // + zero padding after each segment
+    {   // marker parsing, frames in parallel (errors reported for the first failing frame)
+        std::vector<int> prc(n, FM_OK);
+        std::vector<std::string> perr(n);
+        parallel_for(n, [&](int i) {
+            prc[i] = parse_jpeg(perr[i], i, jpegs[i], sizes[i], P[i]);
+        });
+        for (int i = 0; i < n; i++)
+            if (prc[i]) return jfail(d, prc[i], "%s", perr[i].c_str());
     }
     if (!d->have_geom)
         if (int rc = setup_geometry(d, P[0])) return rc;
@@ -1035,37 +1164,42 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         d->g.comp[c].ac = 2 + (sel[c][1] & 1);
     }
     for (int t = 0; t < 2; t++) {
-        build_table(P[0].ht[0][t], d->h_tabs[t], true);
-        build_table(P[0].ht[1][t], d->h_tabs[2 + t], false);
+        build_table(P[0].ht[0][t], H.tabs[t], true);
+        build_table(P[0].ht[1][t], H.tabs[2 + t], false);
     }
-    // entropy-coded bytes: stuffing and RSTn removed, one segment per restart interval
-    if (int rc = grow_host(d, &d->h_stream, d->h_stream_cap, total + 16)) return rc;
+    // entropy-coded bytes: stuffing and RSTn removed, one segment per restart interval, each followed
+    // by kSegPad zero bytes; frame i writes its own region of the staging buffer (bounded by its scan
+    // size), frames in parallel
+    std::vector<size_t> base(n + 1, 0);
+    for (int i = 0; i < n; i++) base[i + 1] = base[i] + P[i].scan_end - P[i].scan_begin + kSegPad * (P[i].nrst + 1);
+    if (int rc = grow_host(d, &H.stream, H.stream_cap, base[n] + 16)) return rc;
     const long long nmcu = (long long)g.mcux * g.mcuy;
-    std::vector<Seg> segs;
-    segs.reserve(n);
-    size_t w = 0;
-    for (int i = 0; i < n; i++) {
+    std::vector<std::vector<Seg>> fsegs(n);
+    std::vector<int> frc(n, FM_OK);
+    parallel_for(n, [&](int i) {
         const ParsedJpeg& J = P[i];
         const uint8_t* s = jpegs[i];
+        std::vector<Seg>& segs = fsegs[i];
+        size_t w = base[i];
         const long long per = J.dri > 0 ? J.dri : nmcu;
         Seg cur{(uint32_t)w, 0, i, 0, (int32_t)std::min<long long>(per, nmcu)};
         size_t k = J.scan_begin;
         while (k < J.scan_end) {
             const uint8_t* ff = (const uint8_t*)memchr(s + k, 0xFF, J.scan_end - k);
             const size_t run = ff ? (size_t)(ff - (s + k)) : J.scan_end - k;
-            memcpy(d->h_stream + w, s + k, run);
+            memcpy(H.stream + w, s + k, run);
             w += run;
             k += run;
             if (!ff) break;
             const uint8_t nx = k + 1 < J.scan_end ? s[k + 1] : 0;
             if (nx == 0x00) {
-                d->h_stream[w++] = 0xFF;
+                H.stream[w++] = 0xFF;
                 k += 2;
             } else if (nx >= 0xD0 && nx <= 0xD7) {  // restart marker: the next interval starts here
                 cur.len = (uint32_t)(w - cur.off);
                 segs.push_back(cur);
-                memset(d->h_stream + w, 0, 8);
-                w += 8;
+                memset(H.stream + w, 0, kSegPad);
+                w += kSegPad;
                 const long long m0 = (long long)cur.mcu0 + cur.nmcu;
                 cur = Seg{(uint32_t)w, 0, i, (int32_t)m0, (int32_t)std::min<long long>(per, nmcu - m0)};
                 k += 2;
@@ -1076,26 +1210,31 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         }
         cur.len = (uint32_t)(w - cur.off);
         if (cur.nmcu > 0) segs.push_back(cur);
-        memset(d->h_stream + w, 0, 8);
-        w += 8;
-        if (J.dri > 0 && (long long)(segs.back().mcu0 + segs.back().nmcu) != nmcu)
-            return jfail(d, FM_EINVAL, "frame %d: restart markers do not cover the %lld MCUs", i, nmcu);
-        for (int c = 0; c < g.nc; c++) memcpy(d->h_qt + ((size_t)i * kMaxComp + c) * 64, J.qt[J.ctq[c]], 128);
+        memset(H.stream + w, 0, kSegPad);
+        if (J.dri > 0 && (segs.empty() || (long long)(segs.back().mcu0 + segs.back().nmcu) != nmcu)) frc[i] = FM_EINVAL;
+        for (int c = 0; c < g.nc; c++) memcpy(H.qt + ((size_t)i * kMaxComp + c) * 64, J.qt[J.ctq[c]], 128);
+    });
+    std::vector<Seg> segs;
+    segs.reserve(n);
+    for (int i = 0; i < n; i++) {
+        if (frc[i]) return jfail(d, FM_EINVAL, "frame %d: restart markers do not cover the %lld MCUs", i, nmcu);
+        segs.insert(segs.end(), fsegs[i].begin(), fsegs[i].end());
     }
-    memset(d->h_stream + w, 0, 16);
+    size_t w = base[n];
+    memset(H.stream + w, 0, 16);
     w += 16;
     if (w >= (size_t)UINT32_MAX) return jfail(d, FM_ENOTSUP, "compressed batch too large");
-    if (int rc = grow_host(d, &d->h_segs, d->h_segs_cap, segs.size())) return rc;
-    memcpy(d->h_segs, segs.data(), segs.size() * sizeof(Seg));
+    if (int rc = grow_host(d, &H.segs, H.segs_cap, segs.size())) return rc;
+    memcpy(H.segs, segs.data(), segs.size() * sizeof(Seg));
     // chunks of CB bits per segment (at least one), 64 per tile
     const int nseg = (int)segs.size();
-    if (int rc = grow_host(d, &d->h_chunk0, d->h_chunk0_cap, (size_t)nseg + 1)) return rc;
+    if (int rc = grow_host(d, &H.chunk0, H.chunk0_cap, (size_t)nseg + 1)) return rc;
     size_t nchunks = 0;
     for (int i = 0; i < nseg; i++) {
-        d->h_chunk0[i] = (uint32_t)nchunks;
+        H.chunk0[i] = (uint32_t)nchunks;
         nchunks += std::max<size_t>(1, ((size_t)segs[i].len * 8 + d->CB - 1) / d->CB);
     }
-    d->h_chunk0[nseg] = (uint32_t)nchunks;
+    H.chunk0[nseg] = (uint32_t)nchunks;
     if (nchunks >= (size_t)INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "compressed batch too large");
     const size_t ntiles = (nchunks + 63) / 64;
     if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + kStreamSlack)) return rc;  // look-ahead reads
@@ -1105,12 +1244,15 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     size_t tcap = d->tabs_cap;
     if (int rc = grow_dev(d, &d->d_tabs, tcap, 4)) return rc;
     d->tabs_cap = (int)tcap;
-    JHIP(d, hipMemcpyAsync(d->d_stream, d->h_stream, w, hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_segs, d->h_segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_chunk0, d->h_chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_stream, H.stream, w, hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_segs, H.segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_chunk0, H.chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     JHIP(d, hipMemsetAsync(d->d_ts, 0, (ntiles + 1) * sizeof(TileState), st));  // flags + the tile counter
-    JHIP(d, hipMemcpyAsync(d->d_tabs, d->h_tabs, 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_qt, d->h_qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_tabs, H.tabs, 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(d->d_qt, H.qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    JHIP(d, hipEventRecord(H.done, st));
+    H.used = true;
+    d->cur ^= 1;
     if (d->timing) JHIP(d, hipEventRecord(d->e0, st));
     hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((ntiles + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
                        d->d_stream, (uint32_t)w, d->d_segs, nseg, d->d_chunk0, (int)nchunks, d->d_tabs, d->g, d->CB,
@@ -1120,11 +1262,23 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 31) / 32)), dim3(256), 0, st, d->d_coef, d->d_qt, d->g, nb,
                        d->d_planes);
     JHIP(d, hipGetLastError());
-    const size_t lds = (((size_t)g.W * 3 + 15) & ~(size_t)15) + (g.nc == 3 ? 4 * (size_t)g.comp[1].bw * 8 : 0);
+    // colour bands: as many rows as keep the staging within 48 KB of LDS
+    int rb = 16;
+    size_t lds = 0;
+    for (;; rb >>= 1) {
+        const size_t orow = ((size_t)g.W * 3 + 15) & ~(size_t)15, wr = ((size_t)g.W + 7) & ~(size_t)7;
+        size_t nr = 0;
+        if (g.nc == 3) nr = g.vmax / g.comp[1].v == 2 ? (size_t)rb / 2 + 3 : (size_t)rb;
+        lds = 2 * orow + rb * wr + (g.nc == 3 ? 2 * nr * (size_t)g.comp[1].bw * 8 + 16 : 0);  // + word look-ahead
+        if (lds <= 48 * 1024 || rb == 1) break;
+    }
     if (lds > 64 * 1024) return jfail(d, FM_ENOTSUP, "frame width %d too large for the colour kernel", g.W);
-    hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)g.H, (unsigned)n), dim3(256), lds, st, d->d_planes, d->g, out);
+    hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((g.H + rb - 1) / rb), (unsigned)n), dim3(256), lds, st, d->d_planes, d->g,
+                       rb, out);
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
+    JHIP(d, hipEventRecord(d->last_ev, st));
+    d->last_st = st;
     return FM_OK;
 }
 
