@@ -109,6 +109,55 @@ def cpu_baseline(cfg: dict, frames_host: np.ndarray, n_frames: int) -> dict:
                       f"(oracle/fm_oracle.c, gcc -O3 -march=x86-64-v3; cv2 is not installed); CPU: {cpu_model()}"}
 
 
+def mjpeg_fed(eng, host: np.ndarray, T: int, S: int, quality: int = 75) -> dict | None:
+    """Frames/s through BatchFeeder's JPEG mode (host parse + compressed H2D + GPU decode + hot path),
+    the decoder's kernels alone (HIP events), and Pillow's libjpeg-turbo decode on one host core."""
+    try:
+        from PIL import Image
+    except ImportError:
+        return None
+    import io
+
+    import torch
+
+    from find_motion_amd import MJpegDecoder, videoio
+    from find_motion_amd.feeder import BatchFeeder
+    R, H, W = host.shape[0], host.shape[2], host.shape[3]
+    enc = []
+    for t in range(min(R, 64)):
+        b = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(host[t, 0][..., ::-1])).save(b, "JPEG", quality=quality)
+        enc.append(b.getvalue())
+    dec = MJpegDecoder(W, H, max_frames=T * S, device=eng.device)
+    dst = torch.empty((T * S, H, W, 3), dtype=torch.uint8, device="cuda")
+    jp = [enc[i % len(enc)] for i in range(T * S)]
+    dec.decode_device(jp, dst.data_ptr())
+    kms = []
+    for _ in range(3):
+        dec.decode_device(jp, dst.data_ptr())
+        kms.append(dec.last_ms())
+    dec.close()
+    del dst
+    n = max(8 * T, 512)
+    for _ in BatchFeeder(eng, [videoio.JpegListCapture(enc[:2]) for _ in range(S)], T):  # warm-up
+        pass
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in BatchFeeder(eng, [videoio.JpegListCapture([enc[i % len(enc)] for i in range(n)]) for _ in range(S)], T):
+        pass
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    for j in enc[:16]:
+        np.asarray(Image.open(io.BytesIO(j)))
+    cpu_fps = 16 / (time.perf_counter() - t1)
+    return {"frames_per_s": round(n * S / dt, 1), "frames": n * S, "jpeg_quality": quality,
+            "bytes_per_frame": int(np.mean([len(j) for j in enc])),
+            "decoder_kernels_ms_per_batch": round(float(np.median(kms)), 3),
+            "decoder_kernels_frames_per_s": round(T * S / (float(np.median(kms)) / 1e3), 1),
+            "libjpeg_turbo_1core_frames_per_s": round(cpu_fps, 1),
+            "mode": "BatchFeeder JPEG mode: JPEG bytes -> host parse -> H2D -> GPU Huffman/IDCT/colour -> hot path"}
+
+
 def spawn_ranks(n: int) -> int:
     """bench.py --gpus N without a launcher: start N ranks of this script (one per GPU, RANK = LOCAL_RANK =
     device ordinal, rendezvous on 127.0.0.1) before any GPU call in this process, and return the worst
@@ -168,6 +217,7 @@ def main() -> None:
     ap.add_argument("--host-fed", action="store_true", help="also time PCIe-fed submits (stderr only)")
     ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed decode-ahead pipeline figure")
     ap.add_argument("--no-ktimes", action="store_true", help="no HIP event timing at all (no roofline)")
+    ap.add_argument("--no-mjpeg", action="store_true", help="skip the MJPEG-fed (GPU decode) figure")
     ap.add_argument("--all-ktimes", action="store_true",
                     help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
@@ -372,6 +422,14 @@ def main() -> None:
                     "frames": n_hf * S, "mode": "BatchFeeder: pre-decoded frames -> page-locked batches -> "
                                                  "hipMemcpyAsync + kernels, fm_max_inflight in flight"}
 
+    # MJPEG-fed (the decode side): the synthetic frames as baseline JPEGs (Pillow,
+    # quality 75, 4:2:0, no restart markers), read by BatchFeeder in JPEG mode: compressed bytes parsed on
+    # the host, copied to the GPU, decoded there (fm_submit_jpeg) in front of the hot path.  Beside
+    # `value`, never as it; libjpeg-turbo (Pillow) on one host core is the CPU decode rate it replaces.
+    mjpeg = None
+    if not args.no_mjpeg:
+        mjpeg = mjpeg_fed(eng, host, T, S)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, host.reshape(R * S, H, W, 3), min(args.cpu_frames, R * S))
@@ -382,6 +440,7 @@ def main() -> None:
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "host_fed_per_gpu": host_fed,
+               "mjpeg_fed_per_gpu": mjpeg,
                "contour_pass": {"heavy_tiles_per_batch": round(ccl["heavy_tiles"] / max(ccl["batches"], 1), 2),
                                 "shared_nodes_max": ccl["shared_nodes_max"],
                                 "fallback_frames": ccl["fallback_frames"]}}

@@ -30,7 +30,7 @@ EXPORTED = (
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
-    "fm_submit_jpeg", "fm_read_frame",
+    "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune",
 )
 
 
@@ -126,6 +126,7 @@ def load() -> C.CDLL:
     L.fm_mjpeg_last_ms.restype = C.c_double
     L.fm_submit_jpeg.argtypes = [vp, vp, vp, vp, i32]
     L.fm_read_frame.argtypes = [vp, i32, i32, vp]
+    L.fm_mjpeg_tune.argtypes = [vp, i32, i32]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
                         "fm_haar_last_ms", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_last_ms"):
@@ -483,7 +484,8 @@ class MJpegDecoder:
     BGR u8 frames as cv2.VideoCapture.read returns them (fm.py:497-506), libjpeg-turbo's default
     decode reproduced bit for bit (jpeg_idct_islow, fancy upsampling, integer YCbCr tables)."""
 
-    def __init__(self, width: int, height: int, max_frames: int = 64, device: int = 0):
+    def __init__(self, width: int, height: int, max_frames: int = 64, device: int = 0,
+                 chunk_bits: int | None = None, spec_bits: int | None = None):
         L = load()
         h = C.c_void_p()
         rc = L.fm_mjpeg_create(int(device), int(width), int(height), int(max_frames), C.byref(h))
@@ -494,6 +496,12 @@ class MJpegDecoder:
             self._h = None
             raise FMError(rc, f"fm_mjpeg_create: {msg}")
         self.width, self.height, self.max_frames = int(width), int(height), int(max_frames)
+        if chunk_bits is not None or spec_bits is not None:  # fm_mjpeg_tune: speed only, same results
+            rc = L.fm_mjpeg_tune(h, int(chunk_bits or 1024), int(512 if spec_bits is None else spec_bits))
+            if rc != FM_OK:
+                msg = L.fm_mjpeg_last_error(h).decode()
+                self.close()
+                raise FMError(rc, f"fm_mjpeg_tune: {msg}")
 
     def decode(self, jpegs) -> np.ndarray:
         """JPEG byte strings -> BGR u8 [n, H, W, 3] (host)."""

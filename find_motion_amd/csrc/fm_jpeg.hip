@@ -741,7 +741,7 @@ struct fm_mjpeg {
     size_t chunk0_cap = 0;
     TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
     size_t ts_cap = 0;
-    int CB = 1024, OV = 512;           // chunk and speculation lengths in bits (FM_JPEG_CB / FM_JPEG_OV)
+    int CB = 1024, OV = 512;           // chunk and speculation lengths in bits (fm_mjpeg_tune)
     HuffDev* d_tabs = nullptr;         // [n_sets][4]
     int tabs_cap = 0;
     uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
@@ -1076,8 +1076,6 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
         JHIP(d, hipEventCreateWithFlags(&H.done, hipEventDisableTiming));
     }
     JHIP(d, hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
-    if (const char* e = getenv("FM_JPEG_CB")) d->CB = std::max(64, atoi(e));
-    if (const char* e = getenv("FM_JPEG_OV")) d->OV = std::max(0, atoi(e));
     return FM_OK;
 }
 
@@ -1100,6 +1098,15 @@ void fm_mjpeg_destroy(fm_mjpeg* d) {
 }
 
 const char* fm_mjpeg_last_error(const fm_mjpeg* d) { return d ? d->err.c_str() : "null decoder"; }
+
+int fm_mjpeg_tune(fm_mjpeg* d, int chunk_bits, int spec_bits) {
+    if (!d) return FM_EINVAL;
+    if (chunk_bits < 64 || chunk_bits > (1 << 24) || spec_bits < 0 || spec_bits > (1 << 24))
+        return jfail(d, FM_EINVAL, "chunk_bits %d / spec_bits %d outside [64, 2^24] / [0, 2^24]", chunk_bits, spec_bits);
+    d->CB = chunk_bits;
+    d->OV = spec_bits;
+    return FM_OK;
+}
 
 double fm_mjpeg_last_ms(const fm_mjpeg* d) { return d ? (double)d->last_ms : 0.0; }
 

@@ -84,6 +84,63 @@ class ArrayCapture:
         self._open = False
 
 
+class JpegListCapture:
+    """VideoCapture protocol over in-memory JPEG frames (an MJPEG stream already split into frames):
+    read_jpeg() hands them to the GPU decoder like MjpegAviCapture; width/height from the first frame."""
+
+    def __init__(self, jpegs, fps: float = 30.0):
+        self._jpegs = list(jpegs)
+        self._i = 0
+        self._open = True
+        self.fps = float(fps)
+        self.w = self.h = 0
+        if self._jpegs:
+            self.h, self.w = _jpeg_size(self._jpegs[0])
+        self._dec = None
+
+    def isOpened(self) -> bool:  # noqa: N802 (cv2 protocol)
+        return self._open
+
+    def read_jpeg(self):
+        if not self._open or self._i >= len(self._jpegs):
+            return False, None
+        j = self._jpegs[self._i]
+        self._i += 1
+        return True, j
+
+    def read(self):
+        ok, j = self.read_jpeg()
+        if not ok:
+            return False, None
+        if self._dec is None:
+            from ._native import MJpegDecoder
+            self._dec = MJpegDecoder(self.w, self.h, max_frames=1)
+        return True, self._dec.decode([j])[0]
+
+    def get(self, prop: int) -> float:
+        return {CAP_PROP_FRAME_COUNT: float(len(self._jpegs)), CAP_PROP_FRAME_WIDTH: float(self.w),
+                CAP_PROP_FRAME_HEIGHT: float(self.h), CAP_PROP_FPS: self.fps}.get(prop, 0.0)
+
+    def release(self) -> None:
+        self._open = False
+        if self._dec is not None:
+            self._dec.close()
+            self._dec = None
+
+
+def _jpeg_size(data: bytes):
+    """(height, width) from a JPEG's SOF0/SOF1/SOF2 marker."""
+    i = 2
+    while i + 9 < len(data):
+        if data[i] != 0xFF:
+            raise ValueError("not a JPEG marker stream")
+        m = data[i + 1]
+        if m in (0xC0, 0xC1, 0xC2):
+            return (data[i + 5] << 8) | data[i + 6], (data[i + 7] << 8) | data[i + 8]
+        i += 2 + ((data[i + 2] << 8) | data[i + 3])
+    raise ValueError("no SOF marker")
+
+
 class SyntheticCapture(ArrayCapture):
     """The seeded synthetic stream of find_motion_amd.synthetic as a capture (frames made on demand)."""
 

@@ -102,11 +102,9 @@ def test_submit_jpeg_equals_submit_of_decoded_frames():
 
 
 @pytest.mark.parametrize("cb,ov", [(64, 0), (64, 48), (200, 1000), (4096, 0), (1024, 512)])
-def test_chunking_and_lookback(monkeypatch, cb, ov):
+def test_chunking_and_lookback(cb, ov):
     """The parallel Huffman decode cut into tiny chunks (many tiles per segment, entry states mostly
     mis-speculated, long look-back chains) and into chunks longer than whole segments: all bit-exact."""
-    monkeypatch.setenv("FM_JPEG_CB", str(cb))
-    monkeypatch.setenv("FM_JPEG_OV", str(ov))
     v = SyntheticVideo(640, 360, 3)
     groups = [  # one decoder per sampling (a decoder keeps its first frame's geometry)
         [encode(v.frame(0), quality=75), encode(v.frame(1), quality=95),
@@ -116,12 +114,12 @@ def test_chunking_and_lookback(monkeypatch, cb, ov):
         [encode(v.frame(4), quality=85, subsampling=0), encode(image(360, 640, "noise", seed=2), quality=88, subsampling=0)],
     ]
     for frames in groups:
-        dec = MJpegDecoder(640, 360, max_frames=len(frames))
+        dec = MJpegDecoder(640, 360, max_frames=len(frames), chunk_bits=cb, spec_bits=ov)
         got = dec.decode(frames)
         for i, f in enumerate(frames):
             assert np.array_equal(got[i], reference_decode(f)), i
         dec.close()
-    g = MJpegDecoder(96, 64, max_frames=2)  # grayscale frames through the same chunking
+    g = MJpegDecoder(96, 64, max_frames=2, chunk_bits=cb, spec_bits=ov)  # grayscale, same chunking
     gj = [encode(image(64, 96, "noise", seed=s)[..., 0], quality=70) for s in range(2)]
     out = g.decode(gj)
     for i, f in enumerate(gj):

@@ -2,7 +2,7 @@
 """Decode side (§8(f)-3): GPU MJPEG decode rate at 1080p, decoder alone and end to end through
 fm_submit_jpeg (JPEG bytes in -> contours out), beside Pillow's libjpeg-turbo on one host core.
 Frames: the synthetic video encoded by Pillow (4:2:0), without and with restart intervals.
-Usage: tools/bench_mjpeg.py [n_frames] [quality]"""
+Usage: tools/bench_mjpeg.py [n_frames] [quality]   (FM_JPEG_CB / FM_JPEG_OV: fm_mjpeg_tune values)"""
 import io
 import json
 import os
@@ -21,6 +21,7 @@ from find_motion_amd.synthetic import SyntheticVideo  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 192
 Q = int(sys.argv[2]) if len(sys.argv) > 2 else 75
 W, H = 1920, 1080
+TUNE = {k: int(os.environ[e]) for k, e in (("chunk_bits", "FM_JPEG_CB"), ("spec_bits", "FM_JPEG_OV")) if e in os.environ}
 v = SyntheticVideo(W, H, 0)
 raw = [v.frame(t) for t in range(64)]
 out = {"frames": N, "quality": Q}
@@ -36,7 +37,7 @@ for name, kw in [("no_restart", {}), ("restart_per_mcu_row", {"restart_marker_ro
     for j in jp[:32]:
         np.asarray(Image.open(io.BytesIO(j)))
     r["pillow_1core_fps"] = round(32 / (time.perf_counter() - t0), 1)
-    dec = MJpegDecoder(W, H, max_frames=N)
+    dec = MJpegDecoder(W, H, max_frames=N, **TUNE)
     dst = torch.empty((N, H, W, 3), dtype=torch.uint8, device="cuda")
     dec.decode_device(jp, dst.data_ptr())  # warm-up
     ms = []
@@ -52,7 +53,7 @@ for name, kw in [("no_restart", {}), ("restart_per_mcu_row", {"restart_marker_ro
     T = min(N, 192)
     eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T,
                        max_contours=1 << 14)
-    dec2 = MJpegDecoder(W, H, max_frames=T)
+    dec2 = MJpegDecoder(W, H, max_frames=T, **TUNE)
     batches = [jp[(i * T) % N:(i * T) % N + T] for i in range(max(1, N // T))]
     nb = 8
     depth = eng.max_inflight
