@@ -249,7 +249,8 @@ struct ChainCtx {
 // fm.py:651-652); `init` says whether this frame is one.  KEEP: apply the
 // keep-mask bytes (off when the stream has no mask).  TAIL: the wave's rows reach
 // accumulateWeighted's scalar tail (per-pixel test of the product order).
-template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
+// HPAIR: H is stored as row pairs (k_pix5): u32 [pair][64 columns] = H[2p][c] | H[2p+1][c] << 16
+template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL, bool HPAIR = false>
 __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const double* atab, const Geo& g,
                                            double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
@@ -260,7 +261,12 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
     const int w = a.w;
     // column ln of H, rows 8*wv .. 8*wv + NV - 1, as u16 pairs (ds_read_u16_d16 / _d16_hi)
     uint32_t P[NP + 1];
-    {
+    if (HPAIR) {  // one ds_read_b32 per row pair
+        const uint32_t* col = reinterpret_cast<const uint32_t*>(Hs) + (RPWV / 2 * wv) * TS + ln;
+#pragma unroll
+        for (int i = 0; i < NP; i++) P[i] = col[i * TS];
+        P[NP] = 0;
+    } else {
         const uint16_t* col = Hs + (RPWV * wv) * g.RSH + ln;
 #pragma unroll
         for (int i = 0; i < NP; i++) {
@@ -664,7 +670,14 @@ constexpr int P5_GFAST = FM_P5_GFAST;
 constexpr int P5_GSLOW = (P5_GSLOTS - 4 * P5_GFAST + 3) / 4;
 constexpr int P5_GJ = P5_GFAST > P5_GSLOW ? P5_GFAST : P5_GSLOW;                 // load rounds per wave
 static_assert(P5_GSLOW >= 0 && 4 * (P5_GFAST + P5_GSLOW) >= P5_GSLOTS, "gray slots");
-constexpr int P5_NH = P5_GH * (TS / 4);  // tap jobs per frame
+// Tap jobs cover 2 H rows x 4 columns and store them as row pairs (one ds_write_b128), which the chain
+// reads back as six dwords instead of twelve u16 reads and their merges (FM_P5_HPAIR 0: 1 x 4 jobs,
+// row-major H, as k_pix)
+#ifndef FM_P5_HPAIR
+#define FM_P5_HPAIR 1
+#endif
+constexpr int P5_HR = FM_P5_HPAIR ? 2 : 1;                 // H rows per tap job
+constexpr int P5_NH = (P5_GH / P5_HR) * (TS / 4);  // tap jobs per frame
 // tap jobs likewise (FM_P5_HFAST slots to each of waves 0..3); 0 keeps the round-robin deal
 #ifndef FM_P5_HFAST
 #define FM_P5_HFAST 0
@@ -678,7 +691,7 @@ static_assert(!P5_HFAST || (P5_HSLOW >= 0 && 4 * (P5_HFAST + P5_HSLOW) >= P5_HSL
 constexpr int P5_HLASTW = (P5_NH - (P5_HJ - 1) * NT + 63) / 64;  // 1 of 8
 constexpr int P5_GBUF = P5_NG + 64;      // + a pad slot per lane for the idle jobs' stores (branch-free)
 constexpr int P5_HROW = TS;              // u16 per H row
-constexpr int P5_HBUF = (P5_GH + 1) * P5_HROW;  // + the pad row idle tap jobs store to
+constexpr int P5_HBUF = (P5_GH + P5_HR) * P5_HROW;  // + the pad row (pair) idle tap jobs store to
 constexpr int p5_lds_bytes() { return 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2 + 256 * 8; }
 
 typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
@@ -743,8 +756,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         const int j = P5_HFAST ? (i < hjobs ? hslot * 64 + ln : P5_NH) : tid + NT * i;
         const bool live = j < P5_NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
-        hsrc[i] = (uint32_t)(hr * P5_GQ + hq);
-        hdst[i] = (uint32_t)((live ? hr : P5_GH) * P5_HROW + 4 * hq);
+        hsrc[i] = (uint32_t)(P5_HR * hr * P5_GQ + hq);
+        // FM_P5_HPAIR: u32 index of the pair's 4 columns, else u16 index of the row's
+        hdst[i] = FM_P5_HPAIR ? (uint32_t)((live ? hr : P5_GH / 2) * TS + 4 * hq)
+                              : (uint32_t)((live ? hr : P5_GH) * P5_HROW + 4 * hq);
     }
     // REFLECT_101 quads: left of column 0 (tile x0 = 0, tap quad 0 reads gray quad 0 = columns -4..-1:
     // bytes 2, 3 = gray(2), gray(1) from quad 1) and the quad starting at column w (bytes 0, 1 =
@@ -824,7 +839,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             const uint32_t h1 = htap<1, 2, 2, 0, 4>(qv, cpk, 0u);
             const uint32_t h2 = htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
             const uint32_t h3 = htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
-            *reinterpret_cast<uint2*>(Hb + hdst[i]) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+            if (FM_P5_HPAIR) {  // the next gray row, then both rows' sums as row pairs
+                uint32_t qw[4] = {gb[hsrc[i] + P5_GQ], gb[hsrc[i] + P5_GQ + 1], gb[hsrc[i] + P5_GQ + 2], 0u};
+                if (edge_tile) {
+                    if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
+                    if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
+                    if (hfix[i] & 4) qw[2] = __builtin_amdgcn_perm(qw[1], qw[1], 0x00000102u);
+                }
+                const uint32_t k0 = htap<0, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k1 = htap<1, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k2 = htap<2, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k3 = htap<3, 2, 2, 0, 4>(qw, cpk, 0u);
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
+                    make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
+            } else {
+                *reinterpret_cast<uint2*>(Hb + hdst[i]) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+            }
         }
     };
     const Geo g(R);
@@ -881,13 +911,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
         var = __builtin_amdgcn_readfirstlane(var);
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-        // chain_rows indexes H as [row][RSH = 64]: the same row-major u16 layout
+        // chain_rows reads H as row pairs (FM_P5_HPAIR) or as [row][RSH = 64] u16
         const uint16_t* Hb = Hs + b * P5_HBUF;
         if (!(skip & 2)) {
             if (!TAIL || var == 0)
-                chain_rows<KC, false, false, KEEP, false>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+                chain_rows<KC, false, false, KEEP, false, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
+                                                                         colbits, fl);
             else
-                chain_rows<KC, false, false, KEEP, true>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false, colbits, fl);
+                chain_rows<KC, false, false, KEEP, true, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
+                                                                        colbits, fl);
         }
         P5_PH(ph1);
         if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);

@@ -10,5 +10,5 @@ HIPCC=/opt/rocm/bin/hipcc
 $HIPCC -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function --offload-arch=gfx950 -munsafe-fp-atomics $FLAGS \
   -c -x hip "$ROOT/find_motion_amd/csrc/fm_pix.hip" -o "$D/fm_pix.o"
 O=$ROOT/build/fm_obj
-$HIPCC -shared -fPIC --offload-arch=gfx950 -o "$D/libfm_hip.so" $O/fm_kernels.o $O/fm_fused.o "$D/fm_pix.o" $O/fm_ccl.o $O/fm_haar.o $O/fm_capi.o $O/fm_raster.o
+$HIPCC -shared -fPIC --offload-arch=gfx950 -o "$D/libfm_hip.so" $O/fm_kernels.o $O/fm_fused.o "$D/fm_pix.o" $O/fm_ccl.o $O/fm_haar.o $O/fm_jpeg.o $O/fm_capi.o $O/fm_raster.o
 echo "$D/libfm_hip.so"
