@@ -184,7 +184,9 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
                                             int& uk_in, int total, const JpegGeom& g, const Seg& sg, int16_t* coef) {
     int u = uk >> 6, k = uk & 63;
     bool marked = WRITE;
-    int16_t* blk = (WRITE && k) ? block_ptr(coef, g, ut, sg, bpm, cnt - 1) : coef;
+    // (corrupt data can give counts past the segment's blocks: nothing is stored for those)
+    bool wr = WRITE && k && cnt >= 1 && cnt <= total;
+    int16_t* blk = wr ? block_ptr(coef, g, ut, sg, bpm, cnt - 1) : coef;
     while (true) {
         if (!WRITE && !marked && br.pos >= mark) {
             marked = true;
@@ -194,7 +196,7 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
             dc0 = dc1 = dc2 = 0;
         }
         if (br.pos >= end) break;
-        if (WRITE && k == 0 && cnt == total) break;
+        if (WRITE && k == 0 && cnt >= total) break;
         br.refill();
         const bool isdc = k == 0;
         const HuffDev& t = T[isdc ? ut.dc[u] : ut.ac[u]];
@@ -226,10 +228,13 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
             dc1 = ci == 1 ? pred : dc1;
             dc2 = ci == 2 ? pred : dc2;
             v = pred;
-            if (WRITE) blk = block_ptr(coef, g, ut, sg, bpm, cnt);
+            if (WRITE) {
+                wr = cnt >= 0;
+                blk = wr ? block_ptr(coef, g, ut, sg, bpm, cnt) : coef;
+            }
             cnt++;
         }
-        if (WRITE && val && v) blk[min(k + r, 63)] = (int16_t)v;
+        if (WRITE && wr && val && v) blk[min(k + r, 63)] = (int16_t)v;
         k = (!val && r != 15) ? 64 : k + r + 1;
         if (k >= 64) {
             k = 0;

@@ -124,3 +124,37 @@ def test_chunking_and_lookback(cb, ov):
     out = g.decode(gj)
     for i, f in enumerate(gj):
         assert np.array_equal(out[i], reference_decode(f)), i
+
+
+def test_corrupt_and_truncated_frames_do_not_fault():
+    """Damaged camera frames: entropy data cut short or overwritten.  The decode must stay inside its
+    buffers (values are unspecified, as libjpeg's are after its corrupt-data warnings) and the decoder
+    must still decode the next, valid call bit-exactly."""
+    v = SyntheticVideo(320, 240, 5)
+    good = [encode(v.frame(t), quality=q, **kw) for t, (q, kw) in
+            enumerate([(75, {}), (90, {}), (85, dict(restart_marker_rows=1)), (60, {})])]
+    rng = np.random.default_rng(7)
+    bad = []
+    for i, j in enumerate(good):
+        b = bytearray(j)
+        sos = b.find(b"\xff\xda")
+        body = sos + 2 + ((b[sos + 2] << 8) | b[sos + 3])
+        if i % 2 == 0:  # truncated scan (cut at 40 %), EOI appended
+            b = b[:body + (len(b) - body) * 2 // 5] + b"\xff\xd9"
+        else:  # random bytes over the middle of the scan (no 0xFF, so no fake markers)
+            n = (len(b) - body) // 3
+            b[body + n:body + 2 * n] = bytes(rng.integers(0, 255, n, dtype=np.uint8))
+        bad.append(bytes(b))
+    for cb, ov in ((1024, 512), (64, 0)):
+        dec = MJpegDecoder(320, 240, max_frames=4, chunk_bits=cb, spec_bits=ov)
+        for j in bad:  # one call each: a frame whose restart markers no longer cover the image is refused
+            try:
+                assert dec.decode([j]).shape == (1, 240, 320, 3)
+            except FMError:
+                pass
+        out = dec.decode([bad[1], bad[3]])
+        assert out.shape == (2, 240, 320, 3)
+        got = dec.decode(good)
+        for i, f in enumerate(good):
+            assert np.array_equal(got[i], reference_decode(f)), (cb, i)
+        dec.close()
