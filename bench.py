@@ -427,7 +427,7 @@ def main() -> None:
     # the host, copied to the GPU, decoded there (fm_submit_jpeg) in front of the hot path.  Beside
     # `value`, never as it; libjpeg-turbo (Pillow) on one host core is the CPU decode rate it replaces.
     mjpeg = None
-    if not args.no_mjpeg:
+    if not args.no_mjpeg and world == 1:  # a per-GPU figure: measured in the 1-GPU run only
         mjpeg = mjpeg_fed(eng, host, T, S)
 
     cpu = None

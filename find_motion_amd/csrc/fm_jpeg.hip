@@ -417,23 +417,25 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
 constexpr int F0_298 = 2446, F0_390 = 3196, F0_541 = 4433, F0_765 = 6270, F0_899 = 7373, F1_175 = 9633,
               F1_501 = 12299, F1_847 = 15137, F1_961 = 16069, F2_053 = 16819, F2_562 = 20995, F3_072 = 25172;
 
+// products by 24-bit multiplies (full rate): the operands of a valid 8-bit JPEG stay far below 2^23
+// (dequantized coefficients < 2^17, pass-1 outputs < 2^21), where they equal the 32-bit products
 __device__ __forceinline__ void idct1d(int v0, int v1, int v2, int v3, int v4, int v5, int v6, int v7, int (&o)[8]) {
-    int z1 = (v2 + v6) * F0_541;
-    const int tmp2 = z1 - v6 * F1_847, tmp3 = z1 + v2 * F0_765;
+    int z1 = __mul24(v2 + v6, F0_541);
+    const int tmp2 = z1 - __mul24(v6, F1_847), tmp3 = z1 + __mul24(v2, F0_765);
     const int tmp0 = (v0 + v4) * 8192, tmp1 = (v0 - v4) * 8192;
     const int t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
     int a0 = v7, a1 = v5, a2 = v3, a3 = v1;
     z1 = a0 + a3;
     int z2 = a1 + a2, z3 = a0 + a2, z4 = a1 + a3;
-    const int z5 = (z3 + z4) * F1_175;
-    a0 *= F0_298;
-    a1 *= F2_053;
-    a2 *= F3_072;
-    a3 *= F1_501;
-    z1 *= -F0_899;
-    z2 *= -F2_562;
-    z3 = z3 * -F1_961 + z5;
-    z4 = z4 * -F0_390 + z5;
+    const int z5 = __mul24(z3 + z4, F1_175);
+    a0 = __mul24(a0, F0_298);
+    a1 = __mul24(a1, F2_053);
+    a2 = __mul24(a2, F3_072);
+    a3 = __mul24(a3, F1_501);
+    z1 = __mul24(z1, -F0_899);
+    z2 = __mul24(z2, -F2_562);
+    z3 = __mul24(z3, -F1_961) + z5;
+    z4 = __mul24(z4, -F0_390) + z5;
     a0 += z1 + z3;
     a1 += z2 + z4;
     a2 += z2 + z3;
@@ -464,7 +466,7 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 // in LDS, runs column r of pass 1, then row r of pass 2
 __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
                                                     long long nblocks, uint8_t* __restrict__ planes) {
-    __shared__ int ws[32][64];
+    __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
     const long long b = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
     const bool live = b < nblocks;
@@ -529,9 +531,10 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, c
 __device__ __forceinline__ int clamp255(int x) { return x < 0 ? 0 : x > 255 ? 255 : x; }
 
 __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor.c ycc_rgb_convert, BGR
-    const int R = clamp255(Y + ((91881 * cr + 32768) >> 16));
-    const int G = clamp255(Y + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-    const int B = clamp255(Y + ((116130 * cb + 32768) >> 16));
+    // |cb|, |cr| <= 128 and the constants < 2^17: 24-bit multiplies (full rate, v_mul_lo_u32 is not)
+    const int R = clamp255(Y + ((__mul24(91881, cr) + 32768) >> 16));
+    const int G = clamp255(Y + ((__mul24(-22554, cb) + 32768 - __mul24(46802, cr)) >> 16));
+    const int B = clamp255(Y + ((__mul24(116130, cb) + 32768) >> 16));
     return (uint32_t)B | (uint32_t)G << 8 | (uint32_t)R << 16;
 }
 
