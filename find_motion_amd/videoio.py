@@ -280,9 +280,10 @@ class RawAviCapture:
             f.seek(pos)
             ck, ln = struct.unpack("<4sI", f.read(8))
             body = pos + 8
-            if ck == b"LIST":
+            if ck == b"LIST" or (ck == b"RIFF" and depth == 0):
+                # RIFF 'AVIX': the OpenDML continuation of a file past 1 GB, more 'movi' data
                 kind = f.read(4)
-                if kind in (b"hdrl", b"strl", b"movi", b"rec ") and depth < 4:
+                if kind in (b"hdrl", b"strl", b"movi", b"rec ", b"AVIX") and depth < 4:
                     self._walk(f, body + 4, min(body + ln, end), depth + 1)
             elif ck == b"avih":
                 vals = struct.unpack("<10I", f.read(40))
@@ -343,9 +344,10 @@ class MjpegAviCapture(RawAviCapture):
             f.seek(pos)
             ck, ln = struct.unpack("<4sI", f.read(8))
             body = pos + 8
-            if ck == b"LIST":
+            if ck == b"LIST" or (ck == b"RIFF" and depth == 0):
+                # RIFF 'AVIX': the OpenDML continuation of a file past 1 GB, more 'movi' data
                 kind = f.read(4)
-                if kind in (b"hdrl", b"strl", b"movi", b"rec ") and depth < 4:
+                if kind in (b"hdrl", b"strl", b"movi", b"rec ", b"AVIX") and depth < 4:
                     self._walk(f, body + 4, min(body + ln, end), depth + 1)
             elif ck == b"avih":
                 vals = struct.unpack("<10I", f.read(40))

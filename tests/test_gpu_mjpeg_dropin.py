@@ -105,3 +105,28 @@ def test_read_frame_after_submit_and_submit_jpeg():
             assert np.array_equal(eng.read_frame(t, s), reference_decode(jp[t * S + s]))
     dec.close()
     eng.close()
+
+
+@pytest.mark.parametrize("codec", ["MJPG", "MP42"])
+def test_cli_on_mjpeg_file(tmp_path, codec):
+    """The reference CLI (python -m find_motion_amd FILE -o DIR, fm.py:1448-1489 flags and defaults:
+    -B 100 -b 20 -t 12 -M 0.5 -C 1.0) on an MJPEG AVI: written frames = the oracle's on the decoded
+    frames; an MJPG output holds the source's JPEG bytes, the default MP42 falls back to uncompressed
+    AVI here (no cv2) with the decoded frames."""
+    from find_motion_amd import cli
+    W, H, n = 480, 270, 90
+    src = tmp_path / "cam.avi"
+    jp = _mjpeg_avi(src, W, H, n, 2, quality=80)
+    out = tmp_path / "out"
+    cli.main([str(src), "-o", str(out), "-I", "-k", codec, "--batch", "16"])
+    st = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=100, ksize=5, thresh=12))
+    want = written_indices([st.step(reference_decode(j))["count"] for j in jp], min_time=0.5, cache_time=1.0)
+    assert want
+    res = out / "cam.avi_1_motion.avi"
+    if codec == "MJPG":
+        assert _read_all(videoio.MjpegAviCapture(str(res))) == [jp[i] for i in want]
+    else:
+        got = _read_all(videoio.RawAviCapture(str(res)))
+        assert len(got) == len(want)
+        for g, i in zip(got, want):
+            assert np.array_equal(g, reference_decode(jp[i])), i

@@ -89,3 +89,29 @@ def test_mjpeg_avi_round_trip(tmp_path):
     videoio.RawAviWriter(raw, 25, (W, H)).release()
     assert not videoio.is_mjpeg_avi(raw)
     assert not videoio.MjpegAviCapture(raw).isOpened()  # cv2-like: a capture that failed to open
+
+
+def test_mjpeg_avi_opendml_continuation(tmp_path):
+    """Frames in an OpenDML 'RIFF AVIX' continuation (files past 1 GB) are read after the first RIFF's."""
+    import struct
+
+    from find_motion_amd import videoio
+    W, H = 32, 16
+    jp = [encode(image(H, W, "smooth", seed=s), quality=80) for s in range(5)]
+    p = str(tmp_path / "big.avi")
+    w = videoio.MjpegAviWriter(p, 30, (W, H))
+    for j in jp[:3]:
+        w.write_jpeg(j)
+    w.release()
+    movi = b"movi" + b"".join(b"00dc" + struct.pack("<I", len(j)) + j + (b"\0" if len(j) & 1 else b"") for j in jp[3:])
+    avix = b"AVIX" + b"LIST" + struct.pack("<I", len(movi)) + movi
+    with open(p, "ab") as f:
+        f.write(b"RIFF" + struct.pack("<I", len(avix)) + avix)
+    cap = videoio.MjpegAviCapture(p)
+    got = []
+    while True:
+        ok, j = cap.read_jpeg()
+        if not ok:
+            break
+        got.append(j)
+    assert got == jp
