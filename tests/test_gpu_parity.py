@@ -375,3 +375,32 @@ def test_batch_size_invariance_1080p():
     assert all(np.array_equal(x, y) for x, y in zip(ma, mb))
     assert np.array_equal(ga, gb)
     assert sum(ca) > 0
+
+
+def test_bench_shape_in_flight_matches_oracle():
+    """bench.py's exact shape (configs[1], mode F): 1080p, k 5, 192-frame launches of the production
+    k_pix5 (no planes), two batches in flight before the first wait, every frame's count, boxes and
+    origins against the oracle, sampled masks, and the final background bit for bit."""
+    W, H, T, NB = 1920, 1080, 192, 2
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    assert eng.max_inflight >= NB
+    frs = [batch(W, H, 1, b * T, T) for b in range(NB)]
+    for fr in frs:
+        eng.submit(fr)
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=5, thresh=12, alpha=0.1))
+    total = 0
+    for b in range(NB):
+        eng.wait()
+        counts = eng.counts()
+        for t in range(T):
+            ref = orc.step(frs[b][t, 0])
+            tag = f"batch {b} frame {t}"
+            assert counts[t, 0] == ref["count"], tag
+            assert [c.bbox for c in eng.contours(t, 0)] == ref["boxes"], tag
+            assert [c.origin for c in eng.contours(t, 0)] == ref["origins"], tag
+            if t % 24 == 0:
+                np.testing.assert_array_equal(eng.mask(t, 0), ref["mask"], err_msg="mask " + tag)
+            total += ref["count"]
+    assert np.array_equal(eng.background(0), orc.bg), "background not bit-identical"
+    assert total > 0
+    eng.close()
