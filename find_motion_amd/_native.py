@@ -497,7 +497,7 @@ class MJpegDecoder:
             raise FMError(rc, f"fm_mjpeg_create: {msg}")
         self.width, self.height, self.max_frames = int(width), int(height), int(max_frames)
         if chunk_bits is not None or spec_bits is not None:  # fm_mjpeg_tune: speed only, same results
-            rc = L.fm_mjpeg_tune(h, int(chunk_bits or 1024), int(512 if spec_bits is None else spec_bits))
+            rc = L.fm_mjpeg_tune(h, int(chunk_bits or 512), int(512 if spec_bits is None else spec_bits))
             if rc != FM_OK:
                 msg = L.fm_mjpeg_last_error(h).decode()
                 self.close()

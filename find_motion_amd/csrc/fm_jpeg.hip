@@ -344,15 +344,21 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
             }
         }
     };
+    // Publication between XCDs without an agent-scope release / acquire: those write back the
+    // whole L2 of the XCD (buffer_wbl2) and invalidate it (buffer_inv) on every poll.  Instead every
+    // field is a relaxed agent-scope atomic (written through to / read from the coherence point);
+    // the writer waits for the fields' stores to complete before it stores the flag, the reader
+    // loads the fields only after it has seen the flag.
     auto publish = [&]() {
         TileState* t = ts + tile;
-        t->p = (uint32_t)(st_out >> 32);
-        t->uk = (int)(uint32_t)st_out;
-        t->cnt = ic;
-        t->dc[0] = id0;
-        t->dc[1] = id1;
-        t->dc[2] = id2;
-        __hip_atomic_store(&t->flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->p, (uint32_t)(st_out >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->uk, (int)(uint32_t)st_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->cnt, ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->dc[0], id0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->dc[1], id1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&t->dc[2], id2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores above are done
+        __hip_atomic_store(&t->flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     for (int it = 0; it < 256; it++) {  // each pass fixes at least the next lane: <= 2 x 64 passes
         if (go) {
@@ -377,7 +383,8 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         if (lane == 63 && valid && f) publish();
         if (lane == 0) {
             const TileState* t = ts + tile - 1;
-            while (__hip_atomic_load(&t->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(1);
+            while (__hip_atomic_load(&t->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the field loads come after the flag's
             lb_state = pack_state(__hip_atomic_load(&t->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                   __hip_atomic_load(&t->uk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             carry_cnt = __hip_atomic_load(&t->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -749,7 +756,7 @@ struct fm_mjpeg {
     size_t chunk0_cap = 0;
     TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
     size_t ts_cap = 0;
-    int CB = 1024, OV = 512;           // chunk and speculation lengths in bits (fm_mjpeg_tune)
+    int CB = 512, OV = 512;            // chunk and speculation lengths in bits (fm_mjpeg_tune)
     HuffDev* d_tabs = nullptr;         // [n_sets][4]
     int tabs_cap = 0;
     uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order

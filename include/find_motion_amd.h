@@ -253,7 +253,7 @@ double fm_mjpeg_last_ms(const fm_mjpeg* dec);
 int fm_submit_jpeg(fm_ctx* ctx, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n_frames);
 /* Tuning of the parallel Huffman decode (no reference counterpart): every entropy-coded segment is
  * cut into chunks of chunk_bits bits, one GPU lane each, and each lane speculates its entry state
- * by decoding from spec_bits bits before its chunk (default 1024 / 512).  Results are identical
+ * by decoding from spec_bits bits before its chunk (default 512 / 512).  Results are identical
  * for any values; only the speed changes. */
 int fm_mjpeg_tune(fm_mjpeg* dec, int chunk_bits, int spec_bits);
 /* The source frame (BGR u8 [H][W][3], cap.read()'s frame.raw, fm.py:501) of (frame, stream) of the
