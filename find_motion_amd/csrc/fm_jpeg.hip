@@ -471,68 +471,84 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 
 // 8 lanes per block: lane r loads zigzag positions 8r..8r+7 (16 B) and scatters them to natural order
 // in LDS, runs column r of pass 1, then row r of pass 2
+constexpr int kIdctGroups = 4;  // groups of 32 blocks per workgroup (their loads issued together)
+
 __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
-                                                    long long nblocks, uint8_t* __restrict__ planes) {
+                                                    int nblocks, uint8_t* __restrict__ planes) {
     __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
-    const long long b = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
-    const bool live = b < nblocks;
-    const long long fb = live ? b : 0;
-    const long long frame = fb / g.frame_blocks;
-    const long long rem = fb - frame * g.frame_blocks;
-    int ci = 0;
-    while (ci + 1 < g.nc && rem >= g.comp[ci + 1].coef0) ci++;
-    const CompDev& c = g.comp[ci];
-    const long long ib = rem - c.coef0;
-    const int by = (int)(ib / c.bw), bx = (int)(ib - (long long)by * c.bw);
-    const uint16_t* q = qt + ((size_t)frame * kMaxComp + ci) * 64;
-    {
-        const uint4 raw = live ? reinterpret_cast<const uint4*>(coef + (size_t)fb * 64)[r] : make_uint4(0, 0, 0, 0);
-        // leave the block zeroed for the next call's sparse coefficient stores
-        if (live) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
-        const uint2 nat = c_zz8[r];
-        const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+    const int b0 = blockIdx.x * (32 * kIdctGroups) + lb;
+    uint4 raw[kIdctGroups];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
-            ws[lb][n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
+    for (int G = 0; G < kIdctGroups; G++) {
+        const int b = b0 + 32 * G;
+        raw[G] = b < nblocks ? reinterpret_cast<const uint4*>(coef + (size_t)b * 64)[r] : make_uint4(0, 0, 0, 0);
+    }
+    const uint2 nat = c_zz8[r];
+    const int fbk = (int)g.frame_blocks;
+#pragma unroll
+    for (int G = 0; G < kIdctGroups; G++) {
+        const int b = b0 + 32 * G;
+        const bool live = b < nblocks;
+        const int fb = live ? b : 0;
+        const int frame = fb / fbk;
+        const int rem = fb - frame * fbk;
+        int ci = 0;
+        while (ci + 1 < g.nc && rem >= (int)g.comp[ci + 1].coef0) ci++;
+        const CompDev& c = g.comp[ci];
+        const int ib = rem - (int)c.coef0;
+        const int by = ib / c.bw, bx = ib - by * c.bw;
+        const uint16_t* q = qt + ((size_t)frame * kMaxComp + ci) * 64;
+        {
+            const uint4 rw = raw[G];
+            // leave the block zeroed for the next call's sparse coefficient stores (only the 16-B
+            // pieces that hold something: most of a typical block is zero already)
+            if (live && (rw.x | rw.y | rw.z | rw.w)) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
+            const uint32_t w4[4] = {rw.x, rw.y, rw.z, rw.w};
+            if (G) __syncthreads();  // the previous group's pass 2 has read ws
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
+                ws[lb][n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
+            }
+        }
+        __syncthreads();
+        // pass 1: column r (jpeg_idct_islow, with the all-zero-AC column shortcut)
+        int v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = ws[lb][8 * k + r] * (int)q[8 * k + r];
+        if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = v[0] * 4;
+        } else {
+            int o[8];
+            idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+#pragma unroll
+            for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = (o[k] + (1 << 10)) >> 11;
+        }
+        __syncthreads();
+        // pass 2: row r (zero-row shortcut), range-limited samples
+        int w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = ws[lb][8 * r + k];
+        uint32_t px[8];
+        if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
+            const uint32_t d = range_idct((w[0] + 16) >> 5);
+#pragma unroll
+            for (int k = 0; k < 8; k++) px[k] = d;
+        } else {
+            int o[8];
+            idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+#pragma unroll
+            for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
+        }
+        if (live) {
+            const int pw = c.bw * 8;
+            uint8_t* row = planes + (size_t)frame * g.frame_plane + c.plane0 + (size_t)(by * 8 + r) * pw + (size_t)bx * 8;
+            reinterpret_cast<uint2*>(row)[0] = make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24,
+                                                          px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
         }
     }
-    __syncthreads();
-    // pass 1: column r (jpeg_idct_islow, with the all-zero-AC column shortcut)
-    int v[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = ws[lb][8 * k + r] * (int)q[8 * k + r];
-    if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = v[0] * 4;
-    } else {
-        int o[8];
-        idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
-#pragma unroll
-        for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = (o[k] + (1 << 10)) >> 11;
-    }
-    __syncthreads();
-    // pass 2: row r (zero-row shortcut), range-limited samples
-    int w[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = ws[lb][8 * r + k];
-    uint32_t px[8];
-    if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
-        const uint32_t d = range_idct((w[0] + 16) >> 5);
-#pragma unroll
-        for (int k = 0; k < 8; k++) px[k] = d;
-    } else {
-        int o[8];
-        idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
-#pragma unroll
-        for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
-    }
-    if (!live) return;
-    const int pw = c.bw * 8;
-    uint8_t* row = planes + (size_t)frame * g.frame_plane + c.plane0 + ((size_t)by * 8 + r) * pw + (size_t)bx * 8;
-    reinterpret_cast<uint2*>(row)[0] = make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24,
-                                                  px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
 }
 
 __device__ __forceinline__ int clamp255(int x) { return x < 0 ? 0 : x > 255 ? 255 : x; }
@@ -1281,8 +1297,9 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
                        d->OV, d->d_ts, reinterpret_cast<uint32_t*>(d->d_ts + ntiles), d->d_coef);
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
-    hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 31) / 32)), dim3(256), 0, st, d->d_coef, d->d_qt, d->g, nb,
-                       d->d_planes);
+    if (nb >= INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "too many coefficient blocks in one call");
+    hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
+                       d->d_coef, d->d_qt, d->g, (int)nb, d->d_planes);
     JHIP(d, hipGetLastError());
     // colour bands: as many rows as keep the staging within 48 KB of LDS
     int rb = 16;
