@@ -24,6 +24,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -755,8 +759,73 @@ using namespace fm::jp;
 // ---------------------------------------------------------------------------------------------
 // host side
 
+// A few persistent host threads for the per-frame parsing and unstuffing (thread start-up per call
+// would cost more than the work): run(n, fn) calls fn(i) for i in [0, n), the caller included.
+class FramePool {
+public:
+    explicit FramePool(int nthreads) {
+        for (int t = 0; t < nthreads; t++) th_.emplace_back([this]() { loop(); });
+    }
+    ~FramePool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int n, const std::function<void(int)>& fn) {
+        if (th_.empty() || n < 16) {
+            for (int i = 0; i < n; i++) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            busy_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        for (int i; (i = next_.fetch_add(1)) < n;) fn(i);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this]() { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* fn;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+                n = n_;
+            }
+            for (int i; (i = next_.fetch_add(1)) < n;) (*fn)(i);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int n_ = 0, busy_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 struct fm_mjpeg {
     int device = 0, W = 0, H = 0, max_frames = 0;
+    FramePool* pool = nullptr;  // host threads for parsing / unstuffing
     std::string err;
     bool have_geom = false;
     JpegGeom g{};
@@ -826,24 +895,6 @@ int pfail(std::string& err, int code, const char* fmt, ...) {
     va_end(ap);
     err = buf;
     return code;
-}
-
-// fn(i) for i in [0, n) on up to 8 host threads (frames are independent)
-template <typename F>
-void parallel_for(int n, F&& fn) {
-    const int nt = std::max(1, std::min({8, (int)std::thread::hardware_concurrency(), n / 8}));
-    if (nt == 1) {
-        for (int i = 0; i < n; i++) fn(i);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(nt - 1);
-    for (int t = 1; t < nt; t++)
-        th.emplace_back([&, t]() {
-            for (int i = t; i < n; i += nt) fn(i);
-        });
-    for (int i = 0; i < n; i += nt) fn(i);
-    for (auto& x : th) x.join();
 }
 
 struct HuffHost {
@@ -1107,6 +1158,7 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
         JHIP(d, hipEventCreateWithFlags(&H.done, hipEventDisableTiming));
     }
     JHIP(d, hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
+    d->pool = new FramePool(std::max(0, std::min(7, (int)std::thread::hardware_concurrency() - 1)));
     return FM_OK;
 }
 
@@ -1122,6 +1174,7 @@ void fm_mjpeg_destroy(fm_mjpeg* d) {
         if (H.done) (void)hipEventDestroy(H.done);
     }
     if (d->last_ev) (void)hipEventDestroy(d->last_ev);
+    delete d->pool;
     if (d->e0) (void)hipEventDestroy(d->e0);
     if (d->e1) (void)hipEventDestroy(d->e1);
     if (d->st) (void)hipStreamDestroy(d->st);
@@ -1149,6 +1202,7 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     if (!d) return FM_EINVAL;
     if (!jpegs || !sizes || !out || n < 1 || n > d->max_frames)
         return jfail(d, FM_EINVAL, "n %d outside [1, max_frames=%d] or null buffers", n, d->max_frames);
+    if (!d->pool) return jfail(d, FM_ESTATE, "decoder not initialised (fm_mjpeg_create failed)");
     JHIP(d, hipSetDevice(d->device));
     if (!st) st = d->st;
     // the staging set's previous uploads must be done before it is refilled; the device buffers are
@@ -1162,9 +1216,7 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     {   // marker parsing, frames in parallel (errors reported for the first failing frame)
         std::vector<int> prc(n, FM_OK);
         std::vector<std::string> perr(n);
-        parallel_for(n, [&](int i) {
-            prc[i] = parse_jpeg(perr[i], i, jpegs[i], sizes[i], P[i]);
-        });
+        d->pool->run(n, [&](int i) { prc[i] = parse_jpeg(perr[i], i, jpegs[i], sizes[i], P[i]); });
         for (int i = 0; i < n; i++)
             if (prc[i]) return jfail(d, prc[i], "%s", perr[i].c_str());
     }
@@ -1214,7 +1266,7 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     const long long nmcu = (long long)g.mcux * g.mcuy;
     std::vector<std::vector<Seg>> fsegs(n);
     std::vector<int> frc(n, FM_OK);
-    parallel_for(n, [&](int i) {
+    d->pool->run(n, [&](int i) {
         const ParsedJpeg& J = P[i];
         const uint8_t* s = jpegs[i];
         std::vector<Seg>& segs = fsegs[i];
