@@ -272,7 +272,8 @@ constexpr int kHuffWaves = 4;
 //      buffer, which k_jpeg_idct leaves zeroed behind it.
 __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __restrict__ stream, uint32_t stream_len,
                                                                 const Seg* __restrict__ segs, int nseg,
-                                                                const uint32_t* __restrict__ seg_chunk0, int nchunks,
+                                                                const uint32_t* __restrict__ seg_chunk0, int chunk0,
+                                                                int nchunks,
                                                                 const HuffDev* __restrict__ tabs, JpegGeom g, int CB, int OV,
                                                                 TileState* __restrict__ ts, uint32_t* __restrict__ tile_ctr,
                                                                 int16_t* __restrict__ coef) {
@@ -295,8 +296,8 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     int tile = 0;
     if (lane == 0) tile = (int)atomicAdd(tile_ctr, 1u);
     tile = __shfl(tile, 0);
-    if (tile * 64 >= nchunks) return;  // the grid's spare waves (whole waves: no barrier follows)
-    const int c = tile * 64 + lane;
+    if (chunk0 + tile * 64 >= nchunks) return;  // the grid's spare waves (whole waves: no barrier follows)
+    const int c = chunk0 + tile * 64 + lane;  // chunks [chunk0, nchunks) belong to this launch's segments
     const bool valid = c < nchunks;
     // the chunk's segment: last s with seg_chunk0[s] <= c
     int lo = 0, hi = nseg - 1;
@@ -858,6 +859,7 @@ struct fm_mjpeg {
         uint32_t* chunk0 = nullptr;
         size_t chunk0_cap = 0;
         HuffDev* tabs = nullptr;
+        size_t tabs_cap = 0;
         uint16_t* qt = nullptr;
         hipEvent_t done = nullptr;  // the set's uploads are finished
         bool used = false;
@@ -1155,6 +1157,7 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
     JHIP(d, hipEventCreate(&d->e1));
     for (auto& H : d->hs) {
         JHIP(d, hipHostMalloc((void**)&H.tabs, 4 * sizeof(HuffDev), hipHostMallocDefault));
+        H.tabs_cap = 4;
         JHIP(d, hipEventCreateWithFlags(&H.done, hipEventDisableTiming));
     }
     JHIP(d, hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
@@ -1223,39 +1226,66 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     if (!d->have_geom)
         if (int rc = setup_geometry(d, P[0])) return rc;
     const JpegGeom& g = d->g;
-    // tables: every frame must use the first frame's Huffman tables (MJPEG streams repeat one set);
-    // quantization tables may differ per frame
-    int sel[kMaxComp][2];
-    for (int c = 0; c < g.nc; c++) {
-        int k = 0;
-        while (k < P[0].ns && P[0].sid[k] != P[0].cid[c]) k++;
-        if (k == P[0].ns) return jfail(d, FM_EINVAL, "frame 0: component %d not in the scan", P[0].cid[c]);
-        sel[c][0] = P[0].std_[k] & 3;
-        sel[c][1] = P[0].sta[k] & 3;
-    }
+    // Huffman tables: per frame, each class (DC, AC) may use two distinct table ids (slots 0, 1 in
+    // order of first use by the components); consecutive frames with the same slots and table
+    // contents form a run, decoded by one launch of k_jpeg_huff with that run's four tables
+    // (MJPEG streams normally repeat one set: one run).  Quantization tables may differ per frame.
+    struct TabSet {
+        int slot[kMaxComp][2];
+        const HuffHost* t[2][2];
+    };
+    std::vector<TabSet> fsets(n);
     for (int i = 0; i < n; i++) {
         const ParsedJpeg& J = P[i];
         if (J.W != g.W || J.H != g.H || J.nc != g.nc) return jfail(d, FM_EINVAL, "frame %d: geometry differs", i);
+        TabSet& ts_ = fsets[i];
+        int ids[2][2] = {{-1, -1}, {-1, -1}};
         for (int c = 0; c < g.nc; c++) {
             if (J.ch[c] != g.comp[c].h || J.cv[c] != g.comp[c].v) return jfail(d, FM_EINVAL, "frame %d: sampling differs", i);
             if (!J.qt_present[J.ctq[c]]) return jfail(d, FM_EINVAL, "frame %d: missing DQT %d", i, J.ctq[c]);
+            int k = 0;
+            while (k < J.ns && J.sid[k] != J.cid[c]) k++;
+            if (k == J.ns) return jfail(d, FM_EINVAL, "frame %d: component %d not in the scan", i, J.cid[c]);
             for (int t = 0; t < 2; t++) {
-                const HuffHost& a = J.ht[t][sel[c][t]];
-                const HuffHost& b = P[0].ht[t][sel[c][t]];
-                if (!a.present) return jfail(d, FM_EINVAL, "frame %d: missing DHT", i);
-                if (i && (a.n != b.n || memcmp(a.bits, b.bits, sizeof a.bits) || memcmp(a.vals, b.vals, a.n)))
-                    return jfail(d, FM_ENOTSUP, "frame %d: Huffman tables differ from frame 0's", i);
+                const int id = (t ? J.sta[k] : J.std_[k]) & 3;
+                if (!J.ht[t][id].present) return jfail(d, FM_EINVAL, "frame %d: missing DHT", i);
+                int sl = ids[t][0] == id ? 0 : ids[t][1] == id ? 1 : -1;
+                if (sl < 0) {
+                    sl = ids[t][0] < 0 ? 0 : ids[t][1] < 0 ? 1 : -1;
+                    if (sl < 0) return jfail(d, FM_ENOTSUP, "frame %d: more than two %s tables in the scan", i, t ? "AC" : "DC");
+                    ids[t][sl] = id;
+                }
+                ts_.slot[c][t] = sl;
             }
         }
+        for (int t = 0; t < 2; t++)
+            for (int sl = 0; sl < 2; sl++) ts_.t[t][sl] = ids[t][sl] >= 0 ? &J.ht[t][ids[t][sl]] : nullptr;
     }
-    // slots 0..3 = (dc, ac) x 2 distinct ids at most
-    for (int c = 0; c < g.nc; c++) {
-        d->g.comp[c].dc = sel[c][0] & 1;
-        d->g.comp[c].ac = 2 + (sel[c][1] & 1);
-    }
-    for (int t = 0; t < 2; t++) {
-        build_table(P[0].ht[0][t], H.tabs[t], true);
-        build_table(P[0].ht[1][t], H.tabs[2 + t], false);
+    auto same_set = [&](const TabSet& x, const TabSet& y) {
+        for (int c = 0; c < g.nc; c++)
+            if (x.slot[c][0] != y.slot[c][0] || x.slot[c][1] != y.slot[c][1]) return false;
+        for (int t = 0; t < 2; t++)
+            for (int sl = 0; sl < 2; sl++) {
+                const HuffHost *p = x.t[t][sl], *q = y.t[t][sl];
+                if (!p != !q) return false;
+                if (p && (p->n != q->n || memcmp(p->bits, q->bits, sizeof p->bits) || memcmp(p->vals, q->vals, p->n)))
+                    return false;
+            }
+        return true;
+    };
+    std::vector<int> run_first;  // first frame of each run
+    for (int i = 0; i < n; i++)
+        if (i == 0 || !same_set(fsets[i], fsets[run_first.back()])) run_first.push_back(i);
+    const int nruns = (int)run_first.size();
+    if (int rc = grow_host(d, &H.tabs, H.tabs_cap, (size_t)nruns * 4)) return rc;
+    for (int r = 0; r < nruns; r++) {
+        const TabSet& ts_ = fsets[run_first[r]];
+        for (int t = 0; t < 2; t++)
+            for (int sl = 0; sl < 2; sl++) {
+                HuffDev& hd = H.tabs[r * 4 + 2 * t + sl];
+                if (ts_.t[t][sl]) build_table(*ts_.t[t][sl], hd, t == 0);
+                else memset(&hd, 0, sizeof hd);
+            }
     }
     // entropy-coded bytes: stuffing and RSTn removed, one segment per restart interval, each followed
     // by kSegPad zero bytes; frame i writes its own region of the staging buffer (bounded by its scan
@@ -1317,36 +1347,63 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     if (int rc = grow_host(d, &H.segs, H.segs_cap, segs.size())) return rc;
     memcpy(H.segs, segs.data(), segs.size() * sizeof(Seg));
     // chunks of CB bits per segment (at least one), 64 per tile
+    // each run's chunks start on a tile boundary (tiles never span runs: no look-back between them)
     const int nseg = (int)segs.size();
     if (int rc = grow_host(d, &H.chunk0, H.chunk0_cap, (size_t)nseg + 1)) return rc;
-    size_t nchunks = 0;
-    for (int i = 0; i < nseg; i++) {
-        H.chunk0[i] = (uint32_t)nchunks;
-        nchunks += std::max<size_t>(1, ((size_t)segs[i].len * 8 + d->CB - 1) / d->CB);
+    std::vector<int> run_seg(nruns + 1, nseg);        // first segment of each run
+    std::vector<size_t> run_chunk(nruns + 1), run_end(nruns), run_tile(nruns + 1);
+    {
+        int r = 0;
+        for (int i = 0; i < nseg && r < nruns; i++)
+            while (r < nruns && segs[i].frame >= run_first[r]) run_seg[r++] = i;
     }
+    size_t nchunks = 0, ntiles = 0;
+    for (int r = 0; r < nruns; r++) {
+        nchunks = (nchunks + 63) & ~(size_t)63;
+        run_chunk[r] = nchunks;
+        run_tile[r] = ntiles;
+        for (int i = run_seg[r]; i < run_seg[r + 1]; i++) {
+            H.chunk0[i] = (uint32_t)nchunks;
+            nchunks += std::max<size_t>(1, ((size_t)segs[i].len * 8 + d->CB - 1) / d->CB);
+        }
+        run_end[r] = nchunks;
+        ntiles += (nchunks - run_chunk[r] + 63) / 64;
+    }
+    run_chunk[nruns] = nchunks;
+    run_tile[nruns] = ntiles;
     H.chunk0[nseg] = (uint32_t)nchunks;
     if (nchunks >= (size_t)INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "compressed batch too large");
-    const size_t ntiles = (nchunks + 63) / 64;
     if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + kStreamSlack)) return rc;  // look-ahead reads
     if (int rc = grow_dev(d, &d->d_segs, d->segs_cap, segs.size())) return rc;
     if (int rc = grow_dev(d, &d->d_chunk0, d->chunk0_cap, (size_t)nseg + 1)) return rc;
-    if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + 1)) return rc;
+    if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + nruns)) return rc;  // + one tile counter per run
     size_t tcap = d->tabs_cap;
-    if (int rc = grow_dev(d, &d->d_tabs, tcap, 4)) return rc;
+    if (int rc = grow_dev(d, &d->d_tabs, tcap, (size_t)nruns * 4)) return rc;
     d->tabs_cap = (int)tcap;
     JHIP(d, hipMemcpyAsync(d->d_stream, H.stream, w, hipMemcpyHostToDevice, st));
     JHIP(d, hipMemcpyAsync(d->d_segs, H.segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
     JHIP(d, hipMemcpyAsync(d->d_chunk0, H.chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemsetAsync(d->d_ts, 0, (ntiles + 1) * sizeof(TileState), st));  // flags + the tile counter
-    JHIP(d, hipMemcpyAsync(d->d_tabs, H.tabs, 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemsetAsync(d->d_ts, 0, (ntiles + nruns) * sizeof(TileState), st));  // flags + the tile counters
+    JHIP(d, hipMemcpyAsync(d->d_tabs, H.tabs, (size_t)nruns * 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
     JHIP(d, hipMemcpyAsync(d->d_qt, H.qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
     JHIP(d, hipEventRecord(H.done, st));
     H.used = true;
     d->cur ^= 1;
     if (d->timing) JHIP(d, hipEventRecord(d->e0, st));
-    hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((ntiles + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
-                       d->d_stream, (uint32_t)w, d->d_segs, nseg, d->d_chunk0, (int)nchunks, d->d_tabs, d->g, d->CB,
-                       d->OV, d->d_ts, reinterpret_cast<uint32_t*>(d->d_ts + ntiles), d->d_coef);
+    for (int r = 0; r < nruns; r++) {
+        const int nt = (int)(run_tile[r + 1] - run_tile[r]);
+        if (nt == 0) continue;
+        JpegGeom gr = d->g;  // this run's table slots
+        for (int c = 0; c < g.nc; c++) {
+            gr.comp[c].dc = fsets[run_first[r]].slot[c][0];
+            gr.comp[c].ac = 2 + fsets[run_first[r]].slot[c][1];
+        }
+        hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((nt + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
+                           d->d_stream, (uint32_t)w, d->d_segs + run_seg[r], run_seg[r + 1] - run_seg[r],
+                           d->d_chunk0 + run_seg[r], (int)run_chunk[r], (int)run_end[r], d->d_tabs + 4 * r, gr,
+                           d->CB, d->OV, d->d_ts + run_tile[r], reinterpret_cast<uint32_t*>(d->d_ts + ntiles + r),
+                           d->d_coef);
+    }
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
     if (nb >= INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "too many coefficient blocks in one call");

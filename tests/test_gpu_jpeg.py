@@ -71,9 +71,10 @@ def test_refusals():
     with pytest.raises(FMError):  # not a JPEG
         dec.decode([b"\x00" * 64])
     dec.close()
-    dec = MJpegDecoder(16, 16, max_frames=2)
-    with pytest.raises(FMError):  # per-frame optimized Huffman tables differ within one call
-        dec.decode([encode(image(16, 16, "noise", seed=s), quality=75, optimize=True) for s in range(2)])
+    dec = MJpegDecoder(16, 16, max_frames=2)  # per-frame optimized Huffman tables: decoded run by run
+    fr = [encode(image(16, 16, "noise", seed=s), quality=75, optimize=True) for s in range(2)]
+    got = dec.decode(fr)
+    assert all(np.array_equal(got[i], reference_decode(fr[i])) for i in range(2))
 
 
 def test_submit_jpeg_equals_submit_of_decoded_frames():
@@ -156,5 +157,20 @@ def test_corrupt_and_truncated_frames_do_not_fault():
         assert out.shape == (2, 240, 320, 3)
         got = dec.decode(good)
         for i, f in enumerate(good):
+            assert np.array_equal(got[i], reference_decode(f)), (cb, i)
+        dec.close()
+
+
+def test_per_frame_optimized_huffman_tables():
+    """Frames with their own (optimized) Huffman tables, mixed with standard-table frames and with a
+    4:2:0 stream whose chroma use table id 1: decoded per run of frames sharing one table set."""
+    v = SyntheticVideo(320, 240, 9)
+    frames = [encode(v.frame(0), quality=75), encode(v.frame(1), quality=75),            # standard tables: one run
+              encode(v.frame(2), quality=80, optimize=True), encode(v.frame(3), quality=80, optimize=True),
+              encode(v.frame(4), quality=75), encode(image(240, 320, "noise", seed=3), quality=90, optimize=True)]
+    for cb in (512, 64):
+        dec = MJpegDecoder(320, 240, max_frames=len(frames), chunk_bits=cb)
+        got = dec.decode(frames)
+        for i, f in enumerate(frames):
             assert np.array_equal(got[i], reference_decode(f)), (cb, i)
         dec.close()
