@@ -571,6 +571,9 @@ __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor
 // with jdmainct.c's edge replication) are staged in LDS with 8-byte loads, all in flight together;
 // then row by row each thread converts 8 consecutive pixels (chroma upsampled from LDS,
 // ycc_rgb_convert) into a BGR row in LDS (two of them, alternating), stored with 16-byte stores.
+// MODE: 0 grayscale, 1 per-pixel chroma (1x1 chroma, or planes too narrow for the fancy filters),
+// 2 h2v1 fancy upsampling, 3 h2v2 fancy upsampling (straight-line code for the common 4:2:2 / 4:2:0)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g, int rb,
                                                      uint8_t* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
     uint8_t* orow = lds;                     // [2][orow_sz]
     uint8_t* ys = lds + 2 * orow_sz;         // [rb][wr]
     uint8_t* cs = ys + rb * wr;              // [2 comps][nr][cpw]
-    const bool color = g.nc == 3;
+    constexpr bool color = MODE != 0;
     int hf = 1, vf = 1, dw = 0, dh = 0, cpw = 0, r_lo = 0, nr = 0;
     if (color) {
         const CompDev& cc = g.comp[1];
@@ -641,7 +644,8 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
         for (int x0 = threadIdx.x * 8; x0 < g.W; x0 += 256 * 8) {
             const uint2 yy = *reinterpret_cast<const uint2*>(yrow + x0);
             uint32_t bgr[8];
-            if (color && hf == 2 && dw > 2) {
+            if constexpr (MODE >= 2) {
+                constexpr bool V2 = MODE == 3;
                 // fancy h2v1 / h2v2 over chroma columns cx0-1 .. cx0+4, read as three LDS words per row
                 const int cx0 = x0 >> 1;
                 int up[2][8];
@@ -649,7 +653,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
                 for (int comp = 0; comp < 2; comp++) {
                     int cs[6];
 #pragma unroll
-                    for (int rr = 0; rr < 2; rr++) {
+                    for (int rr = 0; rr < (V2 ? 2 : 1); rr++) {
                         const uint8_t* row = (rr ? f0 : n0) + comp * nr * cpw;
                         const uint32_t a = cx0 ? *reinterpret_cast<const uint32_t*>(row + cx0 - 4) : 0u;
                         const uint32_t b = *reinterpret_cast<const uint32_t*>(row + cx0);
@@ -658,7 +662,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
                                            (int)(b >> 24), (int)(c & 255)};
 #pragma unroll
                         for (int q = 0; q < 6; q++) {
-                            if (vf == 2) cs[q] = rr ? cs[q] + v6[q] : v6[q] * 3;  // 3 * nearer + farther
+                            if (V2) cs[q] = rr ? cs[q] + v6[q] : v6[q] * 3;  // 3 * nearer + farther
                             else if (!rr) cs[q] = v6[q];
                         }
                     }
@@ -666,7 +670,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
                     for (int m = 0; m < 4; m++) {
                         const int cx = cx0 + m;
                         const int cc = cs[m + 1], cl = cs[m], cr = cs[m + 2];
-                        if (vf == 2) {
+                        if (V2) {
                             up[comp][2 * m] = cx == 0 ? (cc * 4 + 8) >> 4 : (cc * 3 + cl + 8) >> 4;
                             up[comp][2 * m + 1] = cx == dw - 1 ? (cc * 4 + 7) >> 4 : (cc * 3 + cr + 7) >> 4;
                         } else {
@@ -1421,8 +1425,17 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         if (lds <= 48 * 1024 || rb == 1) break;
     }
     if (lds > 64 * 1024) return jfail(d, FM_ENOTSUP, "frame width %d too large for the colour kernel", g.W);
-    hipLaunchKernelGGL(k_jpeg_color, dim3((unsigned)((g.H + rb - 1) / rb), (unsigned)n), dim3(256), lds, st, d->d_planes, d->g,
-                       rb, out);
+    int mode = 0;
+    if (g.nc == 3) {
+        const int hf = g.hmax / g.comp[1].h, vf = g.vmax / g.comp[1].v;
+        const int dw = (g.W * g.comp[1].h + g.hmax - 1) / g.hmax;
+        mode = (hf == 2 && dw > 2) ? (vf == 2 ? 3 : 2) : 1;
+    }
+    const dim3 cgrid((unsigned)((g.H + rb - 1) / rb), (unsigned)n);
+    if (mode == 3) hipLaunchKernelGGL(k_jpeg_color<3>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
+    else if (mode == 2) hipLaunchKernelGGL(k_jpeg_color<2>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
+    else if (mode == 1) hipLaunchKernelGGL(k_jpeg_color<1>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
+    else hipLaunchKernelGGL(k_jpeg_color<0>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
     JHIP(d, hipEventRecord(d->last_ev, st));
