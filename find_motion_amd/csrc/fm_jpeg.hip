@@ -626,6 +626,8 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
     }
     __syncthreads();
     const int nbytes = g.W * 3;
+    // whole 8-pixel groups and 8-B aligned rows: each thread stores its 24 B itself (no LDS row)
+    const bool direct = (g.W & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
     for (int y = y0; y < y1; y++) {
         uint8_t* ob = orow + ((y - y0) & 1) * orow_sz;
         const uint8_t* yrow = ys + (y - y0) * wr;
@@ -722,6 +724,13 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
                 bgr[i] = ycc_bgr(Y, cbv, crv);
             }
             }
+            if (direct) {  // 24 B straight to the frame: three 8-B stores (the L2 merges the wave's 1.5 KB)
+                uint2* d64 = reinterpret_cast<uint2*>(out + ((size_t)frame * g.H + y) * nbytes + (size_t)x0 * 3);
+                d64[0] = make_uint2(bgr[0] | bgr[1] << 24, bgr[1] >> 8 | bgr[2] << 16);
+                d64[1] = make_uint2(bgr[2] >> 16 | bgr[3] << 8, bgr[4] | bgr[5] << 24);
+                d64[2] = make_uint2(bgr[5] >> 8 | bgr[6] << 16, bgr[6] >> 16 | bgr[7] << 8);
+                continue;
+            }
             uint8_t* dst = ob + (size_t)x0 * 3;
             if (x0 + 8 <= g.W) {  // 24 B at a 4-B aligned LDS address
                 uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
@@ -741,6 +750,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
                 }
             }
         }
+        if (direct) continue;
         __syncthreads();  // (also: every thread is past its stores of the row two back, from this buffer)
         uint8_t* o = out + ((size_t)frame * g.H + y) * nbytes;
         const uintptr_t al = reinterpret_cast<uintptr_t>(o) | (uintptr_t)nbytes;
