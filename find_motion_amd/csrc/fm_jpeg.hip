@@ -68,6 +68,9 @@ struct JpegGeom {
     CompDev comp[kMaxComp];
     int bpm;                  // blocks per MCU (1 for a one-component scan)
     int8_t ucomp[10], udv[10], udh[10];  // block u of an MCU: component and offset in the MCU's block grid
+    // the same per block u as bit fields the Huffman loop reads without a memory access: bit u of
+    // udc / uac = the DC / AC table slot, bits 2u..2u+1 of ucomp2 = the component
+    uint32_t udc, uac, ucomp2;
 };
 
 struct Seg {
@@ -168,7 +171,7 @@ __device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, 
     const long long a = (long long)sg.mcu0 * bpm + n;
     const int m = (int)(a / bpm), uu = (int)(a - (long long)m * bpm);
     const int my = m / g.mcux, mx = m - my * g.mcux;
-    const CompDev& c = g.comp[ut.comp[uu]];
+    const CompDev& c = g.comp[(g.ucomp2 >> (2 * uu)) & 3];
     const int by = g.interleaved ? my * c.v + g.udv[uu] : my, bx = g.interleaved ? mx * c.h + g.udh[uu] : mx;
     return coef + ((size_t)sg.frame * g.frame_blocks + c.coef0 + (long long)by * c.bw + bx) * 64;
 }
@@ -203,7 +206,7 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
         if (WRITE && k == 0 && cnt >= total) break;
         br.refill();
         const bool isdc = k == 0;
-        const HuffDev& t = T[isdc ? ut.dc[u] : ut.ac[u]];
+        const HuffDev& t = T[isdc ? (int)((g.udc >> u) & 1) : 2 + (int)((g.uac >> u) & 1)];
         const uint32_t e = t.lut[br.peek(kLook)];
         int sym, v;
         if (e & kFull) {
@@ -226,7 +229,7 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
         const bool val = isdc || (sym & 15);
         if (isdc) {
             // three scalars and selects: an array indexed by ci would live in scratch
-            const int ci = ut.comp[u];
+            const int ci = (int)((g.ucomp2 >> (2 * u)) & 3);
             const int pred = (ci == 0 ? dc0 : ci == 1 ? dc1 : dc2) + v;
             dc0 = ci == 0 ? pred : dc0;
             dc1 = ci == 1 ? pred : dc1;
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
                                                                 int nchunks,
                                                                 const HuffDev* __restrict__ tabs, JpegGeom g, int CB, int OV,
                                                                 TileState* __restrict__ ts, uint32_t* __restrict__ tile_ctr,
-                                                                int16_t* __restrict__ coef) {
+                                                                int16_t* __restrict__ coef, uint64_t* __restrict__ stamps) {
     __shared__ HuffDev T[4];
     __shared__ UTab ut;
     {
@@ -297,6 +300,12 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     if (lane == 0) tile = (int)atomicAdd(tile_ctr, 1u);
     tile = __shfl(tile, 0);
     if (chunk0 + tile * 64 >= nchunks) return;  // the grid's spare waves (whole waves: no barrier follows)
+    // profiling only (dev build, FM_JPEG_STAMPS): per tile, realtime at start / phase-0 end / look-back
+    // seen / scan done / end, and the hardware id
+    uint64_t* stp = (stamps && lane == 0) ? stamps + (size_t)tile * 6 : nullptr;
+#define JP_STAMP(k) do { if (stp) stp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    JP_STAMP(0);
+    if (stp) stp[5] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     const int c = chunk0 + tile * 64 + lane;  // chunks [chunk0, nchunks) belong to this launch's segments
     const bool valid = c < nchunks;
     // the chunk's segment: last s with seg_chunk0[s] <= c
@@ -382,6 +391,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
             mark = (uint32_t)(pv >> 32);
             continue;
         }
+        if (phase == 0) JP_STAMP(1);
         if (phase == 1 || !need_lb) break;
         // consistent with lane 0's speculation: a tile holding a segment head publishes now
         scan();
@@ -389,6 +399,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         if (lane == 0) {
             const TileState* t = ts + tile - 1;
             while (__hip_atomic_load(&t->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(1);
+            JP_STAMP(2);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the field loads come after the flag's
             lb_state = pack_state(__hip_atomic_load(&t->p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                   __hip_atomic_load(&t->uk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -401,6 +412,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         go = false;
     }
     // 3. scan with the previous tile's totals for the lanes of lane 0's segment
+    JP_STAMP(3);
     scan();
     if (need_lb) {
         carry_cnt = __shfl(carry_cnt, 0);
@@ -423,6 +435,8 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     br.init(stream, sg.off, p_in, send);
     int wuk = uk_in;
     run_symbols<true>(br, wuk, 0, ce, T, ut, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef);
+    JP_STAMP(4);
+#undef JP_STAMP
 }
 
 // jidctint.c constants (CONST_BITS 13)
@@ -857,6 +871,9 @@ struct fm_mjpeg {
     TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
     size_t ts_cap = 0;
     int CB = 512, OV = 512;            // chunk and speculation lengths in bits (fm_mjpeg_tune)
+    uint64_t* d_stamps = nullptr;      // dev build, FM_JPEG_STAMPS: per-tile phase stamps of k_jpeg_huff
+    size_t stamps_cap = 0;
+    size_t stamps_n = 0;
     HuffDev* d_tabs = nullptr;         // [n_sets][4]
     int tabs_cap = 0;
     uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
@@ -1183,7 +1200,7 @@ void fm_mjpeg_destroy(fm_mjpeg* d) {
     if (!d) return;
     if (d->st) (void)hipStreamSynchronize(d->st);
     for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef,
-                    (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts})
+                    (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts, (void*)d->d_stamps})
         if (p) (void)hipFree(p);
     for (auto& H : d->hs) {
         for (void* p : {(void*)H.stream, (void*)H.segs, (void*)H.tabs, (void*)H.qt, (void*)H.chunk0})
@@ -1391,6 +1408,13 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     if (int rc = grow_dev(d, &d->d_segs, d->segs_cap, segs.size())) return rc;
     if (int rc = grow_dev(d, &d->d_chunk0, d->chunk0_cap, (size_t)nseg + 1)) return rc;
     if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + nruns)) return rc;  // + one tile counter per run
+#ifdef FM_DEV_SWITCHES
+    if (getenv("FM_JPEG_STAMPS")) {
+        if (int rc = grow_dev(d, &d->d_stamps, d->stamps_cap, ntiles * 6)) return rc;
+        d->stamps_n = ntiles;
+        JHIP(d, hipMemsetAsync(d->d_stamps, 0, ntiles * 6 * sizeof(uint64_t), st));
+    }
+#endif
     size_t tcap = d->tabs_cap;
     if (int rc = grow_dev(d, &d->d_tabs, tcap, (size_t)nruns * 4)) return rc;
     d->tabs_cap = (int)tcap;
@@ -1412,11 +1436,18 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
             gr.comp[c].dc = fsets[run_first[r]].slot[c][0];
             gr.comp[c].ac = 2 + fsets[run_first[r]].slot[c][1];
         }
+        gr.udc = gr.uac = gr.ucomp2 = 0;
+        for (int u = 0; u < gr.bpm; u++) {
+            const int c = gr.ucomp[u];
+            gr.udc |= (uint32_t)gr.comp[c].dc << u;
+            gr.uac |= (uint32_t)(gr.comp[c].ac - 2) << u;
+            gr.ucomp2 |= (uint32_t)c << (2 * u);
+        }
         hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((nt + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
                            d->d_stream, (uint32_t)w, d->d_segs + run_seg[r], run_seg[r + 1] - run_seg[r],
                            d->d_chunk0 + run_seg[r], (int)run_chunk[r], (int)run_end[r], d->d_tabs + 4 * r, gr,
                            d->CB, d->OV, d->d_ts + run_tile[r], reinterpret_cast<uint32_t*>(d->d_ts + ntiles + r),
-                           d->d_coef);
+                           d->d_coef, d->d_stamps ? d->d_stamps + 6 * run_tile[r] : nullptr);
     }
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
@@ -1468,6 +1499,16 @@ int fm_mjpeg_decode(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* size
     if (!out_on_device) JHIP(d, hipMemcpyAsync(out, dst, (size_t)n * fb, hipMemcpyDeviceToHost, d->st));
     JHIP(d, hipStreamSynchronize(d->st));
     JHIP(d, hipEventElapsedTime(&d->last_ms, d->e0, d->e1));
+#ifdef FM_DEV_SWITCHES
+    if (const char* path = getenv("FM_JPEG_STAMPS")) {
+        std::vector<uint64_t> h(d->stamps_n * 6);
+        JHIP(d, hipMemcpy(h.data(), d->d_stamps, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* fp = fopen(path, "wb")) {
+            fwrite(h.data(), 8, h.size(), fp);
+            fclose(fp);
+        }
+    }
+#endif
     return FM_OK;
 }
 
