@@ -12,7 +12,7 @@ $HIPCC -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function --offlo
   -c -x hip "$ROOT/find_motion_amd/csrc/$SRC" -o "$D/$B.o"
 O=$ROOT/build/fm_obj
 OBJS=""
-for o in fm_kernels fm_fused fm_pix fm_ccl fm_haar fm_capi fm_raster; do
+for o in fm_kernels fm_fused fm_pix fm_ccl fm_haar fm_jpeg fm_capi fm_raster; do
   if [ "$o" = "$B" ]; then OBJS="$OBJS $D/$B.o"; else OBJS="$OBJS $O/$o.o"; fi
 done
 $HIPCC -shared -fPIC --offload-arch=gfx950 -o "$D/libfm_hip.so" $OBJS
