@@ -62,11 +62,13 @@ class BatchFeeder:
         self.caps = list(caps)
         self.T = int(batch)
         self.depth = max(1, min(depth or engine.max_inflight, engine.max_inflight))
-        # JPEG mode needs every capture to hand out compressed frames (None: when they all can)
-        can = bool(self.caps) and all(hasattr(c, "read_jpeg") for c in self.caps)
+        # JPEG mode needs every capture to hand out compressed frames of one layout (size and chroma
+        # sampling: one GPU decoder serves the whole batch); None: whenever they do, otherwise the
+        # captures decode (cap.read())
+        can = bool(self.caps) and all(hasattr(c, "read_jpeg") for c in self.caps) and self._one_layout()
         self.jpeg = can if jpeg is None else bool(jpeg)
         if self.jpeg and not can:
-            raise ValueError("JPEG mode needs captures with read_jpeg()")
+            raise ValueError("JPEG mode needs captures with read_jpeg() and one JPEG layout")
         self.decoder = None
         if self.jpeg:
             from ._native import MJpegDecoder
@@ -87,6 +89,20 @@ class BatchFeeder:
         self._copiers = ThreadPoolExecutor(max(1, min(8, len(os.sched_getaffinity(0)))), "fm-copy")
         self._thread = threading.Thread(target=self._decode, name="fm-decode", daemon=True)
         self._thread.start()
+
+    def _one_layout(self) -> bool:
+        from .videoio import jpeg_layout
+        layouts = set()
+        for c in self.caps:
+            peek = getattr(c, "peek_jpeg", None)
+            j = peek() if peek else None
+            if j is None:
+                continue  # an empty stream (or one that cannot be inspected) constrains nothing
+            try:
+                layouts.add(jpeg_layout(j))
+            except ValueError:
+                return False
+        return len(layouts) <= 1
 
     @staticmethod
     def make_buffers(engine, batch: int, depth: int | None = None) -> list:

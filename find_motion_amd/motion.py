@@ -316,7 +316,7 @@ class VideoMotion:
 
     def _load_video(self) -> bool:
         """fm.py:409-424, plus engine creation and the one-time mask rasterisation."""
-        self.cap = videoio.open_capture(self._capture if self._capture is not None else self.filename)
+        self.cap = videoio.open_capture(self._capture if self._capture is not None else self.filename, self.device)
         self.frame_cache = deque(maxlen=self.cache_frames)
         try:
             self._get_video_info()
@@ -698,7 +698,7 @@ class StreamGroup:
         S = len(self.filenames)
         if S == 0:
             raise ValueError("More than 0 files needed")
-        caps = [videoio.open_capture(c if c is not None else f)
+        caps = [videoio.open_capture(c if c is not None else f, device)
                 for f, c in zip(self.filenames, captures or [None] * S)]
         w = {int(c.get(videoio.CAP_PROP_FRAME_WIDTH)) for c in caps}
         h = {int(c.get(videoio.CAP_PROP_FRAME_HEIGHT)) for c in caps}

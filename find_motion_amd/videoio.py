@@ -108,6 +108,9 @@ class JpegListCapture:
         self._i += 1
         return True, j
 
+    def peek_jpeg(self):
+        return self._jpegs[self._i] if self._open and self._i < len(self._jpegs) else None
+
     def read(self):
         ok, j = self.read_jpeg()
         if not ok:
@@ -126,6 +129,22 @@ class JpegListCapture:
         if self._dec is not None:
             self._dec.close()
             self._dec = None
+
+
+def jpeg_layout(data: bytes):
+    """(height, width, ((h, v) sampling factors per component)) from a JPEG's SOF marker: frames of one
+    GPU decode call must share it."""
+    i = 2
+    while i + 9 < len(data):
+        if data[i] != 0xFF:
+            raise ValueError("not a JPEG marker stream")
+        m = data[i + 1]
+        if 0xC0 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+            nc = data[i + 9]
+            comps = tuple((data[i + 11 + 3 * c] >> 4, data[i + 11 + 3 * c] & 15) for c in range(nc))
+            return (data[i + 5] << 8) | data[i + 6], (data[i + 7] << 8) | data[i + 8], comps
+        i += 2 + ((data[i + 2] << 8) | data[i + 3])
+    raise ValueError("no SOF marker")
 
 
 def _jpeg_size(data: bytes):
@@ -369,6 +388,13 @@ class MjpegAviCapture(RawAviCapture):
         self._i += 1
         return True, bytes(self._mm[off: off + ln])
 
+    def peek_jpeg(self):
+        """The next frame's JPEG bytes without consuming it (None at the end)."""
+        if not self._open or self._i >= len(self._offsets):
+            return None
+        off, ln = self._offsets[self._i]
+        return bytes(self._mm[off: off + ln])
+
     def read(self):
         ok, j = self.read_jpeg()
         if not ok:
@@ -462,7 +488,7 @@ def is_mjpeg_avi(path) -> bool:
     return head[:4] == b"RIFF" and head[8:12] == b"AVI " and FOURCC_MJPG in head
 
 
-def open_capture(source):
+def open_capture(source, device: int = 0):
     """cv2.VideoCapture(source) when OpenCV exists (fm.py:413); otherwise the readers above.
 
     `source` may also be an object that already speaks the capture protocol,
@@ -479,7 +505,7 @@ def open_capture(source):
     if isinstance(source, str) and source.endswith(".npy"):
         return ArrayCapture(np.load(source, mmap_mode="r", allow_pickle=False))
     if isinstance(source, str) and is_mjpeg_avi(source):
-        return MjpegAviCapture(source)  # compressed frames to the GPU decoder (§8(f)-3)
+        return MjpegAviCapture(source, device)  # compressed frames to the GPU decoder (§8(f)-3)
     if cv2 is not None:
         return cv2.VideoCapture(source)
     if isinstance(source, int):

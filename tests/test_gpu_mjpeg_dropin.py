@@ -130,3 +130,17 @@ def test_cli_on_mjpeg_file(tmp_path, codec):
         assert len(got) == len(want)
         for g, i in zip(got, want):
             assert np.array_equal(g, reference_decode(jp[i])), i
+
+
+def test_stream_group_mixed_chroma_sampling(tmp_path):
+    """Same-size MJPEG streams with different chroma sampling (4:2:0 and 4:2:2) cannot share one GPU
+    decode call: the feeder leaves JPEG mode and the captures decode frame by frame (on the GPU);
+    decisions still equal the oracle's."""
+    W, H, n = 320, 180, 24
+    srcs = [tmp_path / "a.avi", tmp_path / "b.avi"]
+    jps = [_mjpeg_avi(srcs[0], W, H, n, 0, quality=80), _mjpeg_avi(srcs[1], W, H, n, 1, quality=80, subsampling=1)]
+    grp = motion.StreamGroup([str(p) for p in srcs], batch=6, box_size=320, blur_scale=64, threshold=12,
+                             cache_time=0.3, min_time=0.1, outdir=str(tmp_path))
+    grp.find_motion()
+    for s, v in enumerate(grp.videos):
+        assert v.written_indices == _oracle_written(jps[s], W, H, 320), s

@@ -115,3 +115,12 @@ def test_mjpeg_avi_opendml_continuation(tmp_path):
             break
         got.append(j)
     assert got == jp
+
+
+def test_jpeg_layout():
+    from find_motion_amd import videoio
+    assert videoio.jpeg_layout(encode(image(24, 40, "smooth"), quality=75)) == (24, 40, ((2, 2), (1, 1), (1, 1)))
+    assert videoio.jpeg_layout(encode(image(24, 40, "smooth"), quality=75, subsampling=1))[2] == ((2, 1), (1, 1), (1, 1))
+    assert videoio.jpeg_layout(encode(image(24, 40, "smooth")[..., 0], quality=75)) == (24, 40, ((1, 1),))
+    cap = videoio.JpegListCapture([encode(image(24, 40, "smooth"), quality=75)])
+    assert cap.peek_jpeg() is not None and cap.read_jpeg()[0] and cap.peek_jpeg() is None
