@@ -9,17 +9,19 @@
 //           per restart interval (the whole scan without DRI);
 //   k_jpeg_huff   self-synchronizing parallel Huffman decode: each segment cut into chunks of CB bits,
 //           one lane per chunk, entry states speculated and fixed up through a chained look-back
-//           (see the kernel); 9-bit lookahead tables in LDS, canonical slow path past 9 bits, DC
-//           prediction; quantized coefficients written in zigzag order, int16 [frame][comp][block][64];
+//           (see the kernel); 10-bit lookahead tables in LDS that also return the extra bits'
+//           value, canonical slow path past 10 bits, DC prediction; non-zero quantized coefficients
+//           stored in zigzag order into int16 [frame][comp][block][64] (zeroed by k_jpeg_idct);
 //   k_jpeg_idct   8 lanes per block: dequantize + jpeg_idct_islow (jidctint.c: CONST_BITS 13,
 //           PASS1_BITS 2, zero-column / zero-row shortcuts, IDCT range-limit table) into component
 //           planes;
-//   k_jpeg_color  one workgroup per output row, chroma rows staged in LDS, 8 pixels per thread: fancy
-//           upsampling (jdsample.c h2v1/h2v2 with the edge-replicated context rows of jdmainct.c) and
-//           ycc_rgb_convert (jdcolor.c tables) -> BGR u8 HWC, the cv2.VideoCapture layout, straight
-//           into the caller's frame buffer.
+//   k_jpeg_color  one workgroup per band of 16 output rows (Y and chroma rows staged in LDS), 8 pixels
+//           per thread: fancy upsampling (jdsample.c h2v1/h2v2 with the edge-replicated context rows of
+//           jdmainct.c) and ycc_rgb_convert (jdcolor.c tables) -> BGR u8 HWC, the cv2.VideoCapture
+//           layout, straight into the caller's frame buffer.
 // Supported: 8-bit baseline / extended-sequential Huffman, grayscale or 3-component YCbCr with
-// Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2; restart intervals optional.  Anything else: FM_ENOTSUP.
+// Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2; restart intervals optional; quantization and Huffman
+// tables may change from frame to frame.  Anything else: FM_ENOTSUP.
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -149,10 +151,6 @@ __device__ __forceinline__ int huff_slow(uint32_t c16, const HuffDev& t) {
     return 16 << 8;
 }
 
-// the per-block tables a lane needs, in LDS
-struct UTab {
-    uint8_t dc[10], ac[10], comp[10];
-};
 
 __device__ __forceinline__ uint64_t pack_state(uint32_t p, int uk) { return (uint64_t)p << 32 | (uint32_t)uk; }
 
@@ -167,7 +165,7 @@ __device__ __forceinline__ uint64_t pack_state(uint32_t p, int uk) { return (uin
 // part of it inside this chunk) is flushed to its place in the coefficient buffer; decoding stops
 // once the segment's `total` blocks are complete.
 // the coefficient block (zigzag order) of block n of segment sg
-__device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, const UTab& ut, const Seg& sg, int bpm, int n) {
+__device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, const Seg& sg, int bpm, int n) {
     const long long a = (long long)sg.mcu0 * bpm + n;
     const int m = (int)(a / bpm), uu = (int)(a - (long long)m * bpm);
     const int my = m / g.mcux, mx = m - my * g.mcux;
@@ -186,14 +184,13 @@ __device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, 
 // predictors; each value is stored at its zigzag position of its block in the (zeroed) coefficient
 // buffer; decoding stops once the segment's `total` blocks are complete.
 template <bool WRITE>
-__device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mark, uint32_t end, const HuffDev* T,
-                                            const UTab& ut, int bpm, int& cnt, int& dc0, int& dc1, int& dc2, uint32_t& p_in,
+__device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mark, uint32_t end, const HuffDev* T, int bpm, int& cnt, int& dc0, int& dc1, int& dc2, uint32_t& p_in,
                                             int& uk_in, int total, const JpegGeom& g, const Seg& sg, int16_t* coef) {
     int u = uk >> 6, k = uk & 63;
     bool marked = WRITE;
     // (corrupt data can give counts past the segment's blocks: nothing is stored for those)
     bool wr = WRITE && k && cnt >= 1 && cnt <= total;
-    int16_t* blk = wr ? block_ptr(coef, g, ut, sg, bpm, cnt - 1) : coef;
+    int16_t* blk = wr ? block_ptr(coef, g, sg, bpm, cnt - 1) : coef;
     while (true) {
         if (!WRITE && !marked && br.pos >= mark) {
             marked = true;
@@ -237,7 +234,7 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
             v = pred;
             if (WRITE) {
                 wr = cnt >= 0;
-                blk = wr ? block_ptr(coef, g, ut, sg, bpm, cnt) : coef;
+                blk = wr ? block_ptr(coef, g, sg, bpm, cnt) : coef;
             }
             cnt++;
         }
@@ -281,18 +278,10 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
                                                                 TileState* __restrict__ ts, uint32_t* __restrict__ tile_ctr,
                                                                 int16_t* __restrict__ coef, uint64_t* __restrict__ stamps) {
     __shared__ HuffDev T[4];
-    __shared__ UTab ut;
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tabs);
         uint32_t* dst = reinterpret_cast<uint32_t*>(T);
         for (int i = threadIdx.x; i < (int)(sizeof(T) / 4); i += blockDim.x) dst[i] = src[i];
-        if (threadIdx.x < 10) {
-            const int u = threadIdx.x < g.bpm ? threadIdx.x : 0;
-            const int ci = g.ucomp[u];
-            ut.comp[threadIdx.x] = (uint8_t)ci;
-            ut.dc[threadIdx.x] = (uint8_t)g.comp[ci].dc;
-            ut.ac[threadIdx.x] = (uint8_t)g.comp[ci].ac;
-        }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -378,7 +367,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         if (go) {
             br.init(stream, sg.off, (uint32_t)(want >> 32), send);
             int uk = (int)(uint32_t)want;
-            run_symbols<false>(br, uk, mark, ce, T, ut, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, 0, g, sg, coef);
+            run_symbols<false>(br, uk, mark, ce, T, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, 0, g, sg, coef);
             st_in = pack_state(p_in, uk_in);
             st_out = pack_state(br.pos, uk);
         }
@@ -434,7 +423,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     int wcnt = ic - cnt, w0 = id0 - dc0, w1 = id1 - dc1, w2 = id2 - dc2;
     br.init(stream, sg.off, p_in, send);
     int wuk = uk_in;
-    run_symbols<true>(br, wuk, 0, ce, T, ut, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef);
+    run_symbols<true>(br, wuk, 0, ce, T, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef);
     JP_STAMP(4);
 #undef JP_STAMP
 }
