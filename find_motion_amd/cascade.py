@@ -14,8 +14,15 @@ HaarEvaluator::Feature::read (cascadedetect.cpp, 4.x):
 * node (left, right): > 0 internal node of the same tree, <= 0 leaf -idx;
   every tree has nodeCount + 1 leaves.
 
-The old `opencv-haar-classifier` format (one file in the reference,
-`licence_plate_rus_16stages`, not in CASCADE_LOOKUP) is not read.
+The old `opencv-haar-classifier` format (haartraining's `<stages>` of `<trees>`;
+one file in the reference, `licence_plate_rus_16stages`, commented out of
+CASCADE_LOOKUP) is read the way OpenCV's CascadeClassifier::convert rewrites it
+into the format above (cascadedetect_convert.cpp): one feature per tree node in
+node order, `left_node`/`right_node` kept as internal-node indices of the tree,
+`left_val`/`right_val` numbered as that tree's leaves 0, 1, ... in node order,
+`stage_threshold` then shifted by THRESHOLD_EPS as for a new file.  Only the plain
+stage chain (stage s has parent s - 1 and next -1) is a cascade of that format;
+stage trees are refused.  Detection then runs as for any converted cascade.
 """
 from __future__ import annotations
 
@@ -76,6 +83,10 @@ def parse(path_or_text: str) -> Cascade:
     else:
         root = ET.parse(path_or_text).getroot()
     c = root.find("cascade") if root.tag != "cascade" else root
+    if c is None:
+        old = next((e for e in ([root] + list(root)) if e.get("type_id") == "opencv-haar-classifier"), None)
+        if old is not None:
+            return _parse_old(old)
     if c is None or c.find("stageNum") is None:
         raise ValueError("not a new-format OpenCV cascade (<cascade> with <stageNum>)")
     ftype = (c.findtext("featureType") or "").strip()
@@ -128,6 +139,71 @@ def parse(path_or_text: str) -> Cascade:
                    np.asarray(ntrees, np.int32), np.asarray(sthr, np.float32), np.asarray(tnodes, np.int32),
                    np.asarray(left, np.int32), np.asarray(right, np.int32), np.asarray(feat, np.int32),
                    np.asarray(nthr, np.float32), np.asarray(leaves, np.float32), rects, wts, tilt)
+
+
+def _parse_old(c) -> Cascade:
+    """haartraining's format: <size>W H</size>, <stages> of {<trees> of trees (lists of nodes with
+    <feature>, <threshold>, <left_val>|<left_node>, <right_val>|<right_node>), <stage_threshold>,
+    <parent>, <next>}."""
+    size = _nums(c.findtext("size") or "")
+    if len(size) != 2:
+        raise ValueError("old-format cascade without <size>W H</size>")
+    win_w, win_h = int(size[0]), int(size[1])
+    ntrees, sthr, tnodes = [], [], []
+    left, right, feat, nthr, leaves = [], [], [], [], []
+    frects, fw, ftilt = [], [], []
+    stages = c.find("stages")
+    if stages is None:
+        raise ValueError("old-format cascade without <stages>")
+    for s, st in enumerate(stages.findall("_")):
+        if int(st.findtext("parent", str(s - 1))) != s - 1 or int(st.findtext("next", "-1")) != -1:
+            raise ValueError("stage trees (parent/next other than a chain) are not supported")
+        sthr.append(np.float32(np.float32(float(st.findtext("stage_threshold"))) - THRESHOLD_EPS))
+        trees = st.find("trees").findall("_")
+        ntrees.append(len(trees))
+        for tr in trees:
+            nodes = tr.findall("_")
+            nn = len(nodes)
+            if nn == 0:
+                raise ValueError("empty tree")
+            tnodes.append(nn)
+            nleaf = 0
+            for nd in nodes:
+                rs = nd.find("feature/rects").findall("_")
+                if not 1 <= len(rs) <= 3:
+                    raise ValueError("a HAAR feature has 1..3 rects")
+                r4 = np.zeros((3, 4), np.int32)
+                w3 = np.zeros(3, np.float32)
+                for j, r in enumerate(rs):
+                    v = _nums(r.text)
+                    r4[j] = [int(x) for x in v[:4]]
+                    w3[j] = np.float32(float(v[4]))
+                feat.append(len(frects))
+                frects.append(r4)
+                fw.append(w3)
+                ftilt.append(1 if int((nd.findtext("feature/tilted") or "0").strip()) != 0 else 0)
+                nthr.append(np.float32(float(nd.findtext("threshold"))))
+                for side, out in (("left", left), ("right", right)):
+                    child = nd.findtext(f"{side}_node")
+                    if child is not None:
+                        k = int(child)
+                        if not 0 < k < nn:
+                            raise ValueError(f"{side}_node {k} outside its tree")
+                        out.append(k)
+                    else:
+                        out.append(-nleaf)
+                        leaves.append(np.float32(float(nd.findtext(f"{side}_val"))))
+                        nleaf += 1
+            if nleaf != nn + 1:
+                raise ValueError("a tree needs nodeCount + 1 leaf values")
+    if not ntrees:
+        raise ValueError("cascade without stages")
+    return Cascade(win_w, win_h,
+                   np.asarray(ntrees, np.int32), np.asarray(sthr, np.float32), np.asarray(tnodes, np.int32),
+                   np.asarray(left, np.int32), np.asarray(right, np.int32), np.asarray(feat, np.int32),
+                   np.asarray(nthr, np.float32), np.asarray(leaves, np.float32),
+                   np.asarray(frects, np.int32).reshape(-1, 3, 4), np.asarray(fw, np.float32).reshape(-1, 3),
+                   np.asarray(ftilt, np.uint8))
 
 
 def to_xml(cs: Cascade) -> str:

@@ -52,3 +52,21 @@ def load_frontalface():
         k += n
     z["frames_detections_list"] = dets
     return cs, z
+
+
+def load_licence_plate_old():
+    """(Cascade, [(seed, candidates, detections)]) of tests/golden/cascade_licence_plate_old.npz
+    (make_golden_cascade_old.py)."""
+    from find_motion_amd.cascade import Cascade
+
+    z = dict(np.load(os.path.join(GOLDEN, "cascade_licence_plate_old.npz"), allow_pickle=False))
+    fields = ("stage_ntrees", "stage_threshold", "tree_nodes", "node_left", "node_right", "node_feature",
+              "node_threshold", "leaves", "feat_rects", "feat_weights", "feat_tilted")
+    cs = Cascade(int(z["win"][0]), int(z["win"][1]), *[z[f] for f in fields])
+    cases, kc, kd = [], 0, 0
+    for s, nc, nd in zip(z["seeds"], z["cand_counts"], z["det_counts"]):
+        cases.append((int(s), [tuple(int(v) for v in r) for r in z["candidates"][kc:kc + nc]],
+                      [tuple(int(v) for v in r) for r in z["detections"][kd:kd + nd]]))
+        kc += nc
+        kd += nd
+    return cs, cases

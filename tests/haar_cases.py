@@ -126,3 +126,29 @@ FACE_FRAMES_4K = [
 def face_frame_4k(i: int) -> np.ndarray:
     c = FACE_FRAMES_4K[i]
     return draw_faces(np.empty((2160, 3840, 3), np.uint8), c["faces"], seed=c["seed"])
+
+
+PLATE_SEEDS = [0, 9, 22, 36]
+
+
+def plate_image(seed: int, w: int = 300, h: int = 169) -> np.ndarray:
+    """A ROI-sized frame with three light, dark-framed rectangles holding dark bars (number-plate
+    like), for the reference's licence_plate_rus_16stages cascade (64x16 window)."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w, 3), int(rng.integers(60, 140)), np.uint8) + rng.integers(0, 10, (h, w, 3), dtype=np.uint8)
+    for _ in range(3):
+        pw = int(rng.integers(64, 160))
+        ph = max(16, pw * int(rng.integers(20, 30)) // 100)
+        x, y = int(rng.integers(0, w - pw)), int(rng.integers(0, h - ph))
+        img[y:y + ph, x:x + pw] = int(rng.integers(200, 250))
+        b = int(rng.integers(1, 4))
+        img[y:y + b, x:x + pw] = 20
+        img[y + ph - b:y + ph, x:x + pw] = 20
+        img[y:y + ph, x:x + b] = 20
+        img[y:y + ph, x + pw - b:x + pw] = 20
+        n = int(rng.integers(6, 10))
+        cw = pw // (n + 2)
+        for k in range(n):
+            cx = x + cw + k * cw + int(rng.integers(0, 2))
+            img[y + ph // 4:y + ph - ph // 4, cx:cx + max(1, cw * int(rng.integers(40, 70)) // 100)] = int(rng.integers(10, 50))
+    return img

@@ -190,6 +190,21 @@ def test_frontalface_on_4k_frames_resized_on_device():
     det.close()
 
 
+def test_old_format_licence_plate_cascade():
+    """The reference's one haartraining-format cascade (64x16 window, read as
+    CascadeClassifier::convert rewrites it): candidates and detections equal the fixture's."""
+    from golden_cases import load_licence_plate_old
+    from haar_cases import plate_image
+
+    cs, cases = load_licence_plate_old()
+    det = CascadeClassifier(cs)
+    for seed, cand, dets in cases:
+        got = det.detectMultiScale(plate_image(seed), scaleFactor=1.1, minNeighbors=5)
+        assert [tuple(r) for r in det.candidates().tolist()] == cand, seed
+        assert [tuple(r) for r in np.asarray(got).reshape(-1, 4).tolist()] == dets, seed
+    det.close()
+
+
 def test_config5_workload_streams_masks_and_faces(tmp_path):
     """configs[4] as one workload: 4 streams of 3840x2160 through StreamGroup with -B 3840 -b 183 (k 21),
     the MASK_SCHEMA polygons and the frontalface_default cascade on every 15th written frame

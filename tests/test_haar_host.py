@@ -24,7 +24,7 @@ REF_CASCADES = "/root/reference/find_motion/haarcascades"
 @pytest.mark.skipif(not os.path.isdir(REF_CASCADES), reason="reference cascades not present")
 def test_reference_cascades_parse():
     # every cascade the reference can load (CASCADE_LOOKUP, find_motion.py:104-122) reads into
-    # consistent arrays; the one old-format file is refused
+    # consistent arrays
     for name in CASCADE_LOOKUP:
         cs = parse(os.path.join(REF_CASCADES, f"haarcascade_{name}.xml"))
         assert cs.n_stages > 0 and cs.stage_ntrees.sum() == len(cs.tree_nodes)
@@ -35,8 +35,25 @@ def test_reference_cascades_parse():
     d = parse(os.path.join(REF_CASCADES, "haarcascade_frontalface_default.xml"))
     assert (d.win_w, d.win_h, d.n_stages) == (24, 24, 25)
     assert d.stage_threshold[0] == np.float32(np.float32(-5.0425500869750977) - THRESHOLD_EPS)
-    with pytest.raises(ValueError):
-        parse(os.path.join(REF_CASCADES, "haarcascade_licence_plate_rus_16stages.xml"))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CASCADES), reason="reference cascades not present")
+def test_reference_old_format_cascade():
+    # haarcascade_licence_plate_rus_16stages.xml (haartraining's format, commented out of
+    # CASCADE_LOOKUP): 64x16 window, 16 stages of stumps, values as CascadeClassifier::convert
+    # writes them; its first stage and first tree as the file states them
+    cs = parse(os.path.join(REF_CASCADES, "haarcascade_licence_plate_rus_16stages.xml"))
+    assert (cs.win_w, cs.win_h, cs.n_stages, len(cs.tree_nodes)) == (64, 16, 16, 91)
+    assert (cs.tree_nodes == 1).all() and len(cs.leaves) == 2 * 91 and not cs.has_tilted
+    assert (cs.node_left == 0).all() and (cs.node_right == -1).all()
+    assert list(cs.feat_rects[0, :2].ravel()) == [32, 2, 8, 6, 32, 4, 8, 2]
+    assert list(cs.feat_weights[0]) == [-1, 3, 0]
+    assert cs.node_threshold[0] == np.float32(1.6915600746870041e-002)
+    assert list(cs.leaves[:2]) == [np.float32(-9.5547717809677124e-001), np.float32(8.9129137992858887e-001)]
+    assert cs.stage_ntrees[0] == 4
+    assert cs.stage_threshold[-1] == np.float32(np.float32(-9.1314977407455444e-001) - THRESHOLD_EPS)
+    rc, msg = _create(cs)
+    assert rc in (_native.FM_OK, _native.FM_EHIP), msg
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_CASCADES), reason="reference cascades not present")
@@ -97,6 +114,74 @@ def test_xml_round_trip(kw):
     cs2 = parse(to_xml(cs))
     for f in cs.__dataclass_fields__:
         assert np.array_equal(getattr(cs, f), getattr(cs2, f)), f
+
+
+def test_old_format_fixture():
+    # the committed arrays are the reference file's (when it is here) and the restatement's
+    # candidates on the plate images are the fixture's
+    from golden_cases import load_licence_plate_old
+    from haar_cases import plate_image
+
+    cs, cases = load_licence_plate_old()
+    path = os.path.join(REF_CASCADES, "haarcascade_licence_plate_rus_16stages.xml")
+    if os.path.isfile(path):
+        ref = parse(path)
+        for f in cs.__dataclass_fields__:
+            assert np.array_equal(getattr(cs, f), getattr(ref, f)), f
+    for seed, cand, dets in cases[:2]:
+        got = haar.detect_candidates(cs, plate_image(seed), 1.1)
+        assert [tuple(r) for r in got] == cand and haar.group_rectangles(got, 5) == dets
+
+
+def _old_xml(cs):
+    """The same cascade in haartraining's format (nodes in tree order, leaves by value)."""
+    f9 = lambda x: format(float(x), ".9e")  # noqa: E731
+    out = ["<?xml version=\"1.0\"?>", "<opencv_storage>", "<c type_id=\"opencv-haar-classifier\">",
+           f"<size>{cs.win_w} {cs.win_h}</size>", "<stages>"]
+    ti = ni = li = 0
+    for s in range(cs.n_stages):
+        out.append("<_><trees>")
+        for _ in range(cs.stage_ntrees[s]):
+            nn = int(cs.tree_nodes[ti])
+            out.append("<_>")
+            for k in range(nn):
+                fi = cs.node_feature[ni + k]
+                rs = "".join(f"<_>{' '.join(str(int(v)) for v in cs.feat_rects[fi, j])} {f9(cs.feat_weights[fi, j])}</_>"
+                             for j in range(3) if cs.feat_weights[fi, j] != 0 or j == 0)
+                kids = ""
+                for side, v in (("left", cs.node_left[ni + k]), ("right", cs.node_right[ni + k])):
+                    kids += f"<{side}_node>{v}</{side}_node>" if v > 0 else f"<{side}_val>{f9(cs.leaves[li - v])}</{side}_val>"
+                out.append(f"<_><feature><rects>{rs}</rects><tilted>{int(cs.feat_tilted[fi])}</tilted></feature>"
+                           f"<threshold>{f9(cs.node_threshold[ni + k])}</threshold>{kids}</_>")
+            out.append("</_>")
+            ti += 1
+            ni += nn
+            li += nn + 1
+        from find_motion_amd.cascade import _unshift
+        out.append(f"</trees><stage_threshold>{f9(_unshift(cs.stage_threshold[s]))}</stage_threshold>"
+                   f"<parent>{s - 1}</parent><next>-1</next></_>")
+    out += ["</stages>", "</c>", "</opencv_storage>"]
+    return "\n".join(out)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(depth=2), dict(tilted=True, depth=2)])
+def test_old_format_reads_as_the_same_cascade(kw):
+    # one feature per node and leaves renumbered in node order, so compare what the cascade does:
+    # the same detections on the same image, and the same stage structure and thresholds
+    cs = make_cascade(7, **kw)
+    old = parse(_old_xml(cs))
+    for f in ("win_w", "win_h", "stage_ntrees", "stage_threshold", "tree_nodes", "node_threshold"):
+        assert np.array_equal(getattr(cs, f), getattr(old, f)), f
+    assert len(old.feat_tilted) == len(old.node_left) and len(old.leaves) == len(cs.leaves)
+    img = make_image(3)
+    assert haar.detect_candidates(cs, img) == haar.detect_candidates(old, img)
+    assert len(haar.detect_candidates(cs, img)) > 0
+
+
+def test_old_format_refuses_stage_trees():
+    xml = _old_xml(make_cascade(1)).replace("<parent>1</parent>", "<parent>0</parent>")
+    with pytest.raises(ValueError):
+        parse(xml)
 
 
 def test_linear_exact_known_answers():
