@@ -138,7 +138,7 @@ def mjpeg_fed(eng, host: np.ndarray, T: int, S: int, quality: int = 75) -> dict 
         kms.append(dec.last_ms())
     dec.close()
     del dst
-    n = max(8 * T, 512)
+    n = max(32 * T, 2048)  # long enough that the feeder's fill and drain (about two batches) stay small
     for _ in BatchFeeder(eng, [videoio.JpegListCapture(enc[:2]) for _ in range(S)], T):  # warm-up
         pass
     torch.cuda.synchronize()
