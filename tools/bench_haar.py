@@ -10,7 +10,9 @@ rejection profile resembles, but is not, a trained cascade's: the line reports w
 rate next to frames/s.  A CPU figure comes from oracle/haar.py on a few frames
 (numpy restatement, not OpenCV).
 
-Usage: python tools/bench_haar.py [--frames 64] [--iters 20] [--cpu-frames 1]
+Usage: python tools/bench_haar.py [--frames 64] [--iters 20] [--cpu-frames 1] [--frontalface]
+
+--frontalface runs the reference's own cascade (config 5) from its committed fixture arrays.
 """
 import argparse
 import json
@@ -112,12 +114,18 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu-frames", type=int, default=1)
     ap.add_argument("--cascade", default=None, help="a real haarcascade_*.xml instead of the synthetic one")
+    ap.add_argument("--frontalface", action="store_true",
+                    help="the reference's haarcascade_frontalface_default (parsed arrays in tests/golden)")
     args = ap.parse_args()
     from find_motion_amd import CascadeClassifier
     from haar_cases import make_image
 
     from haar_cases import make_image as _mi
-    if args.cascade:
+    if args.frontalface:
+        from golden_cases import load_frontalface
+        cs = load_frontalface()[0]
+        args.cascade = "haarcascade_frontalface_default (tests/golden/cascade_frontalface_default.npz)"
+    elif args.cascade:
         from find_motion_amd.cascade import parse
         cs = parse(args.cascade)
     else:
