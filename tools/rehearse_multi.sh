@@ -1,0 +1,14 @@
+#!/bin/bash
+# N>1 rehearsal on the box's one GPU (every rank pinned to device 0 over gloo; RCCL refuses two
+# ranks on one device): bench.py's own rank spawning at --gpus 2 and 4, and the driver's
+# torch.distributed.run form at 2 ranks.  Checks that rank 0 prints one line with n_gpus = N.
+set -o pipefail
+mkdir -p gpurun_out
+export FM_BENCH_DEVICE=0 FM_BENCH_BACKEND=gloo
+check() { grep '^{' "$1" | python -c "import json,sys; L=sys.stdin.read().splitlines(); assert len(L)==1, L; d=json.loads(L[0]); assert d['n_gpus']==$2, d['n_gpus']; print('$1', 'n_gpus', d['n_gpus'], 'value', d['value'], 'ms/step', d['ms_per_step'])"; }
+timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 2 --no-host-fed --no-mjpeg > gpurun_out/n2_spawn.log 2>&1 || { tail -20 gpurun_out/n2_spawn.log; exit 1; }
+check gpurun_out/n2_spawn.log 2 || exit 1
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --no-host-fed --no-mjpeg > gpurun_out/n2_torchrun.log 2>&1 || { tail -20 gpurun_out/n2_torchrun.log; exit 1; }
+check gpurun_out/n2_torchrun.log 2 || exit 1
+timeout -k 10 300 python bench.py --gpus 4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-fed --no-mjpeg > gpurun_out/n4_spawn.log 2>&1 || { tail -20 gpurun_out/n4_spawn.log; exit 1; }
+check gpurun_out/n4_spawn.log 4 || exit 1
