@@ -426,15 +426,25 @@ class CascadeClassifier:
 
     def detect_frames(self, frames: np.ndarray, roi_w: int = 300, scaleFactor=1.1, minNeighbors=5, cap: int = 256):
         """find_objects on raw BGR frames [n, H, W, 3]: INTER_AREA to width roi_w on the device, then
-        detectMultiScale; rects are in ROI coordinates (as find_motion.py:724-729 stores them)."""
+        detectMultiScale; rects are in ROI coordinates (as find_motion.py:724-729 stores them).
+        `frames` is a host array, or a contiguous uint8 torch tensor already on the detector's GPU
+        (frames resident in HBM: no host round trip; torch's current stream is synchronised first)."""
         L = load()
-        fr = np.ascontiguousarray(frames, np.uint8)
-        n, H, W = fr.shape[:3]
+        if getattr(frames, "is_cuda", False):
+            import torch
+            if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3 or not frames.is_contiguous():
+                raise ValueError("device frames must be a contiguous uint8 tensor [n, H, W, 3]")
+            torch.cuda.current_stream(frames.device).synchronize()
+            fr, ptr, on_dev = frames, C.c_void_p(frames.data_ptr()), 1
+        else:
+            fr = np.ascontiguousarray(frames, np.uint8)
+            ptr, on_dev = _ptr(fr), 0
+        n, H, W = (int(v) for v in fr.shape[:3])
         rh = C.c_int32()
         while True:
             rects = np.zeros((n, cap, 4), np.int32)
             counts = np.zeros(n, np.int32)
-            rc = L.fm_haar_detect_frames(self._h, _ptr(fr), n, H, W, 0, int(roi_w), float(scaleFactor),
+            rc = L.fm_haar_detect_frames(self._h, ptr, n, H, W, on_dev, int(roi_w), float(scaleFactor),
                                          int(minNeighbors), _ptr(rects), cap, _ptr(counts), C.byref(rh))
             if rc != FM_OK:
                 raise FMError(rc, f"fm_haar_detect_frames: {L.fm_haar_last_error(self._h).decode()}")

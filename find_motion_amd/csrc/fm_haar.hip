@@ -25,12 +25,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/find_motion_amd.h"
@@ -38,6 +40,8 @@
 
 namespace fm {
 namespace haar {
+
+constexpr int kPostThreads = 16;  // host threads for a batch's per-image post-pass (the GPU box's CPU share)
 
 constexpr int MAXSC = 64;  // scales per call (1.1^64 > 400: far beyond any frame)
 
@@ -642,9 +646,10 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
     HH(h, hipEventElapsedTime(&ms, h->e0, h->e1));
     h->last_ms = ms;
 
-    // per image: the row scan with the stage-0 skip, then groupRectangles (eps 0.2)
+    // per image: the row scan with the stage-0 skip, then groupRectangles (eps 0.2); images are
+    // independent (each writes only its own counts / rects), so a batch spreads them over threads
     const double eps = 0.2;
-    for (int img = 0; img < n; ++img) {
+    auto post = [&](int img) {
         std::vector<int32_t> c;
         const int8_t* R = h->h_res.data() + (size_t)img * g.NW;
         for (int s = 0; s < g.n; ++s) {
@@ -735,6 +740,19 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         counts[img] = no;
         const int keep = std::min(no, cap);
         if (keep > 0) std::memcpy(rects + (size_t)img * cap * 4, outr.data(), sizeof(int32_t) * 4 * keep);
+    };
+    // (64 1080p ROI frames of frontalface: 12.1 ms per call single-threaded beside 3.1 ms of kernels)
+    const int nth = std::min(n, std::max(1, std::min(kPostThreads, (int)std::thread::hardware_concurrency())));
+    if (nth <= 1) {
+        for (int img = 0; img < n; ++img) post(img);
+    } else {
+        std::atomic<int> next{0};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nth; ++t)
+            pool.emplace_back([&] {
+                for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) post(i);
+            });
+        for (auto& t : pool) t.join();
     }
     return FM_OK;
 }

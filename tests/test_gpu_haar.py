@@ -96,6 +96,24 @@ def test_detect_frames_resizes_on_device(W, H):
     det.close()
 
 
+def test_detect_frames_device_input():
+    # frames already resident in HBM (on_device = 1: no H2D copy) give the host path's and the
+    # restatement's detections
+    import torch
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    raws = np.stack([_raw_frame(s, 640, 360) for s in range(3)])
+    det = CascadeClassifier(cs)
+    dev = torch.from_numpy(raws).to("cuda:0")
+    got = det.detect_frames(dev, 300, 1.1, 3)
+    host = det.detect_frames(raws, 300, 1.1, 3)
+    for i in range(len(raws)):
+        ref = haar.detect_multiscale(cs, oracle.resize_area_bgr(raws[i], 300), 1.1, 3)
+        assert [tuple(r) for r in got[i].tolist()] == ref, i
+        assert [tuple(r) for r in host[i].tolist()] == ref, i
+    with pytest.raises(ValueError):
+        det.detect_frames(dev[:, :, ::2], 300)  # not contiguous
+    det.close()
+
 def test_video_motion_find_objects(tmp_path):
     # the drop-in loads haarcascade_<name>.xml from cascade_dir and runs find_objects every 15th frame
     from types import SimpleNamespace
