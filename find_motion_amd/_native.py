@@ -30,7 +30,7 @@ EXPORTED = (
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
-    "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune",
+    "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device",
 )
 
 
@@ -126,6 +126,7 @@ def load() -> C.CDLL:
     L.fm_mjpeg_last_ms.restype = C.c_double
     L.fm_submit_jpeg.argtypes = [vp, vp, vp, vp, i32]
     L.fm_read_frame.argtypes = [vp, i32, i32, vp]
+    L.fm_frame_device.argtypes = [vp, i32, i32, C.POINTER(C.c_void_p)]
     L.fm_mjpeg_tune.argtypes = [vp, i32, i32]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
@@ -357,6 +358,13 @@ class MotionEngine:
         self._check(self._L.fm_read_frame(self._h, frame, stream, _ptr(out)))
         return out
 
+    def frame_device_ptr(self, frame: int, stream: int) -> int:
+        """Device address of the source frame (BGR [H][W][3]) of (frame, stream) of the last waited
+        batch, left in HBM (valid until the next wait)."""
+        p = C.c_void_p()
+        self._check(self._L.fm_frame_device(self._h, frame, stream, C.byref(p)))
+        return int(p.value)
+
     def plane(self, which: int, frame: int, stream: int) -> np.ndarray:
         out = np.empty(self.work_shape, np.uint8)
         self._check(self._L.fm_read_plane(self._h, which, frame, stream, _ptr(out)))
@@ -427,9 +435,14 @@ class CascadeClassifier:
     def detect_frames(self, frames: np.ndarray, roi_w: int = 300, scaleFactor=1.1, minNeighbors=5, cap: int = 256):
         """find_objects on raw BGR frames [n, H, W, 3]: INTER_AREA to width roi_w on the device, then
         detectMultiScale; rects are in ROI coordinates (as find_motion.py:724-729 stores them).
-        `frames` is a host array, or a contiguous uint8 torch tensor already on the detector's GPU
-        (frames resident in HBM: no host round trip; torch's current stream is synchronised first)."""
+        `frames` is a host array, a contiguous uint8 torch tensor already on the detector's GPU
+        (frames resident in HBM: no host round trip; torch's current stream is synchronised first),
+        or a tuple (device address, n, H, W) of frames the engine left in HBM (fm_frame_device)."""
         L = load()
+        if isinstance(frames, tuple):  # (device address, n, H, W): frames left in HBM by the engine
+            ptr, n, H, W = frames
+            return self._detect_frames(L, C.c_void_p(ptr), int(n), int(H), int(W), 1, roi_w, scaleFactor,
+                                       minNeighbors, cap)
         if getattr(frames, "is_cuda", False):
             import torch
             if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3 or not frames.is_contiguous():
@@ -440,6 +453,9 @@ class CascadeClassifier:
             fr = np.ascontiguousarray(frames, np.uint8)
             ptr, on_dev = _ptr(fr), 0
         n, H, W = (int(v) for v in fr.shape[:3])
+        return self._detect_frames(L, ptr, n, H, W, on_dev, roi_w, scaleFactor, minNeighbors, cap)
+
+    def _detect_frames(self, L, ptr, n, H, W, on_dev, roi_w, scaleFactor, minNeighbors, cap):
         rh = C.c_int32()
         while True:
             rects = np.zeros((n, cap, 4), np.int32)

@@ -1092,6 +1092,15 @@ int fm_read_frame(fm_ctx* c, int frame, int stream, uint8_t* out) {
     return FM_OK;
 }
 
+int fm_frame_device(fm_ctx* c, int frame, int stream, const uint8_t** out) {
+    if (!c || !out) return fail(c, FM_EINVAL, "null argument");
+    if (int rc = check_frame(c, frame, stream, true)) return rc;
+    const BatchSlot& B = c->slots[c->ready_slot];
+    if (!B.src) return fail(c, FM_ESTATE, "no source frames for the last waited batch");
+    *out = B.src + ((size_t)frame * c->p.n_streams + stream) * c->src_frame_bytes;
+    return FM_OK;
+}
+
 int fm_read_background(fm_ctx* c, int stream, double* out) {
     if (!c || !out) return fail(c, FM_EINVAL, "null argument");
     if (int rc = check_idle(c)) return rc;

@@ -561,8 +561,18 @@ class VideoMotion:
         if self.cascades:
             # frame.resized = imutils.resize(frame.raw, width=width) happens on the device inside
             # detect_frames (INTER_AREA); rects are in ROI coordinates as in the reference
+            lazy = getattr(frame, "_raw", True) is None and getattr(frame, "_load", None) is not None
+            src = None if lazy else frame.raw[None]
+            b = getattr(frame, "_bound", None)
+            if src is None and b is not None and b.engine.generation == b.gen:
+                # an MJPEG frame decoded on the GPU, its batch still current: the cascade reads it
+                # where the decoder left it (fm_frame_device), no round trip through host memory
+                H, W = b.engine.src_shape[:2]
+                src = (b.engine.frame_device_ptr(b.t, b.s), 1, H, W)
+            elif src is None:
+                src = frame.raw[None]
             for title, cascade in self.cascades.items():
-                found = cascade.detect_frames(frame.raw[None], width, scaleFactor, minNeighbours)[0]
+                found = cascade.detect_frames(src, width, scaleFactor, minNeighbours)[0]
                 for rect in found:
                     self.last_objects.setdefault(title, []).append(VideoMotion.make_area_from_rect(tuple(int(v) for v in rect)))
         return set(self.last_objects.keys())

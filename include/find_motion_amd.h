@@ -261,6 +261,10 @@ int fm_mjpeg_tune(fm_mjpeg* dec, int chunk_bits, int spec_bits);
  * fm_submit_jpeg only for the frames it writes (fm.py:535-546) or shows.  Valid until the next
  * fm_wait; for fm_submit(on_device = 1) the caller's buffer must still hold the frames. */
 int fm_read_frame(fm_ctx* ctx, int frame, int stream, uint8_t* out);
+/* The device address of that same source frame, left in HBM: what find_objects (fm.py:703-731)
+ * hands to fm_haar_detect_frames(on_device = 1) so an MJPEG frame decoded on the GPU reaches the
+ * cascade without a round trip through host memory.  Valid until the next fm_wait. */
+int fm_frame_device(fm_ctx* ctx, int frame, int stream, const uint8_t** out);
 
 #ifdef __cplusplus
 }

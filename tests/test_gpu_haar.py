@@ -257,3 +257,31 @@ def test_config5_workload_streams_masks_and_faces(tmp_path):
         fifteenth = order[s][cur[14]] if len(cur) >= 15 else None
         seen = {"Face 4"} if fifteenth is not None and z["frames_detections_list"][fifteenth] else set()
         assert set(res[s][3]) == seen, (s, fifteenth)
+
+
+def test_cascade_on_engine_frames_left_in_hbm():
+    # find_objects on an MJPEG frame the engine decoded on the GPU (fm_frame_device): the cascade
+    # reads the engine's input slot directly and finds what the host round trip and the oracle find
+    from find_motion_amd import MJpegDecoder, MotionEngine
+    from jpeg_cases import encode
+
+    W, H, T, S = 640, 360, 3, 2
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    det = CascadeClassifier(cs)
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    dec = MJpegDecoder(W, H, max_frames=T * S)
+    jp = [encode(_raw_frame(7 * t + s, W, H), quality=90) for t in range(T) for s in range(S)]
+    eng.submit_jpeg(dec, jp)
+    eng.wait()
+    for t in range(T):
+        for s in range(S):
+            got = det.detect_frames((eng.frame_device_ptr(t, s), 1, H, W), 300, 1.1, 3)[0]
+            raw = eng.read_frame(t, s)
+            host = det.detect_frames(raw[None], 300, 1.1, 3)[0]
+            ref = haar.detect_multiscale(cs, oracle.resize_area_bgr(raw, 300), 1.1, 3)
+            assert [tuple(r) for r in got.tolist()] == ref, (t, s)
+            assert [tuple(r) for r in host.tolist()] == ref, (t, s)
+    with pytest.raises(Exception):
+        eng.frame_device_ptr(T, 0)  # past the batch
+    eng.close()
+    det.close()

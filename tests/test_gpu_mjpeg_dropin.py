@@ -144,3 +144,29 @@ def test_stream_group_mixed_chroma_sampling(tmp_path):
     grp.find_motion()
     for s, v in enumerate(grp.videos):
         assert v.written_indices == _oracle_written(jps[s], W, H, 320), s
+
+
+def test_find_objects_reads_gpu_decoded_frames_in_place(tmp_path):
+    """find_objects (fm.py:703-731) on an MJPEG frame whose batch is current: the cascade reads the
+    decoded frame in the engine's input slot (fm_frame_device), raw is never fetched to the host,
+    and the detections equal the oracle's on the libjpeg-turbo-decoded frame."""
+    from find_motion_amd.cascade import to_xml
+    from haar_cases import make_cascade
+    from oracle import haar
+
+    W, H, n = 640, 360, 16
+    src = tmp_path / "v.avi"
+    jp = _mjpeg_avi(src, W, H, n, 2, quality=90)
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    (tmp_path / "haarcascade_frontalface_default.xml").write_text(to_xml(cs))
+    vm = motion.VideoMotion(filename=str(src), box_size=100, threshold=12, batch=8, outdir=str(tmp_path),
+                            cascades=["frontalface_default"], cascade_dir=str(tmp_path))
+    title = next(iter(vm.cascades))
+    for i in range(15):
+        assert vm.read()
+        seen = vm.find_objects(minNeighbours=2)
+    fr = vm.current_frame
+    assert fr.index == 14 and fr._raw is None  # the 15th frame: detected in place, not fetched
+    ref = haar.detect_multiscale(cs, oracle.resize_area_bgr(reference_decode(jp[14]), 300), 1.1, 2)
+    assert seen == ({title} if ref else set())
+    assert vm.last_objects.get(title, []) == [((x, y), (x + w, y + h)) for x, y, w, h in ref]
