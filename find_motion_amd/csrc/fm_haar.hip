@@ -622,7 +622,10 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         #ifdef FM_DEV_SWITCHES  // A/B switch of the dev build only (make VARIANT=dev)
         static const int split_env = std::getenv("FM_HAAR_SPLIT") ? std::atoi(std::getenv("FM_HAAR_SPLIT")) : 4;
 #else
-        static const int split_env = 4;
+#ifndef FM_HAAR_SPLIT_DEFAULT
+#define FM_HAAR_SPLIT_DEFAULT 4
+#endif
+        static const int split_env = FM_HAAR_SPLIT_DEFAULT;
 #endif
         const int split = std::max(1, std::min(split_env, h->n_stages));
         if ((rc = grow(h, &h->d_live, h->cap_live, (size_t)nw))) return rc;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Head-stage count (stages run on every window before survivors are compacted) A/B on the reference's
+# frontalface cascade: abvar/sp<k>/libfm_hip.so built with -DFM_HAAR_SPLIT_DEFAULT=k, alternating 2 rounds.
+set -o pipefail
+mkdir -p gpurun_out
+for r in 1 2; do
+  for k in "$@"; do
+    FM_HIP_LIB=$PWD/abvar/sp$k/libfm_hip.so timeout -k 10 120 python tools/bench_haar.py --frontalface --frames 64 --iters 10 --cpu-frames 0 > gpurun_out/hsp_$k.log 2>&1 || { tail -3 gpurun_out/hsp_$k.log; exit 1; }
+    echo "split $k round $r $(grep '^{' gpurun_out/hsp_$k.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["device_ms_per_call"], d["resident_frames_per_s"])')"
+  done
+done
