@@ -30,7 +30,8 @@ EXPORTED = (
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
-    "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device",
+    "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device", "fm_mjpeg_geometry",
+    "fm_submit_streams",
 )
 
 
@@ -128,6 +129,8 @@ def load() -> C.CDLL:
     L.fm_read_frame.argtypes = [vp, i32, i32, vp]
     L.fm_frame_device.argtypes = [vp, i32, i32, C.POINTER(C.c_void_p)]
     L.fm_mjpeg_tune.argtypes = [vp, i32, i32]
+    L.fm_mjpeg_geometry.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    L.fm_submit_streams.argtypes = [vp, vp, i32, i32]
     for name in EXPORTED:
         if name not in ("fm_destroy", "fm_last_error", "fm_abi_version", "fm_haar_destroy", "fm_haar_last_error",
                         "fm_haar_last_ms", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_last_ms"):
@@ -289,6 +292,35 @@ class MotionEngine:
             raise ValueError(f"frames shape {f.shape} != [n][{self.n_streams}]{self.src_shape}")
         self._check(self._L.fm_submit(self._h, _ptr(f), f.shape[0], 0))
         self._inflight.append((f.shape[0], f))
+
+    def submit_streams(self, frames, on_device: bool = False, n_frames: int | None = None) -> None:
+        """One buffer per stream (fm_submit_streams): frames[s] = stream s's frames [n][H][W][3] -- host
+        arrays, or device addresses (ints) with on_device and n_frames.  Same results as submit() of the
+        frames gathered into [n][n_streams] order, without the host-side gather."""
+        if len(frames) != self.n_streams:
+            raise ValueError(f"{len(frames)} stream buffers for {self.n_streams} streams")
+        if on_device:
+            if n_frames is None:
+                raise ValueError("n_frames is required for device buffers")
+            ptrs = np.array([int(p) for p in frames], np.uint64)
+            self._check(self._L.fm_submit_streams(self._h, _ptr(ptrs), int(n_frames), 1))
+            self._inflight.append((int(n_frames), None))
+            return
+        arrs = []
+        for f in frames:
+            a = np.asarray(f)
+            if a.dtype != np.uint8 or not a.flags.c_contiguous:
+                a = np.ascontiguousarray(a, dtype=np.uint8)
+            if a.ndim == 3:
+                a = a[None]
+            if a.shape[1:] != self.src_shape:
+                raise ValueError(f"stream buffer shape {a.shape} != [n]{self.src_shape}")
+            if arrs and a.shape[0] != arrs[0].shape[0]:
+                raise ValueError("every stream buffer must hold the same number of frames")
+            arrs.append(a)
+        ptrs = np.array([a.ctypes.data for a in arrs], np.uint64)
+        self._check(self._L.fm_submit_streams(self._h, _ptr(ptrs), arrs[0].shape[0], 0))
+        self._inflight.append((arrs[0].shape[0], arrs))
 
     def submit_device(self, ptr: int, n_frames: int) -> None:
         """Frames already in device memory (e.g. a torch CUDA tensor's data_ptr()).

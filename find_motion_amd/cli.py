@@ -1,7 +1,7 @@
 """Command line with the reference's flag surface (fm.py:1448-1489) plus GPU placement.
 
     python -m find_motion_amd [files] -i DIR -o DIR -c cfg.ini -B 100 -b 20 -t 12 -a 0.1 ...
-                              [--gpus N] [--device D] [--batch T] [--group]
+                              [--gpus N] [--device D] [--batch T] [--group] [--gpu-decode]
 
 Everything the reference's `run` does around the hot path is kept in its
 shape (INI overriding the CLI, masks from literals and a JSON file, mtime
@@ -76,6 +76,8 @@ def get_args(parser: ArgumentParser) -> None:
     parser.add_argument("--batch", type=int, default=8, help="Frames per stream decoded ahead per kernel launch")
     parser.add_argument("--group", action="store_true",
                         help="Batch same-sized videos of a GPU's shard into one launch (StreamGroup)")
+    parser.add_argument("--gpu-decode", action="store_true", default=None,
+                        help="Decode MJPEG AVIs on the GPU (libjpeg-turbo-exact) even when OpenCV is present")
 
 
 def process_config(config_file: str, args: Namespace) -> Namespace:
@@ -89,7 +91,8 @@ def process_config(config_file: str, args: Namespace) -> Namespace:
             use_value = int(value)
         if setting in ("mintime", "cachetime", "avg"):
             use_value = float(value)
-        if setting in ("mem", "progress", "debug", "show", "ignore_progress", "ignore_drive", "yolo_tiny", "group"):
+        if setting in ("mem", "progress", "debug", "show", "ignore_progress", "ignore_drive", "yolo_tiny", "group",
+                       "gpu_decode"):
             if value not in ("True", "False"):
                 raise ValueError("{} must be True or False".format(setting))
             use_value = value == "True"
@@ -201,7 +204,7 @@ def _job_kwargs(args) -> dict:
                 blur_scale=args.blur_scale, box_size=args.box_size, min_box_scale=args.min_box_scale,
                 threshold=args.threshold, avg=args.avg, fps=args.fps, min_time=args.mintime,
                 cache_time=args.cachetime, multiprocess=args.processes > 1, cascades=args.cascade_object,
-                yolo_tiny=args.yolo_tiny)
+                yolo_tiny=args.yolo_tiny, gpu_decode=getattr(args, "gpu_decode", None))
 
 
 def run_shard(files: list, kwargs: dict, device: int, batch: int, group: bool) -> list:

@@ -96,8 +96,9 @@ struct fm_ctx {
     int32_t* d_label = nullptr;   // pixel-level CCL (v1 path, fused-path overflow fallback)
     int32_t* d_cid = nullptr;
     uint8_t* d_outer = nullptr;
-    int32_t* d_rec_dev = nullptr;  // pixel-level CCL records [rec_dev_cap][5]
-    size_t rec_dev_cap = 0;
+    int32_t* d_rec_dev = nullptr;  // per-frame path: the batch's pixel-level CCL records [frames][max_contours][5]
+    int32_t* d_rec_one = nullptr;  // relabel_frame: one frame's records [rec_one_cap][5] (grown on demand)
+    size_t rec_one_cap = 0;
     int32_t* d_area = nullptr;     // FM_FLAG_CONTOUR_AREA: jobs [area_cap][3] + areas [area_cap]
     size_t area_cap = 0;
     int32_t* d_rec_all = nullptr;  // k_emit_all records of one frame [rec_all_cap][5] + counter
@@ -296,22 +297,24 @@ int relabel_frame(fm_ctx* c, BatchSlot& B, size_t f, std::vector<int32_t>& out, 
     for (int pass = 0; pass < 2; pass++) {
         HIP_TRY(c, hipMemsetAsync(dcnt, 0, sizeof(int32_t), st));
         HIP_TRY(c, hipMemsetAsync(c->d_outer, 0, c->work_plane, st));
-        CclArgs ca{mask, c->d_label, c->d_outer, c->d_cid, dcnt, c->d_rec_dev, 1, c->h, c->w, (int)c->rec_dev_cap};
+        // its own record buffer: the per-frame path's d_rec_dev holds [frames][max_contours] records
+        // for every submit and must keep that size
+        CclArgs ca{mask, c->d_label, c->d_outer, c->d_cid, dcnt, c->d_rec_one, 1, c->h, c->w, (int)c->rec_one_cap};
         HIP_TRY(c, launch_ccl(st, ca, nullptr));
         int32_t n = 0;
         HIP_TRY(c, hipMemcpyAsync(&n, dcnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
-        if ((size_t)n <= c->rec_dev_cap) {
+        if ((size_t)n <= c->rec_one_cap) {
             count = n;
             out.resize((size_t)n * 5);
-            HIP_TRY(c, hipMemcpyAsync(out.data(), c->d_rec_dev, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipMemcpyAsync(out.data(), c->d_rec_one, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
             HIP_TRY(c, hipStreamSynchronize(st));
             return FM_OK;
         }
-        dfree(c->d_rec_dev);
-        c->rec_dev_cap = 0;
-        if (int rc = dalloc(c, &c->d_rec_dev, (size_t)n * 5)) return rc;
-        c->rec_dev_cap = (size_t)n;
+        dfree(c->d_rec_one);
+        c->rec_one_cap = 0;
+        if (int rc = dalloc(c, &c->d_rec_one, (size_t)n * 5)) return rc;
+        c->rec_one_cap = (size_t)n;
     }
     return fail(c, FM_EHIP, "pixel-level relabel of frame %zu did not converge", f);
 }
@@ -573,9 +576,10 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
     if ((rc = dalloc(cp, &c->d_label, ccl_px)) || (rc = dalloc(cp, &c->d_cid, ccl_px)) ||
         (rc = dalloc(cp, &c->d_outer, ccl_px)) ||
-        (rc = dalloc(cp, &c->d_rec_dev, (c->use_fused ? 1 : frames) * (size_t)p.max_contours * 5)))
+        (!c->use_fused && (rc = dalloc(cp, &c->d_rec_dev, frames * (size_t)p.max_contours * 5))) ||
+        (rc = dalloc(cp, &c->d_rec_one, (size_t)p.max_contours * 5)))
         return rc;
-    c->rec_dev_cap = (size_t)p.max_contours;
+    c->rec_one_cap = (size_t)p.max_contours;
     HIP_TRY(cp, hipHostMalloc((void**)&c->h_err, sizeof(int32_t), hipHostMallocMapped));
     HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->dh_err, c->h_err, 0));
     *c->h_err = 0;
@@ -655,7 +659,7 @@ void fm_destroy(fm_ctx* c) {
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
-    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_all); dfree(c->d_area);
+    dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_one); dfree(c->d_rec_all); dfree(c->d_area);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
     for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
         if (st) (void)hipStreamDestroy(st);
@@ -720,11 +724,19 @@ int fm_set_hip_stream(fm_ctx* c, void* s) {
 // fm_submit / fm_submit_jpeg: frames from host memory (copied), device memory, or JPEGs decoded
 // on the input stream into the batch's device buffer (dec != nullptr)
 static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, fm_mjpeg* dec,
-                       const uint8_t* const* jpegs, const size_t* sizes) {
+                       const uint8_t* const* jpegs, const size_t* sizes, const uint8_t* const* per_stream = nullptr) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
     if ((int)c->inflight.size() >= c->nslots)
         return fail(c, FM_ESTATE, "%d batch(es) already in flight: call fm_wait first", (int)c->inflight.size());
-    if ((!frames && !dec) || n < 1 || n > c->p.max_batch)
+    if (per_stream) {
+        for (int s = 0; s < c->p.n_streams; s++)
+            if (!per_stream[s]) return fail(c, FM_EINVAL, "null frames for stream %d", s);
+        if (on_device && c->p.n_streams == 1) {  // one stream: [n][1] is the contiguous layout, read in place
+            frames = per_stream[0];
+            per_stream = nullptr;
+        }
+    }
+    if ((!frames && !dec && !per_stream) || n < 1 || n > c->p.max_batch)
         return fail(c, FM_EINVAL, "n_frames %d outside [1, max_batch=%d] or null frames", n, c->p.max_batch);
     HIP_TRY(c, hipSetDevice(c->p.device));
     const int si = c->next_slot;
@@ -742,10 +754,22 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
             int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
             if (rc) return rc;
         }
-        if (int rc = fm_mjpeg_enqueue(dec, jpegs, sizes, (int)F, B.d_in, rs))
-            return fail(c, rc, "JPEG decode: %s", fm_mjpeg_last_error(dec));
+        const int rc = fm_mjpeg_enqueue(dec, jpegs, sizes, (int)F, B.d_in, rs);
+        HIP_TRY(c, hipSetDevice(c->p.device));
+        if (rc) return fail(c, rc, "JPEG decode: %s", fm_mjpeg_last_error(dec));
         src = B.d_in;
         on_device = 0;  // (the input stream ran: the pixel stream waits for it below)
+    } else if (per_stream) {  // stream s's frames -> rows s, S + s, 2S + s, ... of the [t][s] batch layout
+        if (!B.d_in) {
+            int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
+            if (rc) return rc;
+        }
+        const size_t fb = c->src_frame_bytes;
+        for (int s = 0; s < S; s++)
+            HIP_TRY(c, hipMemcpy2DAsync(B.d_in + (size_t)s * fb, (size_t)S * fb, per_stream[s], fb, fb, (size_t)n,
+                                        on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, rs));
+        src = B.d_in;
+        on_device = 0;
     } else if (!on_device) {
         if (!B.d_in) {
             int rc = dalloc(c, &B.d_in, (size_t)c->p.max_batch * S * c->src_frame_bytes);
@@ -921,9 +945,25 @@ int fm_submit(fm_ctx* c, const uint8_t* frames, int n, int on_device) {
     return submit_impl(c, frames, n, on_device, nullptr, nullptr, nullptr);
 }
 
+int fm_submit_streams(fm_ctx* c, const uint8_t* const* bgr, int n, int on_device) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (!bgr) return fail(c, FM_EINVAL, "null stream pointer array");
+    return submit_impl(c, nullptr, n, on_device, nullptr, nullptr, nullptr, bgr);
+}
+
 int fm_submit_jpeg(fm_ctx* c, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
     if (!dec || !jpegs || !sizes) return fail(c, FM_EINVAL, "null decoder or JPEG arrays");
+    // the decoder writes n * S frames of its own size into the batch's input buffer (sized for this
+    // context's frames): refuse any mismatch before anything is enqueued
+    int dw = 0, dh = 0, ddev = -1, dmax = 0;
+    if (fm_mjpeg_geometry(dec, &dw, &dh, &ddev, &dmax)) return fail(c, FM_EINVAL, "bad decoder");
+    if (dw != c->p.src_w || dh != c->p.src_h || ddev != c->p.device)
+        return fail(c, FM_EINVAL, "decoder for %dx%d frames on device %d, context for %dx%d on device %d", dw, dh, ddev,
+                    c->p.src_w, c->p.src_h, c->p.device);
+    if (n >= 1 && (long long)n * c->p.n_streams > dmax)
+        return fail(c, FM_EINVAL, "decoder takes %d frames per call, the batch has %lld", dmax,
+                    (long long)n * c->p.n_streams);
     return submit_impl(c, nullptr, n, 0, dec, jpegs, sizes);
 }
 

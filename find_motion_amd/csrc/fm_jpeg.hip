@@ -942,6 +942,40 @@ const int kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,
                       41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
                       30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// T.81 Annex K.3 Huffman tables, which libjpeg-turbo's std_huff_tables (jstdhuff.c) installs in
+// table slots 0 (luminance) and 1 (chrominance) of each class that the stream leaves undefined:
+// Motion-JPEG (AVI1) frames from many cameras carry no DHT at all.  The AC symbol lists are an
+// irregular head followed by every remaining (run, size) symbol, size 1..10, in increasing order.
+void std_huff(HuffHost& t, const uint8_t (&bits)[16], const uint8_t* head, int nhead, bool ac) {
+    for (int l = 1; l <= 16; l++) t.bits[l] = bits[l - 1];
+    int n = 0;
+    bool used[256] = {};
+    for (int k = 0; k < nhead; k++) used[t.vals[n++] = head[k]] = true;
+    if (ac)
+        for (int rs = 0; rs < 256; rs++)
+            if ((rs & 15) >= 1 && (rs & 15) <= 10 && !used[rs]) t.vals[n++] = (uint8_t)rs;
+    t.n = n;
+    t.present = true;
+}
+
+void add_std_huff(ParsedJpeg& J) {
+    static const uint8_t dc_bits[2][16] = {{0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0},
+                                           {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0}};
+    static const uint8_t ac_bits[2][16] = {{0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d},
+                                           {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77}};
+    static const uint8_t dc_vals[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+    static const uint8_t ac_head0[40] = {0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51,
+                                         0x61, 0x07, 0x22, 0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1,
+                                         0x15, 0x52, 0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72, 0x82, 0x09, 0x0a, 0x16};
+    static const uint8_t ac_head1[43] = {0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61,
+                                         0x71, 0x13, 0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33,
+                                         0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1};
+    for (int id = 0; id < 2; id++) {
+        if (!J.ht[0][id].present) std_huff(J.ht[0][id], dc_bits[id], dc_vals, 12, false);
+        if (!J.ht[1][id].present) std_huff(J.ht[1][id], ac_bits[id], id ? ac_head1 : ac_head0, id ? 43 : 40, true);
+    }
+}
+
 int parse_jpeg(std::string& err, int idx, const uint8_t* p, size_t n, ParsedJpeg& J) {
     if (n < 4 || p[0] != 0xFF || p[1] != 0xD8) return pfail(err, FM_EINVAL, "frame %d: no SOI", idx);
     size_t i = 2;
@@ -1016,17 +1050,29 @@ int parse_jpeg(std::string& err, int idx, const uint8_t* p, size_t n, ParsedJpeg
                 J.sta[k] = s[2 + 2 * k] & 15;
             }
             J.scan_begin = i + len;
-            // the scan ends at the first marker that is neither stuffing nor RSTn
-            size_t k = J.scan_begin;
-            while (k + 1 < n && !(p[k] == 0xFF && p[k + 1] != 0 && !(p[k + 1] >= 0xD0 && p[k + 1] <= 0xD7))) k++;
-            J.scan_end = k + 1 < n ? k : n;
-            for (size_t q = J.scan_begin; q + 1 < J.scan_end;) {
-                const uint8_t* ff = (const uint8_t*)memchr(p + q, 0xFF, J.scan_end - 1 - q);
+            // the scan ends at the first marker that is neither stuffing (FF 00) nor RSTn; any run of
+            // 0xFF fill bytes may precede a marker (T.81 B.1.1.2) and is skipped, as libjpeg's
+            // fill_bit_buffer and next_marker do (FF FF 00 is a stuffed data byte there too)
+            J.scan_end = n;
+            for (size_t k = J.scan_begin; k < n;) {
+                const uint8_t* ff = (const uint8_t*)memchr(p + k, 0xFF, n - k);
                 if (!ff) break;
-                q = (size_t)(ff - p);
-                if (p[q + 1] >= 0xD0 && p[q + 1] <= 0xD7) J.nrst++;
-                q += 2;
+                k = (size_t)(ff - p);
+                size_t j = k + 1;
+                while (j < n && p[j] == 0xFF) j++;
+                if (j >= n) {
+                    J.scan_end = k;
+                    break;
+                }
+                if (p[j] >= 0xD0 && p[j] <= 0xD7) {
+                    J.nrst++;
+                } else if (p[j] != 0x00) {
+                    J.scan_end = k;
+                    break;
+                }
+                k = j + 1;
             }
+            add_std_huff(J);
             return FM_OK;
         }
         i += len;
@@ -1216,6 +1262,15 @@ int fm_mjpeg_tune(fm_mjpeg* d, int chunk_bits, int spec_bits) {
 }
 
 double fm_mjpeg_last_ms(const fm_mjpeg* d) { return d ? (double)d->last_ms : 0.0; }
+
+int fm_mjpeg_geometry(const fm_mjpeg* d, int* width, int* height, int* device, int* max_frames) {
+    if (!d) return FM_EINVAL;
+    if (width) *width = d->W;
+    if (height) *height = d->H;
+    if (device) *device = d->device;
+    if (max_frames) *max_frames = d->max_frames;
+    return FM_OK;
+}
 
 }  // extern "C"
 

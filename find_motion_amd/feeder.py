@@ -65,7 +65,8 @@ class BatchFeeder:
         # JPEG mode needs every capture to hand out compressed frames of one layout (size and chroma
         # sampling: one GPU decoder serves the whole batch); None: whenever they do, otherwise the
         # captures decode (cap.read())
-        can = bool(self.caps) and all(hasattr(c, "read_jpeg") for c in self.caps) and self._one_layout()
+        can = (bool(self.caps) and all(hasattr(c, "read_jpeg") and getattr(c, "gpu_decode", True) for c in self.caps)
+               and self._one_layout())
         self.jpeg = can if jpeg is None else bool(jpeg)
         if self.jpeg and not can:
             raise ValueError("JPEG mode needs captures with read_jpeg() and one JPEG layout")
@@ -129,11 +130,13 @@ class BatchFeeder:
                     break
                 if self.jpeg:
                     jp = []
+                    # padding for a stream with no frame yet: any frame of this batch (same layout)
+                    pad = next(g[0] for g in got if g)
                     for t in range(T):
                         for s in range(S):
                             if t < len(got[s]):
                                 last[s] = got[s][t]
-                            jp.append(last[s] if last[s] is not None else got[0][0])  # padding
+                            jp.append(last[s] if last[s] is not None else pad)
                     self._full.put(Batch(None, got, T, jp))
                     continue
                 buf = self._free.get()

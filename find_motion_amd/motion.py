@@ -25,16 +25,20 @@ VideoFrame:
   access.  The mask polygons are rasterised once per video (they are static)
   and applied inside the kernel, so mask_off_areas() has nothing left to do.
 
-MJPEG sources (videoio.MjpegAviCapture) are decoded on the GPU in front of
-the hot path (fm_submit_jpeg): frame.raw is then fetched
-from the device on first access (a frame the state machine writes, shows or
-runs a cascade on), and an MJPG output receives the source's JPEG bytes
-unchanged instead of a re-encode.
+Capture: cv2.VideoCapture whenever OpenCV imports, as the reference does
+(fm.py:413).  MJPEG AVIs are decoded on the GPU in front of the hot path
+(videoio.MjpegAviCapture + fm_submit_jpeg) when the caller
+opts in (gpu_decode=True) or OpenCV is absent: frame.raw is then fetched from
+the device on first access (a frame the state machine writes, shows or runs a
+cascade on), and an MJPG output receives the source's JPEG bytes unchanged
+instead of a re-encode.  That decode equals libjpeg-turbo's (cv2.imdecode),
+not FFmpeg's (cv2.VideoCapture's default backend): see videoio.
 
 Extra keyword arguments (not in the reference): device (HIP ordinal),
 batch (frames decoded ahead and processed per kernel launch; the per-frame
 results and the decisions are identical for any batch -- only ref_frame is
-then observed at batch boundaries), capture (a ready capture object).
+then observed at batch boundaries), capture (a ready capture object),
+gpu_decode (see above).
 
 There is no CPU fallback: without the HIP library this module raises
 NativeLibraryMissing at VideoMotion construction.
@@ -209,7 +213,7 @@ class VideoMotion:
                  yolo_tiny: bool = False, *,
                  device: int = 0, batch: int = 1, capture=None, engine: MotionEngine = None,
                  stream: int = 0, keep_planes: bool = None, cascade_dir: str = None,
-                 pipeline_depth: int = None) -> None:
+                 pipeline_depth: int = None, gpu_decode: bool = None) -> None:
         self.filename = filename
         if self.filename is None and capture is None:
             raise Exception("Filename required")
@@ -269,6 +273,7 @@ class VideoMotion:
         self.pipeline_depth = pipeline_depth
         self._stream = int(stream)
         self._capture = capture
+        self.gpu_decode = gpu_decode
         self._ahead: typing.Deque[VideoFrame] = deque()
         self.frames_read = 0
         self._jpeg_dec = None  # one-frame GPU decoder for raw frames of batches already overwritten
@@ -316,7 +321,8 @@ class VideoMotion:
 
     def _load_video(self) -> bool:
         """fm.py:409-424, plus engine creation and the one-time mask rasterisation."""
-        self.cap = videoio.open_capture(self._capture if self._capture is not None else self.filename, self.device)
+        self.cap = videoio.open_capture(self._capture if self._capture is not None else self.filename, self.device,
+                                        self.gpu_decode)
         self.frame_cache = deque(maxlen=self.cache_frames)
         try:
             self._get_video_info()
@@ -708,7 +714,7 @@ class StreamGroup:
         S = len(self.filenames)
         if S == 0:
             raise ValueError("More than 0 files needed")
-        caps = [videoio.open_capture(c if c is not None else f, device)
+        caps = [videoio.open_capture(c if c is not None else f, device, kwargs.get("gpu_decode"))
                 for f, c in zip(self.filenames, captures or [None] * S)]
         w = {int(c.get(videoio.CAP_PROP_FRAME_WIDTH)) for c in caps}
         h = {int(c.get(videoio.CAP_PROP_FRAME_HEIGHT)) for c in caps}

@@ -10,13 +10,22 @@ available:
 * otherwise (this image has no cv2): uncompressed RIFF AVI (BI_RGB, 24-bit
   BGR, bottom-up rows), read and written here -- the container OpenCV itself
   writes for fourcc 'DIB ' and reads through FFmpeg's rawvideo decoder;
-* MJPEG AVI (fourcc 'MJPG', one baseline JPEG per '00dc' chunk), read here
-  whether or not cv2 exists: MjpegAviCapture.read_jpeg() hands the compressed
-  frames to the GPU decoder (find_motion_amd.MJpegDecoder / fm_submit_jpeg,
-  SURVEY.md §8(f)-3), so only compressed bytes cross PCIe; read() decodes
-  on the GPU too.  MjpegAviWriter writes such files: the 'MJPG' output of an
-  MJPEG input keeps the source's JPEG bytes (write_jpeg); write() encodes a
-  BGR frame with Pillow;
+* MJPEG AVI (fourcc 'MJPG', one baseline JPEG per '00dc' chunk): with OpenCV
+  present, cv2.VideoCapture reads it as the reference does (fm.py:413) unless
+  the caller opts in to the GPU decoder (gpu_decode=True, CLI --gpu-decode);
+  without OpenCV it is read here.  MjpegAviCapture.read_jpeg() hands the
+  compressed frames to the GPU decoder (find_motion_amd.MJpegDecoder /
+  fm_submit_jpeg), so only compressed bytes cross PCIe.
+  That decode is bit-exact to libjpeg-turbo's default decode, i.e. to
+  cv2.imdecode and OpenCV's built-in MJPEG reader (CAP_OPENCV_MJPEG) -- not to
+  cv2.VideoCapture's default FFmpeg backend (libavcodec's IDCT and swscale's
+  colour conversion), whose frames may differ by a few levels (that parity is
+  unpinned: neither FFmpeg nor OpenCV is in this image).  A stream the GPU
+  decoder does not take (progressive, 12-bit, 4:1:1 ...) is decoded on the host
+  instead (cv2.imdecode, else Pillow: libjpeg-turbo either way).
+  MjpegAviWriter writes such files: the 'MJPG' output of an MJPEG input keeps
+  the source's JPEG bytes (write_jpeg); write() encodes a BGR frame with
+  Pillow;
 * in-memory sources for tests, benchmarks and embedding: ArrayCapture over a
   [N][H][W][3] uint8 array and SyntheticCapture over the deterministic
   synthetic video of find_motion_amd.synthetic.
@@ -145,6 +154,53 @@ def jpeg_layout(data: bytes):
             return (data[i + 5] << 8) | data[i + 6], (data[i + 7] << 8) | data[i + 8], comps
         i += 2 + ((data[i + 2] << 8) | data[i + 3])
     raise ValueError("no SOF marker")
+
+
+def jpeg_gpu_supported(data: bytes) -> bool:
+    """Whether the GPU decoder takes this JPEG's layout (fm_jpeg.hip parse_jpeg / setup_geometry):
+    SOF0/SOF1 Huffman, 8-bit, one component or three with Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2,
+    one interleaved scan."""
+    try:
+        i = 2
+        if data[:2] != b"\xff\xd8":
+            return False
+        while i + 4 <= len(data):
+            if data[i] != 0xFF:
+                return False
+            while i < len(data) and data[i] == 0xFF:
+                i += 1
+            m = data[i]
+            i += 1
+            if m == 0xD9 or m == 0x01 or 0xD0 <= m <= 0xD7:
+                continue
+            ln = (data[i] << 8) | data[i + 1]
+            seg = data[i + 2:i + ln]
+            if 0xC0 <= m <= 0xCF and m not in (0xC4, 0xC8, 0xCC):
+                if m not in (0xC0, 0xC1) or seg[0] != 8:
+                    return False
+                nc = seg[5]
+                hv = [(seg[7 + 3 * c] >> 4, seg[7 + 3 * c] & 15) for c in range(nc)]
+                if nc == 1:
+                    return 1 <= hv[0][0] <= 4 and 1 <= hv[0][1] <= 4
+                return nc == 3 and hv[1] == hv[2] == (1, 1) and hv[0] in ((1, 1), (2, 1), (2, 2))
+            if m == 0xDA:
+                return False
+            i += ln
+    except IndexError:
+        return False
+    return False
+
+
+def host_decode_jpeg(data: bytes) -> np.ndarray:
+    """One JPEG -> BGR u8 on the host with libjpeg-turbo: cv2.imdecode when OpenCV exists, else Pillow."""
+    if cv2 is not None:
+        return cv2.imdecode(np.frombuffer(data, np.uint8), cv2.IMREAD_COLOR)
+    import io
+
+    from PIL import Image
+    im = Image.open(io.BytesIO(data))
+    im = im.convert("RGB") if im.mode != "RGB" else im
+    return np.ascontiguousarray(np.asarray(im)[..., ::-1])
 
 
 def _jpeg_size(data: bytes):
@@ -349,13 +405,21 @@ FOURCC_MJPG = b"MJPG"
 
 
 class MjpegAviCapture(RawAviCapture):
-    """MJPEG AVI reader: read_jpeg() -> (ok, JPEG bytes) for the GPU decoder; read() -> (ok, BGR frame),
-    decoded on the GPU (a one-frame MJpegDecoder on `device`, created on first use)."""
+    """MJPEG AVI reader: read_jpeg() -> (ok, JPEG bytes) for the GPU decoder; read() -> (ok, BGR frame).
 
-    def __init__(self, path: str, device: int = 0):
+    gpu_decode (True unless the caller turns it off or the first frame's layout is one the GPU decoder
+    does not take, jpeg_gpu_supported): read() decodes on the GPU (a one-frame MJpegDecoder on `device`,
+    created on first use) and BatchFeeder hands the compressed frames to fm_submit_jpeg; otherwise
+    read() decodes on the host (host_decode_jpeg) and the feeder copies decoded frames."""
+
+    def __init__(self, path: str, device: int = 0, gpu_decode: bool = True):
         self._device = int(device)
         self._dec = None
         super().__init__(path)
+        first = self.peek_jpeg()
+        self.gpu_decode = bool(gpu_decode) and (first is None or jpeg_gpu_supported(first))
+        if gpu_decode and not self.gpu_decode:
+            log.info("%s: JPEG layout not supported by the GPU decoder; decoding on the host", path)
 
     def _walk(self, f, start, end, depth):
         pos = start
@@ -399,6 +463,8 @@ class MjpegAviCapture(RawAviCapture):
         ok, j = self.read_jpeg()
         if not ok:
             return False, None
+        if not self.gpu_decode:
+            return True, host_decode_jpeg(j)
         if self._dec is None:
             from ._native import MJpegDecoder
             self._dec = MJpegDecoder(self.w, self.h, max_frames=1, device=self._device)
@@ -488,8 +554,13 @@ def is_mjpeg_avi(path) -> bool:
     return head[:4] == b"RIFF" and head[8:12] == b"AVI " and FOURCC_MJPG in head
 
 
-def open_capture(source, device: int = 0):
+def open_capture(source, device: int = 0, gpu_decode: bool | None = None):
     """cv2.VideoCapture(source) when OpenCV exists (fm.py:413); otherwise the readers above.
+
+    gpu_decode: MJPEG AVI files go to MjpegAviCapture (GPU decode, libjpeg-turbo-exact) when True, or
+    when None (the default) and OpenCV is absent.  With OpenCV present and gpu_decode not True the
+    reference's own capture is returned, whatever the codec.  gpu_decode=False without OpenCV still
+    reads MJPEG AVIs with MjpegAviCapture, decoding on the host.
 
     `source` may also be an object that already speaks the capture protocol,
     a uint8 array [N][H][W][3], or "synthetic:WxH:N[:stream]".
@@ -504,8 +575,11 @@ def open_capture(source, device: int = 0):
         return SyntheticCapture(w, h, int(parts[2]), int(parts[3]) if len(parts) > 3 else 0)
     if isinstance(source, str) and source.endswith(".npy"):
         return ArrayCapture(np.load(source, mmap_mode="r", allow_pickle=False))
-    if isinstance(source, str) and is_mjpeg_avi(source):
-        return MjpegAviCapture(source, device)  # compressed frames to the GPU decoder (§8(f)-3)
+    if isinstance(source, str) and is_mjpeg_avi(source) and (cv2 is None or gpu_decode):
+        cap = MjpegAviCapture(source, device, gpu_decode=gpu_decode is not False)
+        if cap.isOpened() and (cap.gpu_decode or cv2 is None):
+            return cap  # compressed frames to the GPU decoder (§8(f)-3), or host decode without cv2
+        cap.release()  # opted in, but the layout needs the host: the reference's capture
     if cv2 is not None:
         return cv2.VideoCapture(source)
     if isinstance(source, int):

@@ -112,6 +112,17 @@ int fm_max_inflight(const fm_ctx* ctx);
  * submitted before waiting; fm_wait completes them in submission order. */
 int fm_submit(fm_ctx* ctx, const uint8_t* frames, int n_frames, int on_device);
 
+/* fm_submit with one frame pointer per stream, SURVEY.md §8(b)'s
+ * fm_submit(ctx, const uint8_t* const* bgr, n_frames): bgr[s] holds stream s's
+ * n_frames consecutive frames [n_frames][src_h][src_w][3] (e.g. what a
+ * per-stream decoder wrote).  Host memory: one strided DMA per stream puts them
+ * into the batch's [t][s] layout on the input stream (no gather copy on the
+ * host; page-locked buffers make it asynchronous).  Device memory: read in
+ * place for one stream, one strided device copy per stream otherwise.
+ * Results are identical to fm_submit of the same frames gathered into
+ * [n_frames][n_streams] order; the same lifetime rules apply. */
+int fm_submit_streams(fm_ctx* ctx, const uint8_t* const* bgr, int n_frames, int on_device);
+
 /* Page-locked host memory for frame batches (a decoder writes frames here): fm_submit
  * of such a buffer is a true asynchronous DMA (hipMemcpyAsync) on the context's input
  * stream, overlapped with the previous batch's kernels (north_star: "frame batches
@@ -220,10 +231,15 @@ int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);
 double fm_haar_last_ms(const fm_haar* det);
 
 /* ---- Decode side: MJPEG frames decoded on the GPU ------
- * Replaces cv2.VideoCapture.read (find_motion.py:413, :497-506) for MJPEG
- * video, where every frame is one baseline JPEG.  The decode is libjpeg-
- * turbo's default one (what OpenCV and Pillow call): jpeg_idct_islow, fancy
- * upsampling, integer YCbCr->RGB tables, BGR u8 HWC out as cap.read() returns.
+ * Stands in for cv2.VideoCapture.read (find_motion.py:413, :497-506) on MJPEG
+ * video, where every frame is one baseline JPEG, when the caller opts in (or
+ * OpenCV is absent).  The decode is libjpeg-turbo's default one: jpeg_idct_islow,
+ * fancy upsampling, integer YCbCr->RGB tables, BGR u8 HWC -- bit-exact to
+ * cv2.imdecode and to OpenCV's built-in MJPEG reader (CAP_OPENCV_MJPEG), NOT to
+ * cv2.VideoCapture's default FFmpeg backend (libavcodec IDCT + swscale), whose
+ * output can differ by a few levels; that parity is unpinned here.
+ * Frames without a DHT segment (AVI1 Motion-JPEG) get the T.81 Annex K tables,
+ * as libjpeg-turbo's std_huff_tables installs them.
  * Supported: 8-bit baseline / extended-sequential Huffman JPEG, grayscale or
  * YCbCr with Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2, restart intervals
  * optional (each interval is decoded by its own lane; without them one lane
@@ -245,11 +261,15 @@ int fm_mjpeg_decode(fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* si
                     int out_on_device);
 /* Device time of the last fm_mjpeg_decode's kernels (HIP events), ms. */
 double fm_mjpeg_last_ms(const fm_mjpeg* dec);
+/* The frame size, device and max_frames the decoder was created with. */
+int fm_mjpeg_geometry(const fm_mjpeg* dec, int* width, int* height, int* device, int* max_frames);
 /* fm_submit from compressed frames: n_frames x n_streams JPEGs in [t][s]
  * order, decoded by dec (created for this context's src_w x src_h) on the
  * context's input stream into the batch's device buffer, then processed as
  * fm_submit (frames, n_frames, on_device = 1) would.  The host buffers may be
- * reused when the call returns. */
+ * reused when the call returns.  FM_EINVAL (nothing enqueued) when dec was
+ * created for another frame size or device, or for fewer than
+ * n_frames x n_streams frames per call. */
 int fm_submit_jpeg(fm_ctx* ctx, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n_frames);
 /* Tuning of the parallel Huffman decode (no reference counterpart): every entropy-coded segment is
  * cut into chunks of chunk_bits bits, one GPU lane each, and each lane speculates its entry state

@@ -86,10 +86,19 @@ def parse(data: bytes) -> dict:
             scan = {"sel": sel}
             j = i + ln
             k = j
-            while k < len(data) - 1:
-                if data[k] == 0xFF and data[k + 1] != 0 and not (0xD0 <= data[k + 1] <= 0xD7):
-                    break
-                k += 1
+            # the scan ends at the first marker that is neither FF 00 nor RSTn; a run of 0xFF fill bytes
+            # may precede any marker (T.81 B.1.1.2; libjpeg's next_marker skips them)
+            while k < len(data):
+                if data[k] != 0xFF:
+                    k += 1
+                    continue
+                q = k + 1
+                while q < len(data) and data[q] == 0xFF:
+                    q += 1
+                if q < len(data) and (data[q] == 0 or 0xD0 <= data[q] <= 0xD7):
+                    k = q + 1
+                    continue
+                break
             scan["data"] = data[j:k]
             i = k
             continue
@@ -98,7 +107,30 @@ def parse(data: bytes) -> dict:
         raise JpegError("no frame or scan")
     if len(scan["sel"]) != len(frame["comps"]):
         raise JpegError("multi-scan (non-interleaved) JPEG not supported")
+    for key, tab in STD_HUFF.items():  # jstdhuff.c std_huff_tables: slots 0 and 1 the stream left undefined
+        ht.setdefault(key, tab)
     return {"qt": qt, "ht": ht, "frame": frame, "scan": scan, "dri": dri}
+
+
+def _std_ac(bits: list[int], head: list[int]) -> tuple:
+    """An Annex K AC table: its irregular head, then every other (run, size) symbol, size 1..10, in order."""
+    tail = [rs for rs in range(256) if 1 <= (rs & 15) <= 10 and rs not in head]
+    return bits, head + tail
+
+
+# T.81 Annex K.3 (libjpeg-turbo jstdhuff.c): what MJPEG frames without a DHT segment are decoded with
+STD_HUFF = {
+    (0, 0): ([0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0], list(range(12))),
+    (0, 1): ([0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0], list(range(12))),
+    (1, 0): _std_ac([0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d],
+                    [0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07,
+                     0x22, 0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0,
+                     0x24, 0x33, 0x62, 0x72, 0x82, 0x09, 0x0a, 0x16]),
+    (1, 1): _std_ac([0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77],
+                    [0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71,
+                     0x13, 0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0,
+                     0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1]),
+}
 
 
 def huff_lookup(bits: list[int], vals: list[int]) -> dict:
@@ -125,10 +157,12 @@ class _Bits:
             byte = 0
             if self.p < len(self.b):
                 byte = self.b[self.p]
-                if byte == 0xFF:
-                    nxt = self.b[self.p + 1] if self.p + 1 < len(self.b) else 0
-                    if nxt == 0:
-                        self.p += 2
+                if byte == 0xFF:  # fill_bit_buffer: skip 0xFF fill bytes; FF 00 is a data 0xFF
+                    q = self.p + 1
+                    while q < len(self.b) and self.b[q] == 0xFF:
+                        q += 1
+                    if q < len(self.b) and self.b[q] == 0:
+                        self.p = q + 1
                     else:  # a marker: feed zeros, do not consume it
                         byte = 0
                 else:

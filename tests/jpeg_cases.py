@@ -1,5 +1,7 @@
 """JPEG test inputs for the decode side (§8(f)-3): frames encoded by Pillow (libjpeg-turbo), decoded by Pillow
-as the reference decode (what cv2.VideoCapture / imdecode call: libjpeg defaults)."""
+as the reference decode.  That is libjpeg-turbo's default decode, i.e. cv2.imdecode and OpenCV's built-in
+MJPEG reader (CAP_OPENCV_MJPEG); cv2.VideoCapture's default FFmpeg backend decodes with libavcodec + swscale
+instead, which nothing here can pin (neither is in the image)."""
 from __future__ import annotations
 
 import io
@@ -47,3 +49,43 @@ def reference_decode(data: bytes) -> np.ndarray:
     if a.ndim == 2:
         return np.repeat(a[..., None], 3, axis=2)
     return np.ascontiguousarray(a[..., ::-1])
+
+
+def segments(data: bytes):
+    """(marker, start, end) of every marker segment before the scan data (SOI excluded)."""
+    out, i = [], 2
+    while i + 4 <= len(data) and data[i] == 0xFF:
+        m = data[i + 1]
+        ln = (data[i + 2] << 8) | data[i + 3]
+        out.append((m, i, i + 2 + ln))
+        if m == 0xDA:
+            break
+        i += 2 + ln
+    return out
+
+
+def strip_dht(data: bytes) -> bytes:
+    """The same JPEG without its DHT segments (the AVI1 Motion-JPEG form many cameras write: the decoder
+    supplies the T.81 Annex K tables, which are exactly what libjpeg-turbo encodes with by default)."""
+    out, last = bytearray(data[:2]), 2
+    for m, a, b in segments(data):
+        out += data[last:a]
+        if m != 0xC4:
+            out += data[a:b]
+        last = b
+    return bytes(out + data[last:])
+
+
+def fill_before_markers(data: bytes, n: int = 2) -> bytes:
+    """Insert n 0xFF fill bytes before every RSTn marker and the EOI of the scan (T.81 B.1.1.2 allows any
+    number; libjpeg skips them)."""
+    sos = [s for s in segments(data) if s[0] == 0xDA][0]
+    head, scan = data[:sos[2]], data[sos[2]:]
+    out, k = bytearray(), 0
+    while k < len(scan):
+        c = scan[k]
+        if c == 0xFF and k + 1 < len(scan) and (0xD0 <= scan[k + 1] <= 0xD7 or scan[k + 1] == 0xD9):
+            out += b"\xff" * n
+        out.append(c)
+        k += 1
+    return bytes(head + out)

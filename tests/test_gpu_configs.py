@@ -171,6 +171,67 @@ def test_k97_per_frame_path():
     _run_streams(1920, 120, 1920, k, S=2, T=3, NB=2, mask_every=1)
 
 
+def test_per_frame_path_more_contours_than_cap_over_batches():
+    """k > 49 (the per-frame k_pixel + pixel-level CCL path): frames with more contours than max_contours,
+    batches of several frames, several batches.  A frame past the cap is relabelled whole at fm_wait; that
+    must not shrink the batch-wide record buffer the next submit writes (advisor, round 2)."""
+    H, W, k, T, NB, cap = 540, 960, 51, 3, 3, 50
+    fr = np.zeros((T * NB, 1, H, W, 3), np.uint8)
+    for i in range(T * NB):
+        o = 8 * (i % 2)
+        for y in range(12 + o, H - 8, 64):
+            for x in range(12 + o, W - 8, 64):
+                fr[i, 0, y:y + 6, x:x + 6] = 255
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=k, threshold=0, avg=0.5, max_batch=T,
+                       max_contours=cap)
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=k, thresh=0, alpha=0.5))
+    res = orc.run(fr[:, 0], cap=1 << 14, mask_frames=range(0, T * NB, 2))
+    assert res.counts[1:].min() > cap
+    for b in range(NB):
+        eng.submit(fr[b * T:(b + 1) * T])
+        eng.wait()
+        for t in range(T):
+            _check_frame(eng, res, t, 0, b * T + t, f"batch {b} frame {t}")
+    np.testing.assert_array_equal(eng.background(0), orc.bg)
+    eng.close()
+
+
+def test_submit_streams_equals_submit():
+    """fm_submit_streams (one frame buffer per stream) == fm_submit of the same frames gathered
+    into [t][s] order: host buffers, device buffers, and one stream's device buffer read in place."""
+    torch = pytest.importorskip("torch")
+    W, H, S, T = 320, 240, 3, 4
+    kw = dict(src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    a, b, c = (MotionEngine(n_streams=S, **kw) for _ in range(3))
+    d, e = MotionEngine(n_streams=1, **kw), MotionEngine(n_streams=1, **kw)
+    for bi in range(3):
+        f = batch(W, H, S, bi * T, T)
+        per = [np.ascontiguousarray(f[:, s]) for s in range(S)]
+        dev = [torch.from_numpy(p).to("cuda:0") for p in per]
+        torch.cuda.synchronize()
+        a.submit(f)
+        b.submit_streams(per)
+        c.submit_streams([t.data_ptr() for t in dev], on_device=True, n_frames=T)
+        d.submit(f[:, :1])
+        e.submit_streams([dev[0].data_ptr()], on_device=True, n_frames=T)
+        for x in (a, b, c, d, e):
+            x.wait()
+        for x in (b, c):
+            assert np.array_equal(a.counts(), x.counts())
+        assert np.array_equal(d.counts(), e.counts()) and np.array_equal(d.counts()[:, 0], a.counts()[:, 0])
+        for t in range(T):
+            for s in range(S):
+                want = [q.bbox for q in a.contours(t, s)]
+                assert [q.bbox for q in b.contours(t, s)] == want and [q.bbox for q in c.contours(t, s)] == want
+                assert np.array_equal(a.mask(t, s), b.mask(t, s)) and np.array_equal(a.mask(t, s), c.mask(t, s))
+            assert [q.bbox for q in e.contours(t, 0)] == [q.bbox for q in a.contours(t, 0)]
+    for s in range(S):
+        assert np.array_equal(a.background(s), b.background(s)) and np.array_equal(a.background(s), c.background(s))
+    assert np.array_equal(e.background(0), a.background(0))
+    for x in (a, b, c, d, e):
+        x.close()
+
+
 @pytest.mark.parametrize("k", [11, 33, 49])
 def test_k_fused_generic_taps(k):
     """k outside k_pix's {3, 5, 7, 21} and <= 49: the generic temporally blocked k_fused kernel."""

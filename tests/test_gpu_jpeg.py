@@ -1,7 +1,9 @@
 """Decode side on the GPU: fm_mjpeg_* / fm_submit_jpeg against Pillow's libjpeg-turbo.
 
-The reference gets frames from cv2.VideoCapture.read (fm.py:413, 497-506); on MJPEG video that is a
-libjpeg(-turbo) default decode per frame.  Every case here is bit-exact against Pillow's decode of the same
+The reference gets frames from cv2.VideoCapture.read (fm.py:413, 497-506).  The GPU decoder reproduces
+libjpeg-turbo's default decode -- cv2.imdecode / OpenCV's built-in MJPEG reader -- not the FFmpeg backend
+cv2.VideoCapture picks by default (that parity is unpinned; videoio keeps cv2.VideoCapture whenever OpenCV
+exists unless the caller opts in).  Every case here is bit-exact against Pillow's decode of the same
 bytes (the CPU restatement oracle/jpeg.py is pinned to it in tests/test_jpeg_host.py), and the whole path
 from JPEG bytes to contours equals the path from the reference-decoded frames."""
 import numpy as np
@@ -9,7 +11,7 @@ import pytest
 
 from find_motion_amd import FMError, MJpegDecoder, MotionEngine
 from find_motion_amd.synthetic import SyntheticVideo
-from jpeg_cases import ENCODINGS, Image, encode, image, reference_decode
+from jpeg_cases import ENCODINGS, Image, encode, fill_before_markers, image, reference_decode, strip_dht
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(Image is None, reason="Pillow not importable")]
 
@@ -174,3 +176,57 @@ def test_per_frame_optimized_huffman_tables():
         for i, f in enumerate(frames):
             assert np.array_equal(got[i], reference_decode(f)), (cb, i)
         dec.close()
+
+
+def test_frames_without_dht_use_the_standard_tables():
+    """AVI1 Motion-JPEG (no DHT segment, as many webcams / IP cameras write): decoded with the T.81 Annex K
+    tables libjpeg-turbo installs (std_huff_tables), alone and mixed with frames that carry the same tables."""
+    v = SyntheticVideo(320, 240, 11)
+    full = [encode(v.frame(t), quality=q) for t, q in enumerate((75, 90, 60, 85))]
+    full.append(encode(v.frame(4), quality=80, restart_marker_rows=1))
+    bare = [strip_dht(j) for j in full]
+    for cb in (512, 64):
+        dec = MJpegDecoder(320, 240, max_frames=len(full) * 2, chunk_bits=cb)
+        got = dec.decode(bare + full[::-1])
+        want = [reference_decode(j) for j in full]
+        for i in range(len(full)):
+            assert np.array_equal(got[i], want[i]), (cb, i)
+            assert np.array_equal(got[len(full) + i], want[len(full) - 1 - i]), (cb, i)
+        dec.close()
+    g = [encode(image(37, 53, "smooth", seed=s)[..., 0], quality=70) for s in range(2)]  # grayscale, table 0 only
+    dec = MJpegDecoder(53, 37, max_frames=2)
+    out = dec.decode([strip_dht(j) for j in g])
+    assert all(np.array_equal(out[i], reference_decode(g[i])) for i in range(2))
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_fill_bytes_before_markers(n):
+    """0xFF fill bytes before every RSTn and the EOI (T.81 B.1.1.2): skipped as libjpeg does, not taken for
+    the end of the scan."""
+    v = SyntheticVideo(320, 240, 12)
+    frames = [encode(v.frame(0), quality=80, restart_marker_blocks=3), encode(v.frame(1), quality=90, restart_marker_rows=1),
+              encode(image(240, 320, "noise", seed=4), quality=75, restart_marker_blocks=1), encode(v.frame(2), quality=70)]
+    filled = [fill_before_markers(j, n) for j in frames]
+    dec = MJpegDecoder(320, 240, max_frames=len(frames))
+    got = dec.decode(filled)
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f)), i
+    dec.close()
+
+
+def test_submit_jpeg_refuses_a_mismatched_decoder():
+    """A decoder created for another frame size, or for fewer frames than a batch holds, is refused before
+    anything is enqueued (its output would not fit the batch's input buffer)."""
+    W, H, S, T = 64, 48, 2, 3
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    jp = [encode(image(H, W, "smooth", seed=s), quality=80) for s in range(T * S)]
+    for dec in (MJpegDecoder(W * 2, H, max_frames=T * S), MJpegDecoder(W, H, max_frames=T * S - 1)):
+        with pytest.raises(FMError):
+            eng.submit_jpeg(dec, jp)
+        dec.close()
+    dec = MJpegDecoder(W, H, max_frames=T * S)
+    eng._inflight.clear()
+    eng.submit_jpeg(dec, jp)  # the context is still usable
+    eng.wait()
+    assert eng.counts().shape == (T, S)
+    eng.close()
