@@ -58,10 +58,26 @@ def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | 
             t = json.load(fh)
     except (OSError, ValueError):
         return None, None, None
-    if t.get("workload") != cfg["workload"] or kernel not in t.get("kernels", {}):
+    entries = t.get("entries", [t])  # one entry per profiled workload (tools/traffic.py)
+    e = next((e for e in entries if e.get("workload") == cfg["workload"] and kernel in e.get("kernels", {})), None)
+    if e is None:
         return None, None, None
-    k = t["kernels"][kernel]
-    return int(k["traffic_bytes"]), t.get("source"), k.get("sq")
+    k = e["kernels"][kernel]
+    return int(k["traffic_bytes"]), e.get("source"), k.get("sq")
+
+
+def config_name(S: int, W: int, H: int, mode: str, k: int) -> str:
+    """Which BASELINE.json config the run's shape is (configs[1] is the headline; the others are the parity
+    configurations run at their quoted perf shapes), so a line is never filed under the wrong one."""
+    if (W, H) == (1920, 1080):
+        if S == 1:
+            return "configs[1]" if mode == "F" else "configs[1] (mode D)"
+        if S == 8:
+            return "configs[2]" if mode == "F" else "configs[2] (mode D)"
+        return f"{S} x 1080p streams (configs[2]/[3] family)"
+    if (W, H) == (3840, 2160) and k == 21:
+        return "configs[4] geometry (no Haar stage)"
+    return "custom shape"
 
 
 def cpu_model() -> str:
@@ -253,7 +269,7 @@ def main() -> None:
     k = make_gaussian(box, blur_scale)
     S, T = args.streams, args.batch
     R = max(args.ring - args.ring % T, T)
-    cfg = {"workload": f"configs[1]: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
+    cfg = {"workload": f"{config_name(S, W, H, args.mode, k)}: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
                        f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
                        + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,

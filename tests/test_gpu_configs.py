@@ -7,9 +7,11 @@ allows, so full-size sequences finish in seconds).
   device-resident ring cycling 64 synthetic frames, the production
   k_pix<5, false, false> (no planes kept), fm_max_inflight batches submitted
   before the first wait, a ring wrap onto reused batch slots;
-* configs[2]: 8 x 1080p streams on one GPU, batches in flight;
+* configs[2]: 8 x 1080p streams on one GPU, batches in flight -- also at the
+  perf shape quoted for it (T = 128 per launch, 4 in flight, device ring);
 * configs[4] geometry: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the two
-  MASK_SCHEMA polygons (find_motion.py:86-100);
+  MASK_SCHEMA polygons (find_motion.py:86-100) -- also at its perf shape
+  (T = 64, 2 in flight);
 * more contours than max_contours (a dot lattice: every contour counted and
   kept, in raster order, fm.py:674-694), heavy tiles, and the pixel-level
   fallback once a batch exhausts its node pool;
@@ -112,6 +114,66 @@ def test_config5_four_4k_streams_k21_masks():
     k = make_gaussian(3840, 183)
     assert k == 21
     _run_streams(3840, 2160, 3840, k, S=4, T=3, NB=2, masks=CONFIG5_MASKS, start=10, mask_every=2)
+
+
+def _run_ring(W, H, box, k, S, T, NB, depth, period, masks=None, mask_every=23, threads=2):
+    """bench.py's loop at a BASELINE config's quoted perf shape: a [T][S] device-resident ring cycling `period`
+    synthetic frames per stream, `depth` batches submitted before the first wait, NB batches (slots reused),
+    every frame of every stream against the oracle (counts, boxes, start pixels; sampled masks), then the
+    final backgrounds."""
+    torch = pytest.importorskip("torch")
+    uniq = batch(W, H, S, 0, period)
+    ring_h = np.concatenate([uniq] * (T // period)) if T > period else uniq[:T]
+    assert ring_h.shape[0] == T
+    ring = torch.from_numpy(ring_h).to("cuda:0")
+    torch.cuda.synchronize()
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=T,
+                       max_contours=1 << 14)
+    assert not eng.keep_planes and depth <= eng.max_inflight
+    h, w = eng.work_shape
+    cfg = oracle.OracleConfig(H=H, W=W, box=box, ksize=k)
+    keeps = [None] * S
+    if masks:
+        for s in range(S):
+            keeps[s] = rasterize_masks(h, w, box / W, masks)
+            eng.set_mask(s, keeps[s])
+    orc = [oracle.OracleStream(cfg, keeps[s]) for s in range(S)]
+    for _ in range(depth):
+        eng.submit_device(ring.data_ptr(), T)
+    pool = ThreadPoolExecutor(S)
+    total = 0
+    for b in range(NB):
+        res = list(pool.map(lambda s: orc[s].run(ring_h[:, s], cap=1 << 14,
+                                                 mask_frames=range((b + 3 * s) % mask_every, T, mask_every),
+                                                 nthreads=threads), range(S)))
+        eng.wait()
+        for s in range(S):
+            for t in range(T):
+                _check_frame(eng, res[s], t, s, t, f"batch {b} frame {t} stream {s}")
+            total += int(res[s].counts.sum())
+        if b + depth < NB:
+            eng.submit_device(ring.data_ptr(), T)
+    for s in range(S):
+        np.testing.assert_array_equal(eng.background(s), orc[s].bg, err_msg=f"background stream {s}")
+    assert total > 0
+    pool.shutdown()
+    eng.close()
+
+
+@pytest.mark.timeout(400)
+def test_config3_perf_shape_eight_streams_t128():
+    """configs[2] at the shape its throughput is quoted on (bench.py --streams 8 --batch 128): 8 x 1080p
+    streams, 128 frames per stream per launch, 4 batches in flight, 5 batches (slot reuse)."""
+    _run_ring(1920, 1080, 1920, 5, S=8, T=128, NB=5, depth=4, period=64)
+
+
+@pytest.mark.timeout(400)
+def test_config5_perf_shape_four_4k_streams_t64():
+    """configs[4] geometry at its quoted perf shape (bench.py --width 3840 --height 2160 --blur-scale 183
+    --streams 4 --batch 64): k 21, the MASK_SCHEMA polygons, 64 frames per stream per launch, 2 batches in
+    flight, 3 batches."""
+    k = make_gaussian(3840, 183)
+    _run_ring(3840, 2160, 3840, k, S=4, T=64, NB=3, depth=2, period=16, masks=CONFIG5_MASKS, threads=4)
 
 
 def _lattice_frames(H, W, pitch, n, offset=0):

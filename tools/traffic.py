@@ -65,8 +65,15 @@ def main(prof, bench_log, tag):
                 "lds_bank_conflict_per_active": round(m.get("SQ_LDS_BANK_CONFLICT", 0) / max(m.get("SQ_ACTIVE_INST_LDS", 1), 1), 3),
                 "waves": round(m.get("SQ_WAVES", 0))}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+    entries = []
+    try:  # one entry per workload: replace this workload's, keep the others
+        with open(path) as fh:
+            old = json.load(fh)
+        entries = [e for e in old.get("entries", [old]) if e.get("workload") != workload]
+    except (OSError, ValueError):
+        pass
     with open(path, "w") as fh:
-        json.dump(out, fh, indent=1)
+        json.dump({"entries": entries + [out]}, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
