@@ -964,6 +964,292 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// k_pixw<KC>: k_pix5's decomposition for wide Gaussians (KC = 21: config 5's -B 3840 -b 183,
+// fm.py:478-484).  k_pix<21> staged raw BGR in LDS, recomputed each gray quad in every lane
+// that needed it and ran a 28-row u16 column per lane through alignbit + dot2 (168 VGPRs, 81
+// SGPR spills, ~90 VALU lane-ops per pixel-frame, one workgroup per CU).  Here, as in k_pix5:
+//   gray  : 12-B pixel quads loaded straight into registers one frame ahead, one gray dword per
+//           job into LDS: (64 + 2R) rows x (16 + 2 PC / 4) quads per frame;
+//   taps  : one job = 2 H rows x 4 columns; only the non-zero taps (OpenCV's k = 21 taps end in
+//           zeros) as v_dot4 groups over byte windows; stored as row pairs (one ds_write_b128);
+//   chain : per output row the pairs start on an even H row, choosing which zero tap of the
+//           window the pair grid absorbs (row parity), so no alignbit; the rest is chain_rows.
+// REFLECT_101 columns: quads left of column 0 / right of column w-1 are never loaded; on the
+// two edge tiles of a tile row the tap jobs rebuild them from the mirrored inside quads (one
+// v_perm of two gray dwords: quad at column c < 0 holds gray(-c .. -c-3), at c >= w gray(2w-2-c ..)).
+// Rows: reflect101 source rows, as k_pix5.  Needs w % 4 == 0 and w >= 2 * PC + 8.
+template <int K> constexpr int tap_c(int t) { return t < 0 || t >= K ? 0 : Taps<K>::c[t]; }
+template <int K> constexpr int tap_lo() {
+    int i = 0;
+    while (Taps<K>::c[i] == 0) i++;
+    return i;
+}
+template <int K> constexpr int tap_hi() {
+    int i = K - 1;
+    while (Taps<K>::c[i] == 0) i--;
+    return i;
+}
+
+template <int KC>
+struct PW {
+    static constexpr int R = KC / 2;
+    static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
+    static constexpr int GH = TS + 2 * R;          // gray rows (even)
+    static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
+    static constexpr int NG = GH * GQ;             // gray jobs per frame
+    static constexpr int GSLOTS = (NG + 63) / 64;
+    static constexpr int GJ = (GSLOTS + NW - 1) / NW;  // gray rounds per wave: slot i * NW + wave
+    static constexpr int NHP = GH / 2;             // H row pairs
+    static constexpr int NH = NHP * (TS / 4);      // tap jobs
+    static constexpr int HJ = (NH + NT - 1) / NT;
+    static constexpr int HLASTW = (NH - (HJ - 1) * NT + 63) / 64;  // waves with a job in the last round
+    static constexpr int GBUF = NG + 64;           // + a pad slot per lane (idle gray jobs)
+    static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
+    static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
+    static constexpr int NGR = (HI - LO + 4) / 4;  // dot4 groups per output
+    static constexpr int OFF = PC - R;             // byte of output k's tap 0 in its job's window: OFF + k
+    static constexpr int WQ = (3 + OFF + LO + 4 * NGR - 1) / 4 + 1;  // gray dwords per row a tap job reads
+    // chain: output row j of a wave takes pairs p0(j) .. p0(j) + np(j) - 1 (relative to the wave's first pair)
+    static constexpr int p0(int j) { return (j + LO) >> 1; }
+    static constexpr int np(int j) { return (j + HI + 2 - 2 * p0(j)) / 2; }
+    static constexpr int np_max() {
+        int m = 0;
+        for (int j = 0; j < RPWV; j++) m = p0(j) + np(j) > m ? p0(j) + np(j) : m;
+        return m;
+    }
+    static constexpr int NP = np_max();            // pairs a wave's chain reads
+    static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
+};
+template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
+    uint32_t v = 0;
+    for (int b = 0; b < 4; b++) {
+        const int t = PW<KC>::LO + 4 * g + b;
+        if (t <= PW<KC>::HI) v |= (uint32_t)Taps<KC>::c[t] << (8 * b);
+    }
+    return v;
+}
+template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of output row j: taps (ft, ft + 1)
+    const int ft = 2 * (PW<KC>::p0(j) + i) - j;
+    return (uint32_t)tap_c<KC>(ft) | (uint32_t)tap_c<KC>(ft + 1) << 16;
+}
+
+// chain_rows for k_pixw: H as row pairs, even-aligned pair windows (no alignbit)
+template <int KC, bool KEEP, bool TAIL>
+__device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
+                                             int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
+                                             uint32_t& flags) {
+    using G = PW<KC>;
+    uint32_t P[G::NP];
+    const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
+#pragma unroll
+    for (int i = 0; i < G::NP; i++) P[i] = col[i * TS];
+    const int w = a.w;
+    const double beta = a.beta;
+    const int thr = min(max(a.thresh, -1), 255);
+    const uint32_t bias = (uint32_t)(255 - thr);
+    uint32_t tb = 0;
+    static_for<RPWV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        uint32_t acc = 32768u;
+        static_for<G::np(j)>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, P[G::p0(j) + i]),
+                                         __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
+        });
+        if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
+        const uint32_t blur = acc >> 16;
+        const double b = bg[j];
+        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
+        const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
+        tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
+        const double bl = atab[blur];
+        double nb = __fma_rn(b, beta, bl);
+        if (TAIL) {
+            const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
+            if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
+        }
+        bg[j] = nb;
+    });
+    tb &= cc.tbmask;
+    colbits = tb;
+    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
+    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
+    uint32_t fl = 0;
+    if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
+    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    flags = fl;
+}
+
+template <int KC, bool KEEP, bool TAIL>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pixw(FusedArgs a) {
+    using G = PW<KC>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
+    uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
+    uint32_t* Hs = reinterpret_cast<uint32_t*>(smem + 2 * G::GBUF * 4);          // [2][HBUF]
+    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 4);
+    const int tid = threadIdx.x, ln = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int s = blockIdx.y;
+    const int ti = swizzle_tile(blockIdx.x, a.ntiles);
+    const int h = a.h, w = a.w, S = a.S;
+    const int tx = ti % a.ntx, ty = ti / a.ntx;
+    const int x0 = tx * TS, y0 = ty * TS;
+    const size_t plane = (size_t)h * w;
+    const size_t fbytes = plane * 3;
+    const bool hk = a.has_keep[s] != 0;
+    const uint8_t* keep = a.keep + (size_t)s * plane;
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+
+    // ---- per-thread job plans (frame invariant)
+    uint32_t goff[G::GJ], gdst[G::GJ];
+#pragma unroll
+    for (int i = 0; i < G::GJ; i++) {
+        const int slot = i * NW + wv;
+        const int j = slot < G::GSLOTS ? slot * 64 + ln : G::NG;  // past the last slot: idle (dummy load)
+        const int gr = j / GQ, gq = j - gr * GQ;
+        const int x = x0 - PC + 4 * gq;
+        const bool live = j < G::NG && x >= 0 && x + 4 <= w;
+        const int y = reflect101(y0 - R + gr, h);
+        goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
+        gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
+    }
+    const int gjobs = __builtin_amdgcn_readfirstlane((G::GSLOTS - wv + NW - 1) / NW);  // this wave's gray rounds
+    uint32_t hsrc[G::HJ], hdst[G::HJ];
+    int hqv[G::HJ];
+#pragma unroll
+    for (int i = 0; i < G::HJ; i++) {
+        const int j = tid + NT * i;
+        const bool live = j < G::NH;
+        const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
+        hqv[i] = hq;
+        hsrc[i] = (uint32_t)(2 * hp * GQ + hq);
+        hdst[i] = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);
+    }
+    const bool edge_tile = x0 - PC < 0 || x0 + TS + PC > w;  // workgroup-uniform
+
+    double bg[RPWV];
+    ChainCtx cc;
+    {
+        const double* bgi = a.bg_in + (size_t)s * plane;
+        const int x = x0 + ln;
+        cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
+        cc.rowvalid = 0;
+        cc.keep_lo = cc.keep_hi = 0;
+        cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;
+#pragma unroll
+        for (int j = 0; j < RPWV; j++) {
+            const int y = y0 + RPWV * wv + j;
+            const bool in = x < w && y < h;
+            if (y < h) cc.rowvalid |= 1u << j;
+            bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
+            const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
+            if (j < 4) cc.keep_lo |= kb << (8 * j);
+            else cc.keep_hi |= kb << (8 * (j - 4));
+        }
+        const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
+        cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
+        cc.tbmask = x < w ? cc.rowvalid : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
+    asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
+
+    uint32_t cpk[G::NGR];
+#pragma unroll
+    for (int gi = 0; gi < G::NGR; gi++) cpk[gi] = tapw4<KC>(gi);
+    u32x3_t rw[G::GJ];
+    // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
+    // branch would make its registers a phi and the prefetch would be waited for at the back-edge
+    auto load = [&](size_t f) __attribute__((always_inline)) {
+        const uint8_t* src = a.src + f * fbytes;
+#pragma unroll
+        for (int i = 0; i < G::GJ; i++) __builtin_memcpy(&rw[i], src + goff[i], 12);
+    };
+    auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < G::GJ; i++) {
+            if (i >= gjobs) break;  // wave-uniform
+            gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z);
+        }
+    };
+    // one row of a tap job: the quad's 4 horizontal sums from WQ gray dwords (edge tiles: the
+    // mirrored quads rebuilt first)
+    auto hrow = [&](const uint32_t* row, int hq, uint32_t (&o)[4]) __attribute__((always_inline)) {
+        uint32_t qv[G::WQ];
+#pragma unroll
+        for (int d = 0; d < G::WQ; d++) qv[d] = row[hq + d];
+        if (edge_tile) {
+#pragma unroll
+            for (int d = 0; d < G::WQ; d++) {
+                const int c = x0 - PC + 4 * (hq + d);
+                if (c < 0 || c >= w) {
+                    const int sp = c < 0 ? -(c + 3) : 2 * w - 5 - c;  // first of the 4 mirrored source pixels
+                    const int qa = min(max((sp - (x0 - PC)) >> 2, 0), GQ - 2);
+                    qv[d] = __builtin_amdgcn_perm(row[qa + 1], row[qa], c < 0 ? 0x01020304u : 0x03040506u);
+                }
+            }
+        }
+        o[0] = htap<0, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
+        o[1] = htap<1, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
+        o[2] = htap<2, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
+        o[3] = htap<3, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
+    };
+    auto tap_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < G::HJ; i++) {
+            if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
+            const uint32_t* r0 = gb + (hsrc[i] - hqv[i]);
+            uint32_t u[4], v[4];
+            hrow(r0, hqv[i], u);
+            hrow(r0 + GQ, hqv[i], v);
+            *reinterpret_cast<uint4*>(Hb + hdst[i]) = make_uint4(u[0] | (v[0] << 16), u[1] | (v[1] << 16),
+                                                                  u[2] | (v[2] << 16), u[3] | (v[3] << 16));
+        }
+    };
+    const int t0 = a.t_begin, t1 = a.t_end;
+    load((size_t)t0 * S + s);
+    gray_stage(gray);
+    load((size_t)min(t0 + 1, t1 - 1) * S + s);
+    __syncthreads();  // atab, gray(t0)
+    tap_stage(gray, Hs);
+    if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
+    load((size_t)min(t0 + 2, t1 - 1) * S + s);
+    const int var0 = TAIL ? (int)(cc.vec == 0) : 0;
+    for (int t = t0; t < t1; t++) {
+        const int b = (t - t0) & 1;
+        const size_t f = (size_t)t * S + s;
+        lds_barrier();
+        uint32_t colbits = 0, fl = 0;
+        ChainCtx ccf = cc;
+        ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+        int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
+        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+        var = __builtin_amdgcn_readfirstlane(var);
+        asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+        const uint32_t* Hb = Hs + b * G::HBUF;
+        if (!TAIL || var == 0)
+            chain_rows_w<KC, KEEP, false>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+        else
+            chain_rows_w<KC, KEEP, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+        if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
+        gray_stage(gray + b * G::GBUF);
+        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        load((size_t)min(t + 3, t1 - 1) * S + s);
+    }
+    double* bgo = a.bg_out + (size_t)s * plane;
+    const int x = x0 + ln;
+#pragma unroll
+    for (int j = 0; j < RPWV; j++) {
+        const int y = y0 + RPWV * wv + j;
+        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+    }
+}
+
 }  // namespace px
 
 int pix_lds_bytes(int ksize) { return px::Geo(ksize >> 1).bytes; }
@@ -995,7 +1281,21 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
         else hipLaunchKernelGGL((px::k_pix5<false, false>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
         return hipGetLastError();
     }
-#define FM_PIX_LAUNCH(K, P, I)                                                                                  \
+#ifndef FM_PIXW
+#define FM_PIXW 1  // k = 21 steady state on k_pixw (0: k_pix<21>, the round-2 kernel)
+#endif
+    if (FM_PIXW && a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 &&
+        ((uintptr_t)a.src & 3) == 0) {
+        using G = px::PW<21>;
+        static_assert(G::bytes <= 64 * 1024, "k_pixw LDS");
+        const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
+        if (keep && tail) hipLaunchKernelGGL((px::k_pixw<21, true, true>), grid, dim3(px::NT), G::bytes, st, a);
+        else if (keep) hipLaunchKernelGGL((px::k_pixw<21, true, false>), grid, dim3(px::NT), G::bytes, st, a);
+        else if (tail) hipLaunchKernelGGL((px::k_pixw<21, false, true>), grid, dim3(px::NT), G::bytes, st, a);
+        else hipLaunchKernelGGL((px::k_pixw<21, false, false>), grid, dim3(px::NT), G::bytes, st, a);
+        return hipGetLastError();
+    }
+#define FM_PIX_LAUNCH(K, P, I)                                                                                \
     do {                                                                                                        \
         (void)hipFuncSetAttribute((const void*)px::k_pix<K, P, I>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
         hipLaunchKernelGGL((px::k_pix<K, P, I>), grid, dim3(px::NT), bytes, st, a);                             \

@@ -111,6 +111,15 @@ def test_4k_k21_masks_config5_geometry():
     run_pair(3840, 2160, 3840, blur_scale=183, T=1, n_batches=2, masks=masks, keep_planes=False)
 
 
+@pytest.mark.parametrize("W,H,S", [(200, 131, 2), (40, 30, 1), (1000, 70, 1), (320, 240, 3), (203, 90, 1)])
+def test_k21_wide_kernel_geometries(W, H, S):
+    """k = 21 steady state (k_pixw, no planes): a right tile 8 px wide, both REFLECT_101 edges in one tile
+    (w = 40), accumulateWeighted's scalar tail (h*w % 16 != 0), several streams with masks; w = 203 (not a
+    multiple of 4) takes k_pix<21>."""
+    masks = [((0, 0), (W // 5, H // 4)), ((W - 1, H - 1), (W // 2, H - 1), (W - 1, H // 2))]
+    run_pair(W, H, W, ksize=21, S=S, T=4, n_batches=2, masks=masks if S > 1 else None, keep_planes=False, start=90)
+
+
 def test_thresholds_and_alpha():
     run_pair(160, 120, 160, blur_scale=32, thresh=0, alpha=0.5)
     run_pair(160, 120, 160, blur_scale=32, thresh=-1, alpha=0.02)
