@@ -999,12 +999,14 @@ struct PW {
     static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
     static constexpr int NG = GH * GQ;             // gray jobs per frame
     static constexpr int GSLOTS = (NG + 63) / 64;
-    static constexpr int GJ = (GSLOTS + NW - 1) / NW;  // gray rounds per wave: slot i * NW + wave
+    static constexpr int gcnt(int w) { return (GSLOTS - w + NW - 1) / NW; }  // gray slots of wave w: i * NW + w
+    static constexpr int GJ = gcnt(0);             // gray rounds per wave
     static constexpr int NHP = GH / 2;             // H row pairs
     static constexpr int NH = NHP * (TS / 4);      // tap jobs
     static constexpr int HJ = (NH + NT - 1) / NT;
     static constexpr int HLASTW = (NH - (HJ - 1) * NT + 63) / 64;  // waves with a job in the last round
-    static constexpr int GBUF = NG + 64;           // + a pad slot per lane (idle gray jobs)
+    static constexpr int GS = GQ;                  // gray row stride in LDS (dwords)
+    static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
     static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
     static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
     static constexpr int NGR = (HI - LO + 4) / 4;  // dot4 groups per output
@@ -1083,8 +1085,11 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     flags = fl;
 }
 
+#ifndef FM_PIXW_WPE
+#define FM_PIXW_WPE 4  // 2 workgroups per CU (<= 128 VGPRs)
+#endif
 template <int KC, bool KEEP, bool TAIL>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pixw(FusedArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
     using G = PW<KC>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
@@ -1109,15 +1114,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #pragma unroll
     for (int i = 0; i < G::GJ; i++) {
         const int slot = i * NW + wv;
-        const int j = slot < G::GSLOTS ? slot * 64 + ln : G::NG;  // past the last slot: idle (dummy load)
+        const int j = (i < G::gcnt(wv) && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
         const int gr = j / GQ, gq = j - gr * GQ;
         const int x = x0 - PC + 4 * gq;
         const bool live = j < G::NG && x >= 0 && x + 4 <= w;
         const int y = reflect101(y0 - R + gr, h);
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
+        gdst[i] = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + ln);
     }
-    const int gjobs = __builtin_amdgcn_readfirstlane((G::GSLOTS - wv + NW - 1) / NW);  // this wave's gray rounds
+    const int gjobs = __builtin_amdgcn_readfirstlane(G::gcnt(wv));  // this wave's gray rounds
     uint32_t hsrc[G::HJ], hdst[G::HJ];
     int hqv[G::HJ];
 #pragma unroll
@@ -1126,7 +1131,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         const bool live = j < G::NH;
         const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
         hqv[i] = hq;
-        hsrc[i] = (uint32_t)(2 * hp * GQ + hq);
+        hsrc[i] = (uint32_t)(2 * hp * G::GS + hq);
         hdst[i] = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);
     }
     const bool edge_tile = x0 - PC < 0 || x0 + TS + PC > w;  // workgroup-uniform
@@ -1183,9 +1188,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #pragma unroll
         for (int d = 0; d < G::WQ; d++) qv[d] = row[hq + d];
         if (edge_tile) {
+            // laundered so the mirror indices are computed here, on the edge tiles only, and not
+            // hoisted out of the frame loop into ~30 registers every tile would carry
+            int hqe = hq, xe = x0 - PC;
+            asm volatile("" : "+v"(hqe), "+v"(xe));
 #pragma unroll
             for (int d = 0; d < G::WQ; d++) {
-                const int c = x0 - PC + 4 * (hq + d);
+                const int c = xe + 4 * (hqe + d);
                 if (c < 0 || c >= w) {
                     const int sp = c < 0 ? -(c + 3) : 2 * w - 5 - c;  // first of the 4 mirrored source pixels
                     const int qa = min(max((sp - (x0 - PC)) >> 2, 0), GQ - 2);
@@ -1205,7 +1214,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             const uint32_t* r0 = gb + (hsrc[i] - hqv[i]);
             uint32_t u[4], v[4];
             hrow(r0, hqv[i], u);
-            hrow(r0 + GQ, hqv[i], v);
+            hrow(r0 + G::GS, hqv[i], v);
             *reinterpret_cast<uint4*>(Hb + hdst[i]) = make_uint4(u[0] | (v[0] << 16), u[1] | (v[1] << 16),
                                                                   u[2] | (v[2] << 16), u[3] | (v[3] << 16));
         }
