@@ -621,8 +621,16 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
 // grid (GW, F); each wave labels candidates of the frame's list with a stride, in LDS
 // (LIGHT runs); a tile with more runs (a dense texture of small blobs) goes to the
 // heavy list
+#ifndef FM_CCL_NVGPR
+#define FM_CCL_NVGPR 0  // cap on k_tile_ccl's VGPRs (0: none), so more of its waves fit beside the pixel kernel's
+#endif
+#if FM_CCL_NVGPR
+#define FM_CCL_ATTR __attribute__((amdgpu_num_vgpr(FM_CCL_NVGPR)))
+#else
+#define FM_CCL_ATTR
+#endif
 template <bool DILATE>
-__global__ __launch_bounds__(64 * CW) void k_tile_ccl(FusedArgs a) {
+__global__ __launch_bounds__(64 * CW) FM_CCL_ATTR void k_tile_ccl(FusedArgs a) {
     __shared__ int par[CW][LIGHT], amin[CW][LIGHT], amax[CW][LIGHT], ay[CW][LIGHT];
     __shared__ uint8_t rx0[CW][LIGHT], rx1[CW][LIGHT], rf[CW][LIGHT];
     __shared__ uint16_t ord[CW][LIGHT];

@@ -634,6 +634,165 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Geometry shared by k_pix5 and k_pixw (below): H as row pairs, the vertical taps over
+// even-aligned pair windows (chain_rows_w), horizontal taps with shifted constants (HS).
+template <int K> constexpr int tap_c(int t) { return t < 0 || t >= K ? 0 : Taps<K>::c[t]; }
+template <int K> constexpr int tap_lo() {
+    int i = 0;
+    while (Taps<K>::c[i] == 0) i++;
+    return i;
+}
+template <int K> constexpr int tap_hi() {
+    int i = K - 1;
+    while (Taps<K>::c[i] == 0) i--;
+    return i;
+}
+
+template <int KC>
+struct PW {
+    static constexpr int R = KC / 2;
+    static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
+    static constexpr int GH = TS + 2 * R;          // gray rows (even)
+    static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
+    static constexpr int NG = GH * GQ;             // gray jobs per frame
+    static constexpr int GSLOTS = (NG + 63) / 64;
+    static constexpr int gcnt(int w) { return (GSLOTS - w + NW - 1) / NW; }  // gray slots of wave w: i * NW + w
+    static constexpr int GJ = gcnt(0);             // gray rounds per wave
+    static constexpr int NHP = GH / 2;             // H row pairs
+    static constexpr int NH = NHP * (TS / 4);      // tap jobs
+    static constexpr int HJ = (NH + NT - 1) / NT;
+    static constexpr int HLASTW = (NH - (HJ - 1) * NT + 63) / 64;  // waves with a job in the last round
+    static constexpr int GS = GQ;                  // gray row stride in LDS (dwords)
+    static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
+    static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
+    static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
+    static constexpr int NGR = (HI - LO + 4) / 4;  // dot4 groups per output
+    static constexpr int OFF = PC - R;             // byte of output k's tap 0 in its job's window: OFF + k
+    static constexpr int WQ = (3 + OFF + LO + 4 * NGR - 1) / 4 + 1;  // gray dwords per row a tap job reads
+    // chain: output row j of a wave takes pairs p0(j) .. p0(j) + np(j) - 1 (relative to the wave's first pair)
+    static constexpr int p0(int j) { return (j + LO) >> 1; }
+    static constexpr int np(int j) { return (j + HI + 2 - 2 * p0(j)) / 2; }
+    static constexpr int np_max() {
+        int m = 0;
+        for (int j = 0; j < RPWV; j++) m = p0(j) + np(j) > m ? p0(j) + np(j) : m;
+        return m;
+    }
+    static constexpr int NP = np_max();            // pairs a wave's chain reads
+    static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
+};
+template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
+    uint32_t v = 0;
+    for (int b = 0; b < 4; b++) {
+        const int t = PW<KC>::LO + 4 * g + b;
+        if (t <= PW<KC>::HI) v |= (uint32_t)Taps<KC>::c[t] << (8 * b);
+    }
+    return v;
+}
+template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of output row j: taps (ft, ft + 1)
+    const int ft = 2 * (PW<KC>::p0(j) + i) - j;
+    return (uint32_t)tap_c<KC>(ft) | (uint32_t)tap_c<KC>(ft + 1) << 16;
+}
+
+// chain_rows over H row pairs with even-aligned pair windows: output row j's window starts on an
+// even H row, absorbing a zero tap (outside the kernel, or one of OpenCV's zero end taps) on the
+// side the row parity needs, so no pair is rebuilt with v_alignbit
+template <int KC, bool KEEP, bool TAIL>
+__device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
+                                             int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
+                                             uint32_t& flags) {
+    using G = PW<KC>;
+    uint32_t P[G::NP];
+    const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
+#pragma unroll
+    for (int i = 0; i < G::NP; i++) P[i] = col[i * TS];
+    const int w = a.w;
+    const double beta = a.beta;
+    const int thr = min(max(a.thresh, -1), 255);
+    const uint32_t bias = (uint32_t)(255 - thr);
+    uint32_t tb = 0;
+    static_for<RPWV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        uint32_t acc = 32768u;
+        static_for<G::np(j)>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, P[G::p0(j) + i]),
+                                         __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
+        });
+        if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
+        const uint32_t blur = acc >> 16;
+        const double b = bg[j];
+        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
+        const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
+        tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
+        const double bl = atab[blur];
+        double nb = __fma_rn(b, beta, bl);
+        if (TAIL) {
+            const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
+            if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
+        }
+        bg[j] = nb;
+    });
+    tb &= cc.tbmask;
+    colbits = tb;
+    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
+    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
+    uint32_t fl = 0;
+    if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
+    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    flags = fl;
+}
+
+
+// Horizontal taps with the byte window folded into the constants: output k of a quad sums its
+// taps over window bytes [B0 + k, B0 + k + NTAPS) of the row's gray dwords; instead of shifting
+// the data (v_alignbyte per 4-byte group unless B0 + k is a multiple of 4), each aligned dword d
+// of that range takes a dot4 with the taps shifted to where its bytes fall (zeros outside).
+// k = 5: 8 dot4, no alignbyte per row of a quad (was 8 dot4 + 6 alignbyte).  The shifted tap words
+// live in VGPRs (VOP3P takes no literal).  (k = 21 would need 22 such words instead of 20 dot4 + 15
+// alignbyte: 128 VGPRs and spills in k_pixw, so it keeps the byte windows.)
+template <int K>
+struct HS {
+    static constexpr int LO = tap_lo<K>(), NTAPS = tap_hi<K>() - LO + 1, B0 = PW<K>::OFF + LO;
+    static constexpr int d0(int k) { return (B0 + k) / 4; }
+    static constexpr int nd(int k) { return (B0 + k + NTAPS - 1) / 4 - d0(k) + 1; }
+    static constexpr int base(int k) { return k == 0 ? 0 : base(k - 1) + nd(k - 1); }
+    static constexpr int NC = base(4);
+    static constexpr int NQ = (B0 + 3 + NTAPS - 1) / 4 + 1;  // dwords a row's 4 outputs read
+    static constexpr uint32_t c(int k, int i) {
+        uint32_t v = 0;
+        const int d = d0(k) + i;
+        for (int b = 0; b < 4; b++) {
+            const int t = 4 * d + b - B0 - k;
+            if (t >= 0 && t < NTAPS) v |= (uint32_t)Taps<K>::c[LO + t] << (8 * b);
+        }
+        return v;
+    }
+};
+template <int K>
+__device__ __forceinline__ void hs_consts(uint32_t (&cs)[HS<K>::NC]) {
+    static_for<4>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        static_for<HS<K>::nd(k)>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            cs[HS<K>::base(k) + i] = HS<K>::c(k, i);
+        });
+    });
+#pragma unroll
+    for (int i = 0; i < HS<K>::NC; i++) asm volatile("" : "+v"(cs[i]));  // kept in VGPRs
+}
+template <int K, int k, int N>
+__device__ __forceinline__ uint32_t hs_tap(const uint32_t (&q)[N], const uint32_t (&cs)[HS<K>::NC]) {
+    static_assert(HS<K>::d0(k) + HS<K>::nd(k) <= N, "window dwords");
+    uint32_t acc = 0;
+    static_for<HS<K>::nd(k)>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        acc = __builtin_amdgcn_udot4(q[HS<K>::d0(k) + i], cs[HS<K>::base(k) + i], acc, false);
+    });
+    return acc;
+}
 
 // ---------------------------------------------------------------------------
 // k_pix5: the 5x5 steady-state chain (the bench configuration, and every k = 5
@@ -801,9 +960,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
     asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
 
+#ifndef FM_HSHIFT
+#define FM_HSHIFT 1  // horizontal taps with shifted constants (HS) instead of v_alignbyte windows
+#endif
+#ifndef FM_P5_EVENP
+#define FM_P5_EVENP 1  // k_pix5's chain on even-aligned pair windows (chain_rows_w)
+#endif
     uint32_t cpk[2];
     cpk[0] = tap4<KC>(0);
     cpk[1] = tap4<KC>(1);
+    uint32_t hcs[HS<KC>::NC];
+    if (FM_HSHIFT) hs_consts<KC>(hcs);
     P5Raw rw;
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
@@ -835,10 +1002,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
                 if (hfix[i] & 4) qv[2] = __builtin_amdgcn_perm(qv[1], qv[1], 0x00000102u);
             }
             // outputs x0+4q+k, k = 0..3: taps over gray columns x0+4q+k-2 .. +2 = bytes k+2 .. k+6 of qv
-            const uint32_t h0 = htap<0, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h1 = htap<1, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h2 = htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h3 = htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h0 = FM_HSHIFT ? hs_tap<KC, 0>(qv, hcs) : htap<0, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h1 = FM_HSHIFT ? hs_tap<KC, 1>(qv, hcs) : htap<1, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h2 = FM_HSHIFT ? hs_tap<KC, 2>(qv, hcs) : htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
+            const uint32_t h3 = FM_HSHIFT ? hs_tap<KC, 3>(qv, hcs) : htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
             if (FM_P5_HPAIR) {  // the next gray row, then both rows' sums as row pairs
                 uint32_t qw[4] = {gb[hsrc[i] + P5_GQ], gb[hsrc[i] + P5_GQ + 1], gb[hsrc[i] + P5_GQ + 2], 0u};
                 if (edge_tile) {
@@ -846,10 +1013,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
                     if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
                     if (hfix[i] & 4) qw[2] = __builtin_amdgcn_perm(qw[1], qw[1], 0x00000102u);
                 }
-                const uint32_t k0 = htap<0, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k1 = htap<1, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k2 = htap<2, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k3 = htap<3, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k0 = FM_HSHIFT ? hs_tap<KC, 0>(qw, hcs) : htap<0, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k1 = FM_HSHIFT ? hs_tap<KC, 1>(qw, hcs) : htap<1, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k2 = FM_HSHIFT ? hs_tap<KC, 2>(qw, hcs) : htap<2, 2, 2, 0, 4>(qw, cpk, 0u);
+                const uint32_t k3 = FM_HSHIFT ? hs_tap<KC, 3>(qw, hcs) : htap<3, 2, 2, 0, 4>(qw, cpk, 0u);
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
                     make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
             } else {
@@ -914,12 +1081,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         // chain_rows reads H as row pairs (FM_P5_HPAIR) or as [row][RSH = 64] u16
         const uint16_t* Hb = Hs + b * P5_HBUF;
         if (!(skip & 2)) {
-            if (!TAIL || var == 0)
+            if (FM_P5_EVENP && FM_P5_HPAIR) {
+                const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hb);
+                if (!TAIL || var == 0)
+                    chain_rows_w<KC, KEEP, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                else
+                    chain_rows_w<KC, KEEP, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            } else if (!TAIL || var == 0) {
                 chain_rows<KC, false, false, KEEP, false, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
                                                                          colbits, fl);
-            else
+            } else {
                 chain_rows<KC, false, false, KEEP, true, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
                                                                         colbits, fl);
+            }
         }
         P5_PH(ph1);
         if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
@@ -979,112 +1153,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 // two edge tiles of a tile row the tap jobs rebuild them from the mirrored inside quads (one
 // v_perm of two gray dwords: quad at column c < 0 holds gray(-c .. -c-3), at c >= w gray(2w-2-c ..)).
 // Rows: reflect101 source rows, as k_pix5.  Needs w % 4 == 0 and w >= 2 * PC + 8.
-template <int K> constexpr int tap_c(int t) { return t < 0 || t >= K ? 0 : Taps<K>::c[t]; }
-template <int K> constexpr int tap_lo() {
-    int i = 0;
-    while (Taps<K>::c[i] == 0) i++;
-    return i;
-}
-template <int K> constexpr int tap_hi() {
-    int i = K - 1;
-    while (Taps<K>::c[i] == 0) i--;
-    return i;
-}
-
-template <int KC>
-struct PW {
-    static constexpr int R = KC / 2;
-    static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
-    static constexpr int GH = TS + 2 * R;          // gray rows (even)
-    static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
-    static constexpr int NG = GH * GQ;             // gray jobs per frame
-    static constexpr int GSLOTS = (NG + 63) / 64;
-    static constexpr int gcnt(int w) { return (GSLOTS - w + NW - 1) / NW; }  // gray slots of wave w: i * NW + w
-    static constexpr int GJ = gcnt(0);             // gray rounds per wave
-    static constexpr int NHP = GH / 2;             // H row pairs
-    static constexpr int NH = NHP * (TS / 4);      // tap jobs
-    static constexpr int HJ = (NH + NT - 1) / NT;
-    static constexpr int HLASTW = (NH - (HJ - 1) * NT + 63) / 64;  // waves with a job in the last round
-    static constexpr int GS = GQ;                  // gray row stride in LDS (dwords)
-    static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
-    static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
-    static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
-    static constexpr int NGR = (HI - LO + 4) / 4;  // dot4 groups per output
-    static constexpr int OFF = PC - R;             // byte of output k's tap 0 in its job's window: OFF + k
-    static constexpr int WQ = (3 + OFF + LO + 4 * NGR - 1) / 4 + 1;  // gray dwords per row a tap job reads
-    // chain: output row j of a wave takes pairs p0(j) .. p0(j) + np(j) - 1 (relative to the wave's first pair)
-    static constexpr int p0(int j) { return (j + LO) >> 1; }
-    static constexpr int np(int j) { return (j + HI + 2 - 2 * p0(j)) / 2; }
-    static constexpr int np_max() {
-        int m = 0;
-        for (int j = 0; j < RPWV; j++) m = p0(j) + np(j) > m ? p0(j) + np(j) : m;
-        return m;
-    }
-    static constexpr int NP = np_max();            // pairs a wave's chain reads
-    static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
-};
-template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
-    uint32_t v = 0;
-    for (int b = 0; b < 4; b++) {
-        const int t = PW<KC>::LO + 4 * g + b;
-        if (t <= PW<KC>::HI) v |= (uint32_t)Taps<KC>::c[t] << (8 * b);
-    }
-    return v;
-}
-template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of output row j: taps (ft, ft + 1)
-    const int ft = 2 * (PW<KC>::p0(j) + i) - j;
-    return (uint32_t)tap_c<KC>(ft) | (uint32_t)tap_c<KC>(ft + 1) << 16;
-}
-
-// chain_rows for k_pixw: H as row pairs, even-aligned pair windows (no alignbit)
-template <int KC, bool KEEP, bool TAIL>
-__device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
-                                             int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
-                                             uint32_t& flags) {
-    using G = PW<KC>;
-    uint32_t P[G::NP];
-    const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
-#pragma unroll
-    for (int i = 0; i < G::NP; i++) P[i] = col[i * TS];
-    const int w = a.w;
-    const double beta = a.beta;
-    const int thr = min(max(a.thresh, -1), 255);
-    const uint32_t bias = (uint32_t)(255 - thr);
-    uint32_t tb = 0;
-    static_for<RPWV>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        uint32_t acc = 32768u;
-        static_for<G::np(j)>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, P[G::p0(j) + i]),
-                                         __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
-        });
-        if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
-        const uint32_t blur = acc >> 16;
-        const double b = bg[j];
-        const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
-        const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
-        tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
-        const double bl = atab[blur];
-        double nb = __fma_rn(b, beta, bl);
-        if (TAIL) {
-            const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
-            if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
-        }
-        bg[j] = nb;
-    });
-    tb &= cc.tbmask;
-    colbits = tb;
-    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
-    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
-    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
-    uint32_t fl = 0;
-    if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
-    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
-    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
-    flags = fl;
-}
-
 #ifndef FM_PIXW_WPE
 #define FM_PIXW_WPE 4  // 2 workgroups per CU (<= 128 VGPRs)
 #endif
