@@ -183,14 +183,29 @@ __device__ __forceinline__ int16_t* block_ptr(int16_t* coef, const JpegGeom& g, 
 // WRITE: the entry is exact, cnt = blocks started before it in the segment and dc0..dc2 = the DC
 // predictors; each value is stored at its zigzag position of its block in the (zeroed) coefficient
 // buffer; decoding stops once the segment's `total` blocks are complete.
+// WRITE also records, per block, which 16-B pieces (8 zigzag positions each) hold a non-zero value:
+// msk[block] bit r, so that k_jpeg_idct loads only those.  A block decoded whole by this lane gets a
+// plain store; the parts of a block split between two chunks are ORed in atomically (k_jpeg_idct
+// zeroes every mask it reads, so the OR starts from 0).
 template <bool WRITE>
 __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mark, uint32_t end, const HuffDev* T, int bpm, int& cnt, int& dc0, int& dc1, int& dc2, uint32_t& p_in,
-                                            int& uk_in, int total, const JpegGeom& g, const Seg& sg, int16_t* coef) {
+                                            int& uk_in, int total, const JpegGeom& g, const Seg& sg, int16_t* coef,
+                                            uint32_t* msk) {
     int u = uk >> 6, k = uk & 63;
     bool marked = WRITE;
     // (corrupt data can give counts past the segment's blocks: nothing is stored for those)
     bool wr = WRITE && k && cnt >= 1 && cnt <= total;
     int16_t* blk = wr ? block_ptr(coef, g, sg, bpm, cnt - 1) : coef;
+    uint32_t bm = 0;      // WRITE: pieces of the current block this lane stored into
+    bool whole = false;   // WRITE: the current block started in this lane
+    auto flush = [&](bool complete) __attribute__((always_inline)) {
+        if (WRITE && wr && bm) {
+            uint32_t* mp = msk + ((blk - coef) >> 6);
+            if (complete && whole) *mp = bm;
+            else atomicOr(mp, bm);
+        }
+        bm = 0;
+    };
     while (true) {
         if (!WRITE && !marked && br.pos >= mark) {
             marked = true;
@@ -233,18 +248,25 @@ __device__ __forceinline__ void run_symbols(BitReader& br, int& uk, uint32_t mar
             dc2 = ci == 2 ? pred : dc2;
             v = pred;
             if (WRITE) {
-                wr = cnt >= 0;
+                wr = cnt >= 0 && cnt < total;
                 blk = wr ? block_ptr(coef, g, sg, bpm, cnt) : coef;
+                whole = true;
             }
             cnt++;
         }
-        if (WRITE && wr && val && v) blk[min(k + r, 63)] = (int16_t)v;
+        if (WRITE && wr && val && v) {
+            const int pos = min(k + r, 63);
+            blk[pos] = (int16_t)v;
+            bm |= 1u << (pos >> 3);
+        }
         k = (!val && r != 15) ? 64 : k + r + 1;
         if (k >= 64) {
+            if (WRITE) flush(true);
             k = 0;
             u = u + 1 == bpm ? 0 : u + 1;
         }
     }
+    if (WRITE) flush(false);  // a block this chunk ends inside (its rest is the next lane's)
     if (!WRITE && !marked) {  // a symbol jumped over the whole chunk: it starts (and ends) here
         p_in = br.pos;
         uk_in = u * 64 + k;
@@ -276,7 +298,8 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
                                                                 int nchunks,
                                                                 const HuffDev* __restrict__ tabs, JpegGeom g, int CB, int OV,
                                                                 TileState* __restrict__ ts, uint32_t* __restrict__ tile_ctr,
-                                                                int16_t* __restrict__ coef, uint64_t* __restrict__ stamps) {
+                                                                int16_t* __restrict__ coef, uint32_t* __restrict__ msk,
+                                                                uint64_t* __restrict__ stamps) {
     __shared__ HuffDev T[4];
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(tabs);
@@ -367,7 +390,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
         if (go) {
             br.init(stream, sg.off, (uint32_t)(want >> 32), send);
             int uk = (int)(uint32_t)want;
-            run_symbols<false>(br, uk, mark, ce, T, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, 0, g, sg, coef);
+            run_symbols<false>(br, uk, mark, ce, T, bpm, cnt, dc0, dc1, dc2, p_in, uk_in, 0, g, sg, coef, nullptr);
             st_in = pack_state(p_in, uk_in);
             st_out = pack_state(br.pos, uk);
         }
@@ -423,7 +446,7 @@ __global__ __launch_bounds__(64 * kHuffWaves) void k_jpeg_huff(const uint8_t* __
     int wcnt = ic - cnt, w0 = id0 - dc0, w1 = id1 - dc1, w2 = id2 - dc2;
     br.init(stream, sg.off, p_in, send);
     int wuk = uk_in;
-    run_symbols<true>(br, wuk, 0, ce, T, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef);
+    run_symbols<true>(br, wuk, 0, ce, T, bpm, wcnt, w0, w1, w2, p_in, uk_in, sg.nmcu * bpm, g, sg, coef, msk);
     JP_STAMP(4);
 #undef JP_STAMP
 }
@@ -481,17 +504,28 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 // in LDS, runs column r of pass 1, then row r of pass 2
 constexpr int kIdctGroups = 4;  // groups of 32 blocks per workgroup (their loads issued together)
 
-__global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, const uint16_t* __restrict__ qt, JpegGeom g,
-                                                    int nblocks, uint8_t* __restrict__ planes) {
+__global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, uint32_t* __restrict__ msk,
+                                                    const uint16_t* __restrict__ qt, JpegGeom g, int nblocks,
+                                                    uint8_t* __restrict__ planes) {
     __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
     const int b0 = blockIdx.x * (32 * kIdctGroups) + lb;
+    uint32_t bm[kIdctGroups];
+#pragma unroll
+    for (int G = 0; G < kIdctGroups; G++) {
+        const int b = b0 + 32 * G;
+        bm[G] = b < nblocks ? msk[b] : 0u;
+    }
+    // only the 16-B pieces the Huffman pass stored into (the rest of the block is zero)
     uint4 raw[kIdctGroups];
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
         const int b = b0 + 32 * G;
-        raw[G] = b < nblocks ? reinterpret_cast<const uint4*>(coef + (size_t)b * 64)[r] : make_uint4(0, 0, 0, 0);
+        raw[G] = ((bm[G] >> r) & 1) ? reinterpret_cast<const uint4*>(coef + (size_t)b * 64)[r] : make_uint4(0, 0, 0, 0);
     }
+#pragma unroll
+    for (int G = 0; G < kIdctGroups; G++)
+        if (r == 0 && bm[G]) msk[b0 + 32 * G] = 0u;  // for the next call's stores
     const uint2 nat = c_zz8[r];
     const int fbk = (int)g.frame_blocks;
 #pragma unroll
@@ -511,7 +545,7 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, c
             const uint4 rw = raw[G];
             // leave the block zeroed for the next call's sparse coefficient stores (only the 16-B
             // pieces that hold something: most of a typical block is zero already)
-            if (live && (rw.x | rw.y | rw.z | rw.w)) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
+            if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
             const uint32_t w4[4] = {rw.x, rw.y, rw.z, rw.w};
             if (G) __syncthreads();  // the previous group's pass 2 has read ws
 #pragma unroll
@@ -867,6 +901,7 @@ struct fm_mjpeg {
     int tabs_cap = 0;
     uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
     int16_t* d_coef = nullptr;         // [max_frames][frame_blocks][64]
+    uint32_t* d_msk = nullptr;         // [max_frames][frame_blocks]: non-zero 16-B pieces of each block
     uint8_t* d_planes = nullptr;       // [max_frames][frame_plane]
     uint8_t* d_out = nullptr;          // device BGR when the caller wants host output
     // pinned host staging, two sets used in turn: a call refills the set whose uploads (two calls
@@ -1194,6 +1229,8 @@ int setup_geometry(fm_mjpeg* d, const ParsedJpeg& J) {
     const size_t nb = (size_t)d->max_frames * blocks * 64;
     JHIP(d, hipMalloc((void**)&d->d_coef, nb * sizeof(int16_t)));
     JHIP(d, hipMemsetAsync(d->d_coef, 0, nb * sizeof(int16_t), d->st));
+    JHIP(d, hipMalloc((void**)&d->d_msk, (size_t)d->max_frames * blocks * sizeof(uint32_t)));
+    JHIP(d, hipMemsetAsync(d->d_msk, 0, (size_t)d->max_frames * blocks * sizeof(uint32_t), d->st));
     JHIP(d, hipMalloc((void**)&d->d_planes, (size_t)d->max_frames * g.frame_plane));
     JHIP(d, hipMalloc((void**)&d->d_qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t)));
     for (auto& H : d->hs)
@@ -1234,7 +1271,7 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
 void fm_mjpeg_destroy(fm_mjpeg* d) {
     if (!d) return;
     if (d->st) (void)hipStreamSynchronize(d->st);
-    for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef,
+    for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef, (void*)d->d_msk,
                     (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts, (void*)d->d_stamps})
         if (p) (void)hipFree(p);
     for (auto& H : d->hs) {
@@ -1491,13 +1528,13 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
                            d->d_stream, (uint32_t)w, d->d_segs + run_seg[r], run_seg[r + 1] - run_seg[r],
                            d->d_chunk0 + run_seg[r], (int)run_chunk[r], (int)run_end[r], d->d_tabs + 4 * r, gr,
                            d->CB, d->OV, d->d_ts + run_tile[r], reinterpret_cast<uint32_t*>(d->d_ts + ntiles + r),
-                           d->d_coef, d->d_stamps ? d->d_stamps + 6 * run_tile[r] : nullptr);
+                           d->d_coef, d->d_msk, d->d_stamps ? d->d_stamps + 6 * run_tile[r] : nullptr);
     }
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
     if (nb >= INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "too many coefficient blocks in one call");
     hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
-                       d->d_coef, d->d_qt, d->g, (int)nb, d->d_planes);
+                       d->d_coef, d->d_msk, d->d_qt, d->g, (int)nb, d->d_planes);
     JHIP(d, hipGetLastError());
     // colour bands: as many rows as keep the staging within 48 KB of LDS
     int rb = 16;

@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"k_pix": "pix", "k_pix5": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit", "k_fold": "fold", "k_emit": "emit",
+SHORT = {"k_pix": "pix", "k_pix5": "pix", "k_pixw": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit", "k_fold": "fold", "k_emit": "emit",
          "k_regions": "regions", "k_resize_area": "resize_area", "k_pixel": "pixel"}
 
 
