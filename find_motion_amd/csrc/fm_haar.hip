@@ -57,7 +57,8 @@ struct Geo {  // per scale, copied to the device as kernel arguments
     int ioff[MAXSC];           // integral offset (elements) within one image
     int woff[MAXSC];           // window offset within one image
     int xtab[MAXSC], ytab[MAXSC];  // offsets into the tap table
-    int P, I, NW;              // per image totals
+    int toff[MAXSC], tnx[MAXSC];   // k_hdetect: first window tile of each scale, tiles per tile row
+    int P, I, NW, NT;          // per image totals (NT: window tiles)
 };
 
 __device__ __forceinline__ int find_scale(const int* off, int n, int r) {
@@ -243,7 +244,25 @@ __device__ __forceinline__ int run_stages(const CascadeDev& c, const Win& w, int
         const int t0 = __builtin_amdgcn_readfirstlane(c.stage_first[si]);
         const int nt = __builtin_amdgcn_readfirstlane(c.stage_ntrees[si]);
         double sum = 0.;
-        if (c.stumps) {
+#ifndef FM_HAAR_PF
+#define FM_HAAR_PF 1
+#endif
+        if (c.stumps && FM_HAAR_PF) {
+            // the next stump's node and feature records are loaded while this one is evaluated (scalar
+            // loads: every lane evaluates the same stump); leaves are summed in stump order as OpenCV does
+            Node n = c.nodes[t0];
+            Feat fe = c.feats[__builtin_amdgcn_readfirstlane(n.feat)];
+            for (int t = t0; t < t0 + nt; ++t) {
+                const int tn = t + 1 < t0 + nt ? t + 1 : t;
+                const Node nn = c.nodes[tn];
+                const Feat fn = c.feats[__builtin_amdgcn_readfirstlane(nn.feat)];
+                const float v = feature(fe, w);
+                const int idx = v < n.thr ? n.left : n.right;
+                sum += (double)c.leaves[2 * t - idx];
+                n = nn;
+                fe = fn;
+            }
+        } else if (c.stumps) {
             for (int t = t0; t < t0 + nt; ++t) {
                 const Node n = c.nodes[t];  // stump t = node t, leaves 2t, 2t + 1
                 const float v = feature(c.feats[__builtin_amdgcn_readfirstlane(n.feat)], w);
@@ -301,6 +320,96 @@ __global__ __launch_bounds__(256) void k_heval_tail(const uint32_t* __restrict__
         Win w;
         set_window(S, Q, T, c, g, i, w);  // a survivor's window is not flat
         res[i] = run_stages(c, w, split, c.n_stages) >= 0 ? -1 : 1;
+    }
+}
+
+// The whole window sweep for one tile of TW x TH windows of one scale of one image: the tile's
+// integral patch (and the tilted one) is staged in LDS once, so every feature's corner reads are
+// LDS reads instead of gathers from L2; every window runs the first `split` stages (one thread
+// each), the survivors are compacted to the workgroup's first threads and run the rest in dense
+// waves.  Same windows, same arithmetic, same res values as k_heval + k_heval_tail.
+constexpr int TW = 16, TH = 16;  // windows per tile (256 threads)
+
+__global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
+                                                     const uint32_t* __restrict__ T, int8_t* __restrict__ res, int split,
+                                                     CascadeDev c, Geo g, int pw_max) {
+    extern __shared__ uint32_t patch[];  // S patch [ph][pw], then T patch (tilted cascades)
+    __shared__ int s_live[TW * TH];
+    __shared__ int s_n;
+    const int img = blockIdx.y;
+    const int s = find_scale(g.toff, g.n, blockIdx.x);
+    const int tile = blockIdx.x - g.toff[s];
+    const int tyi = tile / g.tnx[s], txi = tile - tyi * g.tnx[s];
+    const int step = g.step[s], st = g.sw[s] + 1, ih = g.sh[s] + 1;
+    const int gx0 = txi * TW, gy0 = tyi * TH;
+    const int px0 = gx0 * step, py0 = gy0 * step;
+    const int pw = min((TW - 1) * step + c.win_w + 1, st - px0), ph = min((TH - 1) * step + c.win_h + 1, ih - py0);
+    const size_t base = (size_t)img * g.I + g.ioff[s];
+    const int tid = threadIdx.x;
+    if (tid == 0) s_n = 0;
+    for (int i = tid; i < pw * ph; i += TW * TH) {
+        const int y = i / pw, x = i - y * pw;
+        const size_t gi = base + (size_t)(py0 + y) * st + px0 + x;
+        patch[y * pw_max + x] = S[gi];
+        if (c.has_tilted) patch[ph * pw_max + y * pw_max + x] = T[gi];
+    }
+    __syncthreads();
+    const int gx = gx0 + (tid % TW), gy = gy0 + tid / TW;
+    const bool in = gx < g.gw[s] && gy < g.gh[s];
+    const long long wi = (long long)img * g.NW + g.woff[s] + (long long)gy * g.gw[s] + gx;
+    Win w;
+    w.st = pw_max;
+    w.x = (gx - gx0) * step;
+    w.y = (gy - gy0) * step;
+    w.S = patch;
+    w.T = c.has_tilted ? patch + ph * pw_max : nullptr;
+    int8_t out = -1;
+    bool live = false;
+    if (in) {
+        // HaarEvaluator::setWindow: sum from the patch, squared sum from Q
+        const int nr[4] = {1, 1, c.win_w - 2, c.win_h - 2};
+        const int32_t valsum = rsum(w.S, w.st, w.x, w.y, nr, false);
+        const int gxp = gx * step, gyp = gy * step;
+        const uint32_t valsq = (uint32_t)rsum(Q + base, st, gxp, gyp, nr, false);
+        const double area = (double)((c.win_w - 2) * (c.win_h - 2));
+        double nf = area * (double)valsq - (double)valsum * (double)valsum;
+        bool ok = nf > 0.;
+        if (ok) {
+            nf = sqrt(nf);
+            w.vnf = (float)(1. / nf);
+            ok = area * (double)w.vnf < 1e-1;
+        }
+        if (ok) {
+            const int f = run_stages(c, w, 0, split);
+            if (f >= 0) out = f == 0 ? 0 : -1;
+            else if (split < c.n_stages) live = true;
+            else out = 1;
+        }
+        if (!live) res[wi] = out;
+    }
+    __shared__ float s_vnf[TW * TH];
+    if (live) {
+        s_live[atomicAdd(&s_n, 1)] = tid;
+        s_vnf[tid] = w.vnf;
+    }
+    __syncthreads();
+    const int n = s_n;
+    // survivors spread over the workgroup's waves (survivor k -> wave k % 4): a few deep windows
+    // finish in parallel instead of one after another in one wave's lanes
+    constexpr int NWV = TW * TH / 64;
+    const int k = (tid & 63) * NWV + (tid >> 6);
+    if (k < n) {
+        const int t2 = s_live[k];
+        const int gx2 = gx0 + (t2 % TW), gy2 = gy0 + t2 / TW;
+        Win v;
+        v.st = pw_max;
+        v.x = (gx2 - gx0) * step;
+        v.y = (gy2 - gy0) * step;
+        v.S = patch;
+        v.T = w.T;
+        v.vnf = s_vnf[t2];
+        const long long wi2 = (long long)img * g.NW + g.woff[s] + (long long)gy2 * g.gw[s] + gx2;
+        res[wi2] = run_stages(c, v, split, c.n_stages) >= 0 ? -1 : 1;
     }
 }
 
@@ -574,11 +683,14 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         g.gh[s] = (ylim[s] + g.step[s] - 1) / g.step[s];
         if (g.gw[s] == 0) g.gh[s] = 0;
     }
-    g.P = g.I = g.NW = 0;
+    g.P = g.I = g.NW = g.NT = 0;
     for (int s = 0; s < g.n; ++s) {
         g.poff[s] = g.P;
         g.ioff[s] = g.I;
         g.woff[s] = g.NW;
+        g.toff[s] = g.NT;
+        g.tnx[s] = (g.gw[s] + TW - 1) / TW;
+        g.NT += g.tnx[s] * ((g.gh[s] + TH - 1) / TH);
         g.P += g.sw[s] * g.sh[s];
         g.I += (g.sw[s] + 1) * (g.sh[s] + 1);
         g.NW += g.gw[s] * g.gh[s];
@@ -628,6 +740,17 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         static const int split_env = FM_HAAR_SPLIT_DEFAULT;
 #endif
         const int split = std::max(1, std::min(split_env, h->n_stages));
+#ifndef FM_HAAR_TILES
+#define FM_HAAR_TILES 1  // k_hdetect (LDS integral patches) instead of k_heval + k_heval_tail
+#endif
+        const int pw_max = (TW - 1) * 2 + h->win_w + 1, ph_max = (TH - 1) * 2 + h->win_h + 1;
+        const size_t lds = (size_t)pw_max * ph_max * 4 * (h->has_tilted ? 2 : 1);
+        if (FM_HAAR_TILES && lds <= 56 * 1024) {
+            if (g.NT > 0)
+                hipLaunchKernelGGL(k_hdetect, dim3((unsigned)g.NT, (unsigned)n), dim3(TW * TH), lds, h->stream, h->d_S, h->d_Q,
+                                   h->d_T, h->d_res, split, h->cd, g, pw_max);
+            goto swept;
+        }
         if ((rc = grow(h, &h->d_live, h->cap_live, (size_t)nw))) return rc;
         if (!h->d_nlive) HH(h, hipMalloc((void**)&h->d_nlive, sizeof(int)));
         HH(h, hipMemsetAsync(h->d_nlive, 0, sizeof(int), h->stream));
@@ -640,6 +763,7 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
             k_heval_tail<<<tb, 256, 0, h->stream>>>(h->d_S, h->d_Q, h->d_T, h->d_res, h->d_live, h->d_nlive, split,
                                                       h->cd, g, n);
     }
+swept:
     HH(h, hipGetLastError());
     HH(h, hipEventRecord(h->e1, h->stream));
     h->h_res.resize((size_t)nw);
