@@ -504,12 +504,13 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 // in LDS, runs column r of pass 1, then row r of pass 2
 constexpr int kIdctGroups = 4;  // groups of 32 blocks per workgroup (their loads issued together)
 
+// blocks [b_begin, nblocks) of the call (all frames' blocks in order)
 __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, uint32_t* __restrict__ msk,
-                                                    const uint16_t* __restrict__ qt, JpegGeom g, int nblocks,
+                                                    const uint16_t* __restrict__ qt, JpegGeom g, int b_begin, int nblocks,
                                                     uint8_t* __restrict__ planes) {
     __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
-    const int b0 = blockIdx.x * (32 * kIdctGroups) + lb;
+    const int b0 = b_begin + blockIdx.x * (32 * kIdctGroups) + lb;
     uint32_t bm[kIdctGroups];
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
@@ -584,7 +585,10 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, u
 #pragma unroll
             for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
         }
-        if (live) {
+#ifndef FM_JP_ABL
+#define FM_JP_ABL 0  // timing ablations only (results invalid): 1 IDCT without plane stores, 2 colour without plane loads
+#endif
+        if (live && !(FM_JP_ABL & 1)) {
             const int pw = c.bw * 8;
             uint8_t* row = planes + (size_t)frame * g.frame_plane + c.plane0 + (size_t)(by * 8 + r) * pw + (size_t)bx * 8;
             reinterpret_cast<uint2*>(row)[0] = make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24,
@@ -612,9 +616,9 @@ __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor
 // 2 h2v1 fancy upsampling, 3 h2v2 fancy upsampling (straight-line code for the common 4:2:2 / 4:2:0)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g, int rb,
-                                                     uint8_t* __restrict__ out) {
+                                                     uint8_t* __restrict__ out, int frame0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int y0 = blockIdx.x * rb, frame = blockIdx.y;
+    const int y0 = blockIdx.x * rb, frame = frame0 + blockIdx.y;
     const int y1 = min(y0 + rb, g.H);
     const uint8_t* fp = planes + (size_t)frame * g.frame_plane;
     const CompDev& cy = g.comp[0];
@@ -651,11 +655,11 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
             uint8_t* dst;
             if (i < nyw) {
                 const int r = i / yw, x8 = i - r * yw;
-                v = reinterpret_cast<const uint2*>(fp + cy.plane0 + (size_t)(y0 + r) * ypw)[x8];
+                v = (FM_JP_ABL & 2) ? make_uint2(i, r) : reinterpret_cast<const uint2*>(fp + cy.plane0 + (size_t)(y0 + r) * ypw)[x8];
                 dst = ys + r * wr + x8 * 8;
             } else {
                 const int q = i - nyw, comp = q / (nr * cw), rem = q - comp * nr * cw, r = rem / cw, x8 = rem - r * cw;
-                v = reinterpret_cast<const uint2*>(fp + g.comp[1 + comp].plane0 + (size_t)(r_lo + r) * cpw)[x8];
+                v = (FM_JP_ABL & 2) ? make_uint2(q, r) : reinterpret_cast<const uint2*>(fp + g.comp[1 + comp].plane0 + (size_t)(r_lo + r) * cpw)[x8];
                 dst = cs + (comp * nr + r) * cpw + x8 * 8;
             }
             *reinterpret_cast<uint2*>(dst) = v;
@@ -1533,9 +1537,6 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
     if (nb >= INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "too many coefficient blocks in one call");
-    hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
-                       d->d_coef, d->d_msk, d->d_qt, d->g, (int)nb, d->d_planes);
-    JHIP(d, hipGetLastError());
     // colour bands: as many rows as keep the staging within 48 KB of LDS
     int rb = 16;
     size_t lds = 0;
@@ -1553,11 +1554,15 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         const int dw = (g.W * g.comp[1].h + g.hmax - 1) / g.hmax;
         mode = (hf == 2 && dw > 2) ? (vf == 2 ? 3 : 2) : 1;
     }
-    const dim3 cgrid((unsigned)((g.H + rb - 1) / rb), (unsigned)n);
-    if (mode == 3) hipLaunchKernelGGL(k_jpeg_color<3>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
-    else if (mode == 2) hipLaunchKernelGGL(k_jpeg_color<2>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
-    else if (mode == 1) hipLaunchKernelGGL(k_jpeg_color<1>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
-    else hipLaunchKernelGGL(k_jpeg_color<0>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out);
+    {
+        hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
+                           d->d_coef, d->d_msk, d->d_qt, d->g, 0, (int)nb, d->d_planes);
+        const dim3 cgrid((unsigned)((g.H + rb - 1) / rb), (unsigned)n);
+        if (mode == 3) hipLaunchKernelGGL(k_jpeg_color<3>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
+        else if (mode == 2) hipLaunchKernelGGL(k_jpeg_color<2>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
+        else if (mode == 1) hipLaunchKernelGGL(k_jpeg_color<1>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
+        else hipLaunchKernelGGL(k_jpeg_color<0>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
+    }
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
     JHIP(d, hipEventRecord(d->last_ev, st));
