@@ -504,36 +504,38 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 // in LDS, runs column r of pass 1, then row r of pass 2
 constexpr int kIdctGroups = 4;  // groups of 32 blocks per workgroup (their loads issued together)
 
-// blocks [b_begin, nblocks) of the call (all frames' blocks in order)
+// nblocks blocks of the call: of each frame the blocks from number `skip` on (0: all of them; with
+// k_jpeg_color<., true> decoding the Y blocks itself, the chroma blocks only)
 __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, uint32_t* __restrict__ msk,
-                                                    const uint16_t* __restrict__ qt, JpegGeom g, int b_begin, int nblocks,
+                                                    const uint16_t* __restrict__ qt, JpegGeom g, int skip, int nblocks,
                                                     uint8_t* __restrict__ planes) {
     __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
-    const int b0 = b_begin + blockIdx.x * (32 * kIdctGroups) + lb;
+    const int b0 = blockIdx.x * (32 * kIdctGroups) + lb;
+    const int fbk = (int)g.frame_blocks, dbk = fbk - skip;
+    int fbs[kIdctGroups];  // the call-wide block numbers
     uint32_t bm[kIdctGroups];
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
         const int b = b0 + 32 * G;
-        bm[G] = b < nblocks ? msk[b] : 0u;
+        const int f = b / dbk;
+        fbs[G] = b < nblocks ? f * fbk + skip + (b - f * dbk) : 0;
+        bm[G] = b < nblocks ? msk[fbs[G]] : 0u;
     }
     // only the 16-B pieces the Huffman pass stored into (the rest of the block is zero)
     uint4 raw[kIdctGroups];
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
-        const int b = b0 + 32 * G;
-        raw[G] = ((bm[G] >> r) & 1) ? reinterpret_cast<const uint4*>(coef + (size_t)b * 64)[r] : make_uint4(0, 0, 0, 0);
+        raw[G] = ((bm[G] >> r) & 1) ? reinterpret_cast<const uint4*>(coef + (size_t)fbs[G] * 64)[r] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++)
-        if (r == 0 && bm[G]) msk[b0 + 32 * G] = 0u;  // for the next call's stores
+        if (r == 0 && bm[G]) msk[fbs[G]] = 0u;  // for the next call's stores
     const uint2 nat = c_zz8[r];
-    const int fbk = (int)g.frame_blocks;
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
-        const int b = b0 + 32 * G;
-        const bool live = b < nblocks;
-        const int fb = live ? b : 0;
+        const bool live = b0 + 32 * G < nblocks;
+        const int fb = fbs[G];
         const int frame = fb / fbk;
         const int rem = fb - frame * fbk;
         int ci = 0;
@@ -613,10 +615,19 @@ __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor
 // then row by row each thread converts 8 consecutive pixels (chroma upsampled from LDS,
 // ycc_rgb_convert) into a BGR row in LDS (two of them, alternating), stored with 16-byte stores.
 // MODE: 0 grayscale, 1 per-pixel chroma (1x1 chroma, or planes too narrow for the fancy filters),
-// 2 h2v1 fancy upsampling, 3 h2v2 fancy upsampling (straight-line code for the common 4:2:2 / 4:2:0)
-template <int MODE>
-__global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ planes, JpegGeom g, int rb,
-                                                     uint8_t* __restrict__ out, int frame0) {
+// 2 h2v1 fancy upsampling, 3 h2v2 fancy upsampling (straight-line code for the common 4:2:2 / 4:2:0).
+// FUSEY: the band's Y blocks (rb a multiple of 8) are dequantized and inverse-transformed here, straight
+// into the LDS rows, instead of going through the Y plane in HBM (k_jpeg_idct then does the chroma
+// blocks only): the plane store and reload were a third of the decoder's device time
+#ifndef FM_JP_COLOR_WPE
+#define FM_JP_COLOR_WPE 5  // five workgroups per CU: the LDS bound with the scratch over the chroma rows
+#endif
+// ys_off: LDS bytes before the Y rows (the two BGR rows unless the stores go direct); ws_off: FUSEY's
+// IDCT scratch, either in front of the Y rows or over the chroma rows (which are then staged after it)
+template <int MODE, bool FUSEY>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FM_JP_COLOR_WPE))) void k_jpeg_color(
+    const uint8_t* __restrict__ planes, JpegGeom g, int rb, int ys_off, int ws_off, uint8_t* __restrict__ out, int frame0,
+    int16_t* __restrict__ coef, uint32_t* __restrict__ msk, const uint16_t* __restrict__ qt) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int y0 = blockIdx.x * rb, frame = frame0 + blockIdx.y;
     const int y1 = min(y0 + rb, g.H);
@@ -625,8 +636,8 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
     const int ypw = cy.bw * 8;
     const int wr = (g.W + 7) & ~7;           // Y bytes staged per row
     const int orow_sz = (g.W * 3 + 15) & ~15;
-    uint8_t* orow = lds;                     // [2][orow_sz]
-    uint8_t* ys = lds + 2 * orow_sz;         // [rb][wr]
+    uint8_t* orow = lds;                     // [2][orow_sz] (and the IDCT scratch of FUSEY before them)
+    uint8_t* ys = lds + ys_off;              // [rb][wr]
     uint8_t* cs = ys + rb * wr;              // [2 comps][nr][cpw]
     constexpr bool color = MODE != 0;
     int hf = 1, vf = 1, dw = 0, dh = 0, cpw = 0, r_lo = 0, nr = 0;
@@ -647,8 +658,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
         }
         nr = r_hi - r_lo + 1;
     }
-    {   // stage: Y rows, then chroma rows (8-byte words)
-        const int yw = wr >> 3, nyw = (y1 - y0) * yw;
+    const bool ws_over_cs = FUSEY && ws_off >= ys_off;
+    auto stage = [&]() {  // Y rows (unless decoded below), then chroma rows (8-byte words)
+        const int yw = wr >> 3, nyw = FUSEY ? 0 : (y1 - y0) * yw;
         const int cw = cpw >> 3, ncw = 2 * nr * cw;
         for (int i = threadIdx.x; i < nyw + ncw; i += 256) {
             uint2 v;
@@ -664,10 +676,97 @@ __global__ __launch_bounds__(256) void k_jpeg_color(const uint8_t* __restrict__ 
             }
             *reinterpret_cast<uint2*>(dst) = v;
         }
+    };
+    if (!ws_over_cs) stage();
+    if constexpr (FUSEY) {
+        // Y block rows y0/8 .. (y1-1)/8, block columns 0 .. wr/8-1, as k_jpeg_idct does them (8 lanes per
+        // block), four groups of 32 blocks with their loads in flight together.  The 8 lanes of a block are
+        // one wave's: its scratch row ws[lb] needs wave-level ordering only.
+        int* ws = reinterpret_cast<int*>(lds + ws_off);  // [32][65], over rows not used yet
+        const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
+        const int nbx = wr >> 3, nyb = nbx * (((y1 - 1) >> 3) - (y0 >> 3) + 1);
+        const int64_t blk0 = (int64_t)frame * g.frame_blocks + cy.coef0 + (int64_t)(y0 >> 3) * cy.bw;
+        const uint16_t* q = qt + (size_t)frame * kMaxComp * 64;
+        int qv[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) qv[k] = (int)q[8 * k + r];
+        const uint2 nat = c_zz8[r];
+        for (int base = 0; base < nyb; base += 32 * kIdctGroups) {
+            int64_t bk[kIdctGroups];
+            uint32_t bm[kIdctGroups];
+            uint4 raw[kIdctGroups];
+#pragma unroll
+            for (int G = 0; G < kIdctGroups; G++) {
+                const int j = base + 32 * G + lb, jr = j / nbx;
+                bk[G] = blk0 + (int64_t)jr * cy.bw + (j - jr * nbx);
+                bm[G] = j < nyb ? msk[bk[G]] : 0u;
+            }
+#pragma unroll
+            for (int G = 0; G < kIdctGroups; G++)
+                raw[G] = ((bm[G] >> r) & 1) ? reinterpret_cast<const uint4*>(coef + bk[G] * 64)[r] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int G = 0; G < kIdctGroups; G++) {
+                if (r == 0 && bm[G]) msk[bk[G]] = 0u;  // for the next call's stores
+                if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + bk[G] * 64)[r] = make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int G = 0; G < kIdctGroups; G++) {
+                const int j = base + 32 * G + lb, jr = j / nbx;
+                if (base + 32 * G >= nyb) break;  // uniform over the workgroup
+                const uint32_t w4[4] = {raw[G].x, raw[G].y, raw[G].z, raw[G].w};
+                int* wb = ws + lb * 65;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
+                    wb[n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
+                }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                int v[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) v[k] = wb[8 * k + r] * qv[k];
+                if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
+#pragma unroll
+                    for (int k = 0; k < 8; k++) wb[8 * k + r] = v[0] * 4;
+                } else {
+                    int o[8];
+                    idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+#pragma unroll
+                    for (int k = 0; k < 8; k++) wb[8 * k + r] = (o[k] + (1 << 10)) >> 11;
+                }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                int w[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) w[k] = wb[8 * r + k];
+                uint32_t px[8];
+                if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
+                    const uint32_t d = range_idct((w[0] + 16) >> 5);
+#pragma unroll
+                    for (int k = 0; k < 8; k++) px[k] = d;
+                } else {
+                    int o[8];
+                    idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+#pragma unroll
+                    for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
+                }
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");  // pass 2's reads before the next group's scatter
+                const int yr = jr * 8 + r;  // band row (y0 is a multiple of 8)
+                if (j < nyb && y0 + yr < y1)
+                    *reinterpret_cast<uint2*>(ys + yr * wr + (j - jr * nbx) * 8) =
+                        make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24, px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
+            }
+        }
+    }
+    if (ws_over_cs) {
+        __syncthreads();  // the scratch is read
+        stage();
     }
     __syncthreads();
     const int nbytes = g.W * 3;
-    // whole 8-pixel groups and 8-B aligned rows: each thread stores its 24 B itself (no LDS row)
+    // whole 8-pixel groups and 8-B aligned rows: each thread stores its 24 B itself (no LDS row; as
+    // jpeg_color_direct on the host decides)
     const bool direct = (g.W & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
     for (int y = y0; y < y1; y++) {
         uint8_t* ob = orow + ((y - y0) & 1) * orow_sz;
@@ -1538,13 +1637,30 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     const long long nb = (long long)n * g.frame_blocks;
     if (nb >= INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "too many coefficient blocks in one call");
     // colour bands: as many rows as keep the staging within 48 KB of LDS
+#ifndef FM_JP_FUSEY
+#define FM_JP_FUSEY 1
+#endif
+#ifndef FM_JP_WSCS
+#define FM_JP_WSCS 1
+#endif
+    const bool direct = (g.W & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
     int rb = 16;
-    size_t lds = 0;
+    size_t lds = 0, ys_off = 0, ws_off = 0;
     for (;; rb >>= 1) {
         const size_t orow = ((size_t)g.W * 3 + 15) & ~(size_t)15, wr = ((size_t)g.W + 7) & ~(size_t)7;
         size_t nr = 0;
         if (g.nc == 3) nr = g.vmax / g.comp[1].v == 2 ? (size_t)rb / 2 + 3 : (size_t)rb;
-        lds = 2 * orow + rb * wr + (g.nc == 3 ? 2 * nr * (size_t)g.comp[1].bw * 8 + 16 : 0);  // + word look-ahead
+        const size_t wsz = FM_JP_FUSEY && rb >= 8 ? 32 * 65 * 4 : 0, front = direct ? 0 : 2 * orow;
+        const size_t csz = g.nc == 3 ? 2 * nr * (size_t)g.comp[1].bw * 8 + 16 : 0;  // + word look-ahead
+        if (wsz && FM_JP_WSCS != 0) {  // the scratch over the chroma rows
+            ys_off = front;
+            ws_off = ys_off + rb * wr;
+            lds = ws_off + std::max(csz, wsz);
+        } else {
+            ys_off = std::max(front, wsz);
+            ws_off = 0;
+            lds = ys_off + rb * wr + csz;
+        }
         if (lds <= 48 * 1024 || rb == 1) break;
     }
     if (lds > 64 * 1024) return jfail(d, FM_ENOTSUP, "frame width %d too large for the colour kernel", g.W);
@@ -1554,14 +1670,29 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         const int dw = (g.W * g.comp[1].h + g.hmax - 1) / g.hmax;
         mode = (hf == 2 && dw > 2) ? (vf == 2 ? 3 : 2) : 1;
     }
+    // the Y blocks decoded inside the colour kernel when its bands are whole block rows
+    const bool fuse = FM_JP_FUSEY && rb >= 8 && g.comp[0].coef0 == 0;
+    const int skip = fuse ? (g.nc > 1 ? (int)g.comp[1].coef0 : (int)g.frame_blocks) : 0;
+    const long long nbi = (long long)n * ((long long)g.frame_blocks - skip);
+    if (nbi > 0)
+        hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nbi + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
+                           d->d_coef, d->d_msk, d->d_qt, d->g, skip, (int)nbi, d->d_planes);
     {
-        hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nb + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
-                           d->d_coef, d->d_msk, d->d_qt, d->g, 0, (int)nb, d->d_planes);
         const dim3 cgrid((unsigned)((g.H + rb - 1) / rb), (unsigned)n);
-        if (mode == 3) hipLaunchKernelGGL(k_jpeg_color<3>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
-        else if (mode == 2) hipLaunchKernelGGL(k_jpeg_color<2>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
-        else if (mode == 1) hipLaunchKernelGGL(k_jpeg_color<1>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
-        else hipLaunchKernelGGL(k_jpeg_color<0>, cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, out, 0);
+#define FM_JP_COLOR(M, F) \
+    hipLaunchKernelGGL((k_jpeg_color<M, F>), cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, (int)ys_off, (int)ws_off, out, 0, d->d_coef, d->d_msk, d->d_qt)
+        if (fuse) {
+            if (mode == 3) FM_JP_COLOR(3, true);
+            else if (mode == 2) FM_JP_COLOR(2, true);
+            else if (mode == 1) FM_JP_COLOR(1, true);
+            else FM_JP_COLOR(0, true);
+        } else {
+            if (mode == 3) FM_JP_COLOR(3, false);
+            else if (mode == 2) FM_JP_COLOR(2, false);
+            else if (mode == 1) FM_JP_COLOR(1, false);
+            else FM_JP_COLOR(0, false);
+        }
+#undef FM_JP_COLOR
     }
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
