@@ -488,12 +488,6 @@ __device__ __forceinline__ void idct1d(int v0, int v1, int v2, int v3, int v4, i
     o[4] = t13 - a0;
 }
 
-// IDCT_range_limit(cinfo)[x & RANGE_MASK] (jdmaster.c prepare_range_limit_table)
-__device__ __forceinline__ uint32_t range_idct(int x) {
-    const int v = x & 1023;
-    return (uint32_t)(v < 128 ? v + 128 : v < 512 ? 255 : v < 896 ? 0 : v - 896);
-}
-
 // zigzag position -> natural index, 8 per lane of a block's 8-lane group (the coefficient buffer holds
 // blocks in zigzag order): lane r holds positions 8r .. 8r+7
 __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040B12u}, {0x211A130Cu, 0x22293028u},
@@ -503,14 +497,85 @@ __constant__ uint2 c_zz8[8] = {{0x10080100u, 0x0A030209u}, {0x19201811u, 0x05040
 // 8 lanes per block: lane r loads zigzag positions 8r..8r+7 (16 B) and scatters them to natural order
 // in LDS, runs column r of pass 1, then row r of pass 2
 constexpr int kIdctGroups = 4;  // groups of 32 blocks per workgroup (their loads issued together)
+// IDCT scratch of a wave's 8 blocks: row-interleaved, element (row, col) of block b at
+// row * 65 + 8 * b + col, so that pass 1 (lanes = block x column) and pass 2 (lanes = block x
+// row) both hit 64 distinct banks (a [block][65] layout put pass 1 on 8-way conflicts)
+constexpr int kWsWave = 8 * 65;
+__device__ __forceinline__ int ws_block(int lb) { return (lb >> 3) * kWsWave + (lb & 7) * 8; }
+
+// IDCT_range_limit[x & RANGE_MASK] (jdmaster.c prepare_range_limit_table) with x = DESCALE(v, SH): the 10 bits above the rounding point,
+// sign-extended, + CENTERJSAMPLE, clamped to [0, 255] (four VALU ops instead of the table's compare chain)
+template <int SH>
+__device__ __forceinline__ uint32_t range_limit(int v) {
+    const int x = (int)__builtin_amdgcn_sbfe(v + (1 << (SH - 1)), SH, 10) + 128;  // (int: mixed-type min/max go to f64)
+    return (uint32_t)(x < 0 ? 0 : x > 255 ? 255 : x);
+}
+
+// scratch offsets of lane r's zigzag positions 8r .. 8r+7 in its block's rows
+__device__ __forceinline__ void zz_offsets(int r, int (&zo)[8]) {
+    const uint2 nat = c_zz8[r];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
+        zo[i] = (n >> 3) * 65 + (n & 7);
+    }
+}
+
+// a wave's LDS accesses complete in order: its 8-lane blocks need no barrier, only that the compiler
+// keep the accesses in program order
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// lane r of a block's 8 lanes (one wave's): raw = the block's zigzag coefficients 8r .. 8r+7,
+// qc[k] = the dequantization factor of row k, column r -> the 8 samples of row r, packed
+// (jpeg_idct_islow: dequantize, columns with the all-zero-AC shortcut, rows with the zero-row shortcut)
+__device__ __forceinline__ uint2 idct_lane(int* wb, int r, uint4 raw, const int (&qc)[8], const int (&zo)[8]) {
+    const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 8; i++) wb[zo[i]] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
+    wave_lds_order();
+    int v[8];
+    // |coefficient| < 2^15, factor < 2^16: 24-bit multiplies are exact
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = __mul24(wb[65 * k + r], qc[k]);
+    if ((v[1] | v[2] | v[3] | v[4] | v[5] | v[6] | v[7]) == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) wb[65 * k + r] = v[0] * 4;
+    } else {
+        int o[8];
+        idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
+#pragma unroll
+        for (int k = 0; k < 8; k++) wb[65 * k + r] = (o[k] + (1 << 10)) >> 11;
+    }
+    wave_lds_order();
+    int w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = wb[65 * r + k];
+    wave_lds_order();  // (pass 2's reads before the block's next scatter)
+    uint32_t px[8];
+    if ((w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) == 0) {
+        const uint32_t d = range_limit<5>(w[0]);
+#pragma unroll
+        for (int k = 0; k < 8; k++) px[k] = d;
+    } else {
+        int o[8];
+        idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+#pragma unroll
+        for (int k = 0; k < 8; k++) px[k] = range_limit<18>(o[k]);
+    }
+    return make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24, px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
+}
 
 // nblocks blocks of the call: of each frame the blocks from number `skip` on (0: all of them; with
 // k_jpeg_color<., true> decoding the Y blocks itself, the chroma blocks only)
 __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, uint32_t* __restrict__ msk,
                                                     const uint16_t* __restrict__ qt, JpegGeom g, int skip, int nblocks,
                                                     uint8_t* __restrict__ planes) {
-    __shared__ int ws[32][65];  // rows padded by one dword: the 8 blocks of a wave hit different banks
+    __shared__ int ws[4 * kWsWave];
     const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
+    int* wb = ws + ws_block(lb);
     const int b0 = blockIdx.x * (32 * kIdctGroups) + lb;
     const int fbk = (int)g.frame_blocks, dbk = fbk - skip;
     int fbs[kIdctGroups];  // the call-wide block numbers
@@ -531,7 +596,8 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, u
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++)
         if (r == 0 && bm[G]) msk[fbs[G]] = 0u;  // for the next call's stores
-    const uint2 nat = c_zz8[r];
+    int zo[8];
+    zz_offsets(r, zo);
 #pragma unroll
     for (int G = 0; G < kIdctGroups; G++) {
         const bool live = b0 + 32 * G < nblocks;
@@ -544,57 +610,20 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, u
         const int ib = rem - (int)c.coef0;
         const int by = ib / c.bw, bx = ib - by * c.bw;
         const uint16_t* q = qt + ((size_t)frame * kMaxComp + ci) * 64;
-        {
-            const uint4 rw = raw[G];
-            // leave the block zeroed for the next call's sparse coefficient stores (only the 16-B
-            // pieces that hold something: most of a typical block is zero already)
-            if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
-            const uint32_t w4[4] = {rw.x, rw.y, rw.z, rw.w};
-            if (G) __syncthreads();  // the previous group's pass 2 has read ws
+        int qc[8];
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
-                ws[lb][n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
-            }
-        }
-        __syncthreads();
-        // pass 1: column r (jpeg_idct_islow, with the all-zero-AC column shortcut)
-        int v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = ws[lb][8 * k + r] * (int)q[8 * k + r];
-        if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = v[0] * 4;
-        } else {
-            int o[8];
-            idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
-#pragma unroll
-            for (int k = 0; k < 8; k++) ws[lb][8 * k + r] = (o[k] + (1 << 10)) >> 11;
-        }
-        __syncthreads();
-        // pass 2: row r (zero-row shortcut), range-limited samples
-        int w[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) w[k] = ws[lb][8 * r + k];
-        uint32_t px[8];
-        if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
-            const uint32_t d = range_idct((w[0] + 16) >> 5);
-#pragma unroll
-            for (int k = 0; k < 8; k++) px[k] = d;
-        } else {
-            int o[8];
-            idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
-#pragma unroll
-            for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
-        }
+        for (int k = 0; k < 8; k++) qc[k] = (int)q[8 * k + r];
+        // leave the block zeroed for the next call's sparse coefficient stores (only the 16-B
+        // pieces that hold something: most of a typical block is zero already)
+        if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
+        const uint2 px = idct_lane(wb, r, raw[G], qc, zo);
 #ifndef FM_JP_ABL
 #define FM_JP_ABL 0  // timing ablations only (results invalid): 1 IDCT without plane stores, 2 colour without plane loads
 #endif
         if (live && !(FM_JP_ABL & 1)) {
             const int pw = c.bw * 8;
             uint8_t* row = planes + (size_t)frame * g.frame_plane + c.plane0 + (size_t)(by * 8 + r) * pw + (size_t)bx * 8;
-            reinterpret_cast<uint2*>(row)[0] = make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24,
-                                                          px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
+            reinterpret_cast<uint2*>(row)[0] = px;
         }
     }
 }
@@ -619,6 +648,9 @@ __device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr) {  // jdcolor
 // FUSEY: the band's Y blocks (rb a multiple of 8) are dequantized and inverse-transformed here, straight
 // into the LDS rows, instead of going through the Y plane in HBM (k_jpeg_idct then does the chroma
 // blocks only): the plane store and reload were a third of the decoder's device time
+// FUSEY: groups of 32 Y blocks with their loads in flight together (8 groups: 96 VGPRs and spills,
+// 3.0 vs 1.95 ms; loading whole blocks without the piece masks, 1.91-1.96 ms: unchanged)
+constexpr int kYGroups = 4;
 #ifndef FM_JP_COLOR_WPE
 #define FM_JP_COLOR_WPE 5  // five workgroups per CU: the LDS bound with the scratch over the chroma rows
 #endif
@@ -681,81 +713,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FM_JP_COLOR
     if constexpr (FUSEY) {
         // Y block rows y0/8 .. (y1-1)/8, block columns 0 .. wr/8-1, as k_jpeg_idct does them (8 lanes per
         // block), four groups of 32 blocks with their loads in flight together.  The 8 lanes of a block are
-        // one wave's: its scratch row ws[lb] needs wave-level ordering only.
-        int* ws = reinterpret_cast<int*>(lds + ws_off);  // [32][65], over rows not used yet
+        // one wave's: its scratch needs wave-level ordering only (idct_lane).
+        int* ws = reinterpret_cast<int*>(lds + ws_off);  // [4][kWsWave], over rows not used yet
         const int r = threadIdx.x & 7, lb = threadIdx.x >> 3;
         const int nbx = wr >> 3, nyb = nbx * (((y1 - 1) >> 3) - (y0 >> 3) + 1);
         const int64_t blk0 = (int64_t)frame * g.frame_blocks + cy.coef0 + (int64_t)(y0 >> 3) * cy.bw;
         const uint16_t* q = qt + (size_t)frame * kMaxComp * 64;
-        int qv[8];
+        int qv[8], zo[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) qv[k] = (int)q[8 * k + r];
-        const uint2 nat = c_zz8[r];
-        for (int base = 0; base < nyb; base += 32 * kIdctGroups) {
-            int64_t bk[kIdctGroups];
-            uint32_t bm[kIdctGroups];
-            uint4 raw[kIdctGroups];
+        zz_offsets(r, zo);
+        for (int base = 0; base < nyb; base += 32 * kYGroups) {
+            int64_t bk[kYGroups];
+            uint32_t bm[kYGroups];
+            uint4 raw[kYGroups];
 #pragma unroll
-            for (int G = 0; G < kIdctGroups; G++) {
+            for (int G = 0; G < kYGroups; G++) {
                 const int j = base + 32 * G + lb, jr = j / nbx;
                 bk[G] = blk0 + (int64_t)jr * cy.bw + (j - jr * nbx);
                 bm[G] = j < nyb ? msk[bk[G]] : 0u;
             }
 #pragma unroll
-            for (int G = 0; G < kIdctGroups; G++)
+            for (int G = 0; G < kYGroups; G++)
                 raw[G] = ((bm[G] >> r) & 1) ? reinterpret_cast<const uint4*>(coef + bk[G] * 64)[r] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-            for (int G = 0; G < kIdctGroups; G++) {
+            for (int G = 0; G < kYGroups; G++) {
                 if (r == 0 && bm[G]) msk[bk[G]] = 0u;  // for the next call's stores
                 if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + bk[G] * 64)[r] = make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
-            for (int G = 0; G < kIdctGroups; G++) {
+            for (int G = 0; G < kYGroups; G++) {
                 const int j = base + 32 * G + lb, jr = j / nbx;
                 if (base + 32 * G >= nyb) break;  // uniform over the workgroup
-                const uint32_t w4[4] = {raw[G].x, raw[G].y, raw[G].z, raw[G].w};
-                int* wb = ws + lb * 65;
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int n = (int)(((i < 4 ? nat.x : nat.y) >> (8 * (i & 3))) & 63);
-                    wb[n] = (int)(int16_t)(w4[i >> 1] >> (16 * (i & 1)));
-                }
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");
-                int v[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) v[k] = wb[8 * k + r] * qv[k];
-                if (v[1] == 0 && v[2] == 0 && v[3] == 0 && v[4] == 0 && v[5] == 0 && v[6] == 0 && v[7] == 0) {
-#pragma unroll
-                    for (int k = 0; k < 8; k++) wb[8 * k + r] = v[0] * 4;
-                } else {
-                    int o[8];
-                    idct1d(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], o);
-#pragma unroll
-                    for (int k = 0; k < 8; k++) wb[8 * k + r] = (o[k] + (1 << 10)) >> 11;
-                }
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");
-                int w[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) w[k] = wb[8 * r + k];
-                uint32_t px[8];
-                if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
-                    const uint32_t d = range_idct((w[0] + 16) >> 5);
-#pragma unroll
-                    for (int k = 0; k < 8; k++) px[k] = d;
-                } else {
-                    int o[8];
-                    idct1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
-#pragma unroll
-                    for (int k = 0; k < 8; k++) px[k] = range_idct((o[k] + (1 << 17)) >> 18);
-                }
-                __builtin_amdgcn_wave_barrier();
-                asm volatile("" ::: "memory");  // pass 2's reads before the next group's scatter
+                const uint2 px = idct_lane(ws + ws_block(lb), r, raw[G], qv, zo);
                 const int yr = jr * 8 + r;  // band row (y0 is a multiple of 8)
                 if (j < nyb && y0 + yr < y1)
-                    *reinterpret_cast<uint2*>(ys + yr * wr + (j - jr * nbx) * 8) =
-                        make_uint2(px[0] | px[1] << 8 | px[2] << 16 | px[3] << 24, px[4] | px[5] << 8 | px[6] << 16 | px[7] << 24);
+                    *reinterpret_cast<uint2*>(ys + yr * wr + (j - jr * nbx) * 8) = px;
             }
         }
     }
@@ -1650,7 +1643,7 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         const size_t orow = ((size_t)g.W * 3 + 15) & ~(size_t)15, wr = ((size_t)g.W + 7) & ~(size_t)7;
         size_t nr = 0;
         if (g.nc == 3) nr = g.vmax / g.comp[1].v == 2 ? (size_t)rb / 2 + 3 : (size_t)rb;
-        const size_t wsz = FM_JP_FUSEY && rb >= 8 ? 32 * 65 * 4 : 0, front = direct ? 0 : 2 * orow;
+        const size_t wsz = FM_JP_FUSEY && rb >= 8 ? 4 * kWsWave * 4 : 0, front = direct ? 0 : 2 * orow;
         const size_t csz = g.nc == 3 ? 2 * nr * (size_t)g.comp[1].bw * 8 + 16 : 0;  // + word look-ahead
         if (wsz && FM_JP_WSCS != 0) {  // the scratch over the chroma rows
             ys_off = front;
