@@ -618,7 +618,8 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(int16_t* __restrict__ coef, u
         if ((bm[G] >> r) & 1) reinterpret_cast<uint4*>(coef + (size_t)fb * 64)[r] = make_uint4(0, 0, 0, 0);
         const uint2 px = idct_lane(wb, r, raw[G], qc, zo);
 #ifndef FM_JP_ABL
-#define FM_JP_ABL 0  // timing ablations only (results invalid): 1 IDCT without plane stores, 2 colour without plane loads
+#define FM_JP_ABL 0  // timing ablations only (results invalid): 1 IDCT without plane stores, 2 colour without plane
+                     // loads, 4 colour without its Y blocks' IDCT, 8 colour kernel without the colour rows
 #endif
         if (live && !(FM_JP_ABL & 1)) {
             const int pw = c.bw * 8;
@@ -710,7 +711,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FM_JP_COLOR
         }
     };
     if (!ws_over_cs) stage();
-    if constexpr (FUSEY) {
+    if constexpr (FUSEY && !(FM_JP_ABL & 4)) {
         // Y block rows y0/8 .. (y1-1)/8, block columns 0 .. wr/8-1, as k_jpeg_idct does them (8 lanes per
         // block), four groups of 32 blocks with their loads in flight together.  The 8 lanes of a block are
         // one wave's: its scratch needs wave-level ordering only (idct_lane).
@@ -761,7 +762,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FM_JP_COLOR
     // whole 8-pixel groups and 8-B aligned rows: each thread stores its 24 B itself (no LDS row; as
     // jpeg_color_direct on the host decides)
     const bool direct = (g.W & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0;
-    for (int y = y0; y < y1; y++) {
+    for (int y = y0; y < ((FM_JP_ABL & 8) ? y0 : y1); y++) {
         uint8_t* ob = orow + ((y - y0) & 1) * orow_sz;
         const uint8_t* yrow = ys + (y - y0) * wr;
         const uint8_t *n0 = nullptr, *f0 = nullptr;
