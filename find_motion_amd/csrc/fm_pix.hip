@@ -234,6 +234,48 @@ template <int K> constexpr uint32_t tap2(int t) {
     return (uint32_t)Taps<K>::c[2 * t] | (2 * t + 1 < K ? (uint32_t)Taps<K>::c[2 * t + 1] << 16 : 0u);
 }
 
+#ifndef FM_PIX_FMA_INPLACE
+#define FM_PIX_FMA_INPLACE 1
+#endif
+#ifndef FM_PIX_SADDR
+#define FM_PIX_SADDR 1
+#endif
+// accumulateWeighted's bg = fma(bg, beta, blur * alpha) updating the background register in place.
+// As __fma_rn the compiler picks v_fmac_f64 accumulating into the register of the table read, so
+// every loop-carried background value went through a v_mov_b64 at the top of the frame loop
+// (8 of the chain's ~95 VALU instructions per wave-frame).
+__device__ __forceinline__ double bg_fma(double b, double beta, double bl) {
+#if FM_PIX_FMA_INPLACE
+    asm("v_fma_f64 %0, %0, %1, %2" : "+v"(b) : "s"(beta), "v"(bl));
+    return b;
+#else
+    return __fma_rn(b, beta, bl);
+#endif
+}
+
+// A frame's base address in SGPRs, so the quad loads take the saddr form (SGPR base + the lane's
+// 32-bit offset) instead of a per-lane 64-bit multiply-add per load (LICM had hoisted
+// src + offset out of the frame loop as a 64-bit VGPR pair).
+typedef const __attribute__((address_space(1))) uint8_t* gbytes_t;  // global (not flat) addressing
+typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
+// 12 bytes at a 4-B aligned global address (global_load_dwordx3)
+// (the compiler keeps base + offset as one 64-bit add per load: passing the offset through an empty
+// asm to get SGPR base + 32-bit VGPR offset cost a copy per load and a vmcnt wait at the back-edge)
+__device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) {
+    typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
+    d = *(const __attribute__((address_space(1))) u3a*)(base + off);
+}
+__device__ __forceinline__ gbytes_t frame_base(const uint8_t* p) {
+#if FM_PIX_SADDR
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (gbytes_t)(((uint64_t)hi << 32) | lo);
+#else
+    return (gbytes_t)reinterpret_cast<uintptr_t>(p);
+#endif
+}
+
 // Per-frame, per-wave constants of the chain stage (computed once per tile).
 struct ChainCtx {
     uint64_t colmask;   // lanes whose column is inside the image
@@ -320,7 +362,7 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         // (double)blur * alpha from a 256-entry LDS table (the same correctly rounded product):
         // an LDS read instead of two f64-rate VALU ops per pixel
         const double bl = atab[blur];
-        double nb = __fma_rn(b, beta, bl);
+        double nb = bg_fma(b, beta, bl);
 #endif
         if (TAIL) {  // accumulateWeighted's scalar tail: two products, one add there
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
@@ -726,7 +768,7 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
         const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
         tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
         const double bl = atab[blur];
-        double nb = __fma_rn(b, beta, bl);
+        double nb = bg_fma(b, beta, bl);
         if (TAIL) {
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
             if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
@@ -853,7 +895,6 @@ constexpr int P5_HROW = TS;              // u16 per H row
 constexpr int P5_HBUF = (P5_GH + P5_HR) * P5_HROW;  // + the pad row (pair) idle tap jobs store to
 constexpr int p5_lds_bytes() { return 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2 + 256 * 8; }
 
-typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
 struct P5Raw {
     u32x3_t v[P5_GJ];  // one 96-bit value per job: one register triple the allocator keeps whole
 };
@@ -977,10 +1018,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        const uint8_t* src = a.src + f * fbytes;
+        const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
         for (int i = 0; i < P5_GJ; i++) {
-            __builtin_memcpy(&rw.v[i], src + goff[i], 12);  // global_load_dwordx3 (4-B aligned)
+            load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
@@ -1238,9 +1279,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE)
     // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        const uint8_t* src = a.src + f * fbytes;
+        const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
-        for (int i = 0; i < G::GJ; i++) __builtin_memcpy(&rw[i], src + goff[i], 12);
+        for (int i = 0; i < G::GJ; i++) load12(rw[i], src, goff[i]);
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
