@@ -61,6 +61,7 @@ constexpr int RG = 512;         // k_regions threads
 #define FM_MERGE_PRIO 2
 #endif
 constexpr int MAX_REGION_TILES = 8192;
+static_assert(MAX_REGION_TILES <= 32 * RG, "k_regions keeps one candidate bit per tile of a thread in a u32");
 constexpr uint32_t REF_OUTER = 0x80000000u;
 constexpr uint32_t REF_EDGE = 0x40000000u;
 
@@ -533,28 +534,32 @@ __device__ __forceinline__ uint32_t tile_flags(const FusedArgs& a, size_t f, int
     return x.x | x.y | x.z | x.w | y.x | y.y | y.z | y.w;
 }
 
-__device__ __forceinline__ bool is_candidate(const FusedArgs& a, size_t f, int ti, bool dilate) {
-    if (tile_flags(a, f, ti)) return true;
+// the candidate test (above) over the frame's flag words staged in LDS (fl[t] = tile_flags of tile t)
+__device__ __forceinline__ bool is_candidate_lds(const int* fl, const FusedArgs& a, int ti, bool dilate) {
+    if (fl[ti]) return true;
     if (!dilate) return false;
     const int ntx = a.ntx, tx = ti % ntx, ty = ti / ntx;
     const bool l = tx > 0, r = tx + 1 < ntx, u = ty > 0, d = ty + 1 < a.nty;
     uint32_t m = 0;
-    if (l) m |= tile_flags(a, f, ti - 1) & FLAG_R;
-    if (r) m |= tile_flags(a, f, ti + 1) & FLAG_L;
-    if (u) m |= tile_flags(a, f, ti - ntx) & FLAG_B;
-    if (d) m |= tile_flags(a, f, ti + ntx) & FLAG_T;
-    if (u && l) m |= tile_flags(a, f, ti - ntx - 1) & FLAG_BR;
-    if (u && r) m |= tile_flags(a, f, ti - ntx + 1) & FLAG_BL;
-    if (d && l) m |= tile_flags(a, f, ti + ntx - 1) & FLAG_TR;
-    if (d && r) m |= tile_flags(a, f, ti + ntx + 1) & FLAG_TL;
+    if (l) m |= (uint32_t)fl[ti - 1] & FLAG_R;
+    if (r) m |= (uint32_t)fl[ti + 1] & FLAG_L;
+    if (u) m |= (uint32_t)fl[ti - ntx] & FLAG_B;
+    if (d) m |= (uint32_t)fl[ti + ntx] & FLAG_T;
+    if (u && l) m |= (uint32_t)fl[ti - ntx - 1] & FLAG_BR;
+    if (u && r) m |= (uint32_t)fl[ti - ntx + 1] & FLAG_BL;
+    if (d && l) m |= (uint32_t)fl[ti + ntx - 1] & FLAG_TR;
+    if (d && r) m |= (uint32_t)fl[ti + ntx + 1] & FLAG_TL;
     return m != 0;
 }
 
 // one workgroup per frame: candidate list, empty-tile regions (4-connected: two
 // empty tiles share a whole background edge), one node per region
 template <bool DILATE>
+// (uf is sized to the frame's tiles at launch: a fixed MAX_REGION_TILES array was 32 KB of LDS per
+// workgroup, which the contour kernels resident beside the pixel kernel often did not leave free,
+// so a batch's k_regions waited for the pixel kernel to end: 269 µs instead of 10)
 __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
-    __shared__ int uf[MAX_REGION_TILES];
+    extern __shared__ int uf[];  // [a.ntiles]
     __shared__ int s_nc, s_nr;
     const int f = blockIdx.x;
     const int nt = a.ntiles, ntx = a.ntx, nty = a.nty;
@@ -570,9 +575,16 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
             a.count[2 * (size_t)a.T * a.S + 1] = 0;
         }
     }
+    // each tile's flag words read once into LDS (uf doubles as the staging array), then the
+    // candidate test over LDS: is_candidate from global memory read every tile's words up to 9 times
+    for (int t = tid; t < nt; t += RG) uf[t] = (int)tile_flags(a, f, t);
     __syncthreads();
-    for (int t = tid; t < nt; t += RG) {
-        const bool c = is_candidate(a, f, t, DILATE);
+    uint32_t cm = 0;  // bit i: tile tid + i * RG (nt <= MAX_REGION_TILES = 16 * RG)
+    for (int t = tid, i = 0; t < nt; t += RG, i++)
+        if (is_candidate_lds(uf, a, t, DILATE)) cm |= 1u << i;
+    __syncthreads();
+    for (int t = tid, i = 0; t < nt; t += RG, i++) {
+        const bool c = (cm >> i) & 1;
         a.candf[(size_t)f * nt + t] = c ? 1 : 0;
         uf[t] = c ? -1 : t;
         if (c) a.clist[(size_t)f * nt + atomicAdd(&s_nc, 1)] = t;
@@ -1030,8 +1042,9 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     const unsigned F = (unsigned)(a.T * a.S);
     const dim3 gf(cc::GW, F);
     int tok = tm ? tm->begin("regions", st) : -1;
-    if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), 0, st, a);
-    else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), 0, st, a);
+    const size_t rg_lds = (size_t)a.ntiles * sizeof(int);
+    if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), rg_lds, st, a);
+    else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), rg_lds, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("tile_ccl", st) : -1;
     if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), 0, st, a);
