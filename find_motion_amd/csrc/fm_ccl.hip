@@ -173,6 +173,61 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+#ifndef FM_CCL_DPP_SCAN
+#define FM_CCL_DPP_SCAN 1  // (end to end neutral: 372-380 k either way over 7 alternating rounds on two boxes)
+#endif
+// Wave-wide inclusive prefix sum by DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast 15 / 31 across rows): six VALU adds, where a __shfl_up loop is six ds_bpermute
+// round trips through the LDS unit.  Needs every lane active (callers are in wave-uniform flow).
+__device__ __forceinline__ int wave_incl_sum(int v) {
+#if FM_CCL_DPP_SCAN
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+#else
+    const int ln = (int)__lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (ln >= o) v += u;
+    }
+    return v;
+#endif
+}
+// __shfl_up(v, 1) / __shfl_down(v, 1) (lane 0 / 63 keep their own value) by DPP wave shifts
+__device__ __forceinline__ int lane_up1(int v) {
+#if FM_CCL_DPP_SCAN
+    return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+#else
+    return __shfl_up(v, 1, 64);
+#endif
+}
+__device__ __forceinline__ int lane_down1(int v) {
+#if FM_CCL_DPP_SCAN
+    return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false);  // wave_shl:1
+#else
+    return __shfl_down(v, 1, 64);
+#endif
+}
+__device__ __forceinline__ uint64_t lane_down1_64(uint64_t v) {
+    return ((uint64_t)(uint32_t)lane_down1((int)(uint32_t)(v >> 32)) << 32) | (uint32_t)lane_down1((int)(uint32_t)v);
+}
+// a lane's value broadcast (v_readlane with the DPP variant, else ds_bpermute as __shfl)
+__device__ __forceinline__ int lane_at(int v, int lane) {
+#if FM_CCL_DPP_SCAN
+    return __builtin_amdgcn_readlane(v, lane);
+#else
+    return __shfl(v, lane, 64);
+#endif
+}
+__device__ __forceinline__ uint64_t lane_at64(uint64_t v, int lane) {
+    return ((uint64_t)(uint32_t)lane_at((int)(uint32_t)(v >> 32), lane) << 32) | (uint32_t)lane_at((int)(uint32_t)v, lane);
+}
+
 // the value of lane ln ^ J, without LDS: v_permlane32_swap / v_permlane16_swap for 32 / 16, DPP
 // row_ror:8 for 8, row_half_mirror then a reversed quad_perm for 4, quad_perm for 2 and 1
 template <int J>
@@ -294,7 +349,7 @@ __device__ __forceinline__ int take_nodes(const FusedArgs& a, size_t f, int n, i
             if (sh0 + c + n <= (long long)a.nnodes) first = sh0 + c;
         }
     }
-    return __shfl((int)first, 0, 64);
+    return lane_at((int)first, 0);
 }
 
 // TCCL_RUNS (nothing written) if the tile has more than CAP runs
@@ -336,13 +391,8 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
 
     const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
     const int nr = __popcll(starts);
-    int incl = nr;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (ln >= o) incl += v;
-    }
-    const int total = __shfl(incl, 63, 64);
+    const int incl = wave_incl_sum(nr);
+    const int total = lane_at(incl, 63);
     const int base = incl - nr;
     if (total > CAP) return TCCL_RUNS;
     FM_STAMP(3);
@@ -372,8 +422,8 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
     // Adjacent-row run pairs to union, from the bit masks (no LDS walk): a run B of
     // row ln+1 touches a contiguous range of same-colour runs of row ln -- window
     // [b0-1, b1+1] for foreground (8-connected), [b0, b1] for background (4-connected).
-    const uint64_t m2 = __shfl_down(m, 1, 64), s2 = __shfl_down(starts, 1, 64);
-    const int base2 = __shfl_down(base, 1, 64);
+    const uint64_t m2 = lane_down1_64(m), s2 = lane_down1_64(starts);
+    const int base2 = lane_down1(base);
     int npl = 0;
     // count pass
     if (ln < 63) {
@@ -389,13 +439,8 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             if (hits) npl += ((run_at(base, starts, 63 - __builtin_clzll(hits)) - run_at(base, starts, __builtin_ctzll(hits))) >> 1) + 1;
         }
     }
-    int pin = npl;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(pin, o, 64);
-        if (ln >= o) pin += v;
-    }
-    const int np = __shfl(pin, 63, 64);
+    const int pin = wave_incl_sum(npl);
+    const int np = lane_at(pin, 63);
     if (np > 2 * CAP) return TCCL_RUNS;
     const int pbase = pin - npl;
     if (ln < 63) {  // write pass
@@ -464,13 +509,8 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
     // ordinals of the roots in raster order
     int myr = 0;
     for (int i = base; i < base + nr; i++) myr += ((par[i]) == i);
-    int rin = myr;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(rin, o, 64);
-        if (ln >= o) rin += v;
-    }
-    const int nroots = __shfl(rin, 63, 64);
+    const int rin = wave_incl_sum(myr);
+    const int nroots = lane_at(rin, 63);
     const int nb = take_nodes(a, f, nroots, ln);
     if (nb < 0) return TCCL_NODES;
     if (ln == 63) {
@@ -510,8 +550,8 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
         NR[ord[i]] = nrec;
     }
     const uint64_t mask_c = (2ull << ln) - 1;
-    const uint64_t s0 = __shfl(starts, 0, 64), s63 = __shfl(starts, 63, 64);
-    const uint64_t m0 = __shfl(m, 0, 64), m63 = __shfl(m, 63, 64);
+    const uint64_t s0 = lane_at64(starts, 0), s63 = lane_at64(starts, 63);
+    const uint64_t m0 = lane_at64(m, 0), m63 = lane_at64(m, 63);
     const int id0 = rb[0] + __popcll(s0 & mask_c) - 1;
     const int id63 = rb[63] + __popcll(s63 & mask_c) - 1;
     TR->edges[ln] = (uint16_t)(ord[(par[base])] | ((rf[base] & 1) << 15));
@@ -747,10 +787,10 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
         // right edge
         if (hasR) {
             const uint16_t A = TR[t].edges[64 + ln];
-            const int Ap = __shfl_up((int)A, 1, 64);
+            const int Ap = lane_up1((int)A);
             if (cf[t + 1]) {
                 const uint16_t B = TR[t + 1].edges[ln];
-                const int Bp = __shfl_up((int)B, 1, 64);
+                const int Bp = lane_up1((int)B);
                 if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, t + 1, B));
                 if (efg(A)) {
                     if (ln > 0) {
@@ -770,10 +810,10 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
         if (hasD) {
             const int n = t + ntx;
             const uint16_t A = TR[t].edges[192 + ln];
-            const int Ap = __shfl_up((int)A, 1, 64);
+            const int Ap = lane_up1((int)A);
             if (cf[n]) {
                 const uint16_t B = TR[n].edges[128 + ln];
-                const int Bp = __shfl_up((int)B, 1, 64);
+                const int Bp = lane_up1((int)B);
                 if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, n, B));
                 if (efg(A)) {
                     if (ln > 0) {
@@ -801,12 +841,12 @@ __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
         // left / top edges against empty regions (candidate pairs are done by the neighbour)
         if (tx > 0 && !cf[t - 1]) {
             const uint16_t A = TR[t].edges[ln];
-            const int Ap = __shfl_up((int)A, 1, 64);
+            const int Ap = lane_up1((int)A);
             if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - 1]);
         }
         if (ty > 0 && !cf[t - ntx]) {
             const uint16_t A = TR[t].edges[128 + ln];
-            const int Ap = __shfl_up((int)A, 1, 64);
+            const int Ap = lane_up1((int)A);
             if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - ntx]);
         }
     }
