@@ -27,9 +27,32 @@ def test_decoder_equals_libjpeg(name, kw, H, W):
     dec.close()
 
 
+@pytest.mark.parametrize("name,kw", ENCODINGS)
+def test_wide_frames_without_the_fused_y_idct(name, kw):
+    """3840 px wide: the colour kernel's LDS budget leaves bands of 4 rows, narrower than a block
+    row, so k_jpeg_idct transforms every block (Y too) and the colour kernel reads the Y plane --
+    the path the fused Y IDCT replaced for 1080p.  Two calls: the coefficient buffer and the piece
+    masks must come back zeroed from both kernels."""
+    H, W = 19, 3840
+    frames = [encode(image(H, W, kind, seed=s), **kw) for s, kind in enumerate(["noise", "smooth"])]
+    dec = MJpegDecoder(W, H, max_frames=2)
+    for _ in range(2):
+        got = dec.decode(frames)
+        for i, f in enumerate(frames):
+            assert np.array_equal(got[i], reference_decode(f)), (name, i)
+        frames = frames[::-1]
+    dec.close()
+
+
 def test_grayscale_frames_come_out_bgr():
     frames = [encode(image(37, 53, "smooth", seed=s)[..., 1], quality=75) for s in range(3)]
     dec = MJpegDecoder(53, 37, max_frames=3)
+    got = dec.decode(frames)
+    for i, f in enumerate(frames):
+        assert np.array_equal(got[i], reference_decode(f))
+    # and 3840 wide (k_jpeg_idct on every block, not fused into the colour kernel)
+    frames = [encode(image(11, 3840, "noise", seed=s)[..., 1], quality=75) for s in range(2)]
+    dec = MJpegDecoder(3840, 11, max_frames=2)
     got = dec.decode(frames)
     for i, f in enumerate(frames):
         assert np.array_equal(got[i], reference_decode(f))
