@@ -890,8 +890,13 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // consecutive batches on different contour streams: with 4 slots on 3 streams a fixed
         // slot -> stream map put every fourth pair of consecutive chains on one stream, one after
         // the other (the last batch's chain waited ≈130 µs for its predecessor's)
-        B.ccl_stream = c->ccl_streams[c->ccl_next];
-        c->ccl_next = (c->ccl_next + 1) % c->nccl;
+#ifndef FM_CCL_ROTATE
+#define FM_CCL_ROTATE 1
+#endif
+        if (FM_CCL_ROTATE) {
+            B.ccl_stream = c->ccl_streams[c->ccl_next];
+            c->ccl_next = (c->ccl_next + 1) % c->nccl;
+        }
         hipStream_t cs = c->serial ? ps : B.ccl_stream;
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
         HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
