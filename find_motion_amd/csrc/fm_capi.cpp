@@ -36,7 +36,10 @@ enum class ResizeMode { Identity, Fast, General };
 // recurrence), each slot's contour pass on its own stream, so the latency-bound
 // contour passes of consecutive batches overlap each other and the next
 // batches' pixel kernels.
-constexpr int kSlots = 4;
+#ifndef FM_SLOTS
+#define FM_SLOTS 4
+#endif
+constexpr int kSlots = FM_SLOTS;
 struct BatchSlot {
     uint8_t* d_in = nullptr;        // host-fed staging [T][S][H][W][3]
     uint8_t* d_work = nullptr;      // resized BGR [T][S][h][w][3] (mode D)
