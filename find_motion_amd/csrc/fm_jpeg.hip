@@ -981,25 +981,30 @@ struct fm_mjpeg {
     int tsel[kMaxComp][2] = {};      // (td, ta) of each component in the scan
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    // device buffers
-    uint8_t* d_stream = nullptr;
-    size_t stream_cap = 0;
-    Seg* d_segs = nullptr;
-    size_t segs_cap = 0;
-    uint32_t* d_chunk0 = nullptr;      // [nseg + 1] first chunk of each segment
-    size_t chunk0_cap = 0;
-    TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
-    size_t ts_cap = 0;
+    // device buffers of one call, two sets used in turn, each with its own stream: a call's Huffman
+    // pass (latency-bound, few waves) runs beside the previous call's IDCT and colour kernels
+    struct DevSet {
+        hipStream_t st = nullptr;
+        hipEvent_t done = nullptr;         // the call's kernels are finished (the caller's stream waits for it)
+        uint8_t* d_stream = nullptr;
+        size_t stream_cap = 0;
+        Seg* d_segs = nullptr;
+        size_t segs_cap = 0;
+        uint32_t* d_chunk0 = nullptr;      // [nseg + 1] first chunk of each segment
+        size_t chunk0_cap = 0;
+        TileState* d_ts = nullptr;         // look-back records, one per tile of 64 chunks (+ the tile counter)
+        size_t ts_cap = 0;
+        HuffDev* d_tabs = nullptr;         // [n_sets][4]
+        size_t tabs_cap = 0;
+        uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
+        int16_t* d_coef = nullptr;         // [max_frames][frame_blocks][64]
+        uint32_t* d_msk = nullptr;         // [max_frames][frame_blocks]: non-zero 16-B pieces of each block
+        uint8_t* d_planes = nullptr;       // [max_frames][frame_plane]
+    } ds[2];
     int CB = 512, OV = 512;            // chunk and speculation lengths in bits (fm_mjpeg_tune)
     uint64_t* d_stamps = nullptr;      // dev build, FM_JPEG_STAMPS: per-tile phase stamps of k_jpeg_huff
     size_t stamps_cap = 0;
     size_t stamps_n = 0;
-    HuffDev* d_tabs = nullptr;         // [n_sets][4]
-    int tabs_cap = 0;
-    uint16_t* d_qt = nullptr;          // [max_frames][3][64] natural order
-    int16_t* d_coef = nullptr;         // [max_frames][frame_blocks][64]
-    uint32_t* d_msk = nullptr;         // [max_frames][frame_blocks]: non-zero 16-B pieces of each block
-    uint8_t* d_planes = nullptr;       // [max_frames][frame_plane]
     uint8_t* d_out = nullptr;          // device BGR when the caller wants host output
     // pinned host staging, two sets used in turn: a call refills the set whose uploads (two calls
     // back) are done, so host parsing overlaps the previous call's transfers and kernels
@@ -1016,9 +1021,7 @@ struct fm_mjpeg {
         hipEvent_t done = nullptr;  // the set's uploads are finished
         bool used = false;
     } hs[2];
-    int cur = 0;
-    hipStream_t last_st = nullptr;     // stream of the previous call, and its kernels' completion
-    hipEvent_t last_ev = nullptr;
+    int cur = 0;  // the next call's host and device sets
     float last_ms = 0.f;
     bool timing = false;
 };
@@ -1324,12 +1327,14 @@ int setup_geometry(fm_mjpeg* d, const ParsedJpeg& J) {
         g.bpm = 1;
     }
     const size_t nb = (size_t)d->max_frames * blocks * 64;
-    JHIP(d, hipMalloc((void**)&d->d_coef, nb * sizeof(int16_t)));
-    JHIP(d, hipMemsetAsync(d->d_coef, 0, nb * sizeof(int16_t), d->st));
-    JHIP(d, hipMalloc((void**)&d->d_msk, (size_t)d->max_frames * blocks * sizeof(uint32_t)));
-    JHIP(d, hipMemsetAsync(d->d_msk, 0, (size_t)d->max_frames * blocks * sizeof(uint32_t), d->st));
-    JHIP(d, hipMalloc((void**)&d->d_planes, (size_t)d->max_frames * g.frame_plane));
-    JHIP(d, hipMalloc((void**)&d->d_qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t)));
+    for (auto& S : d->ds) {
+        JHIP(d, hipMalloc((void**)&S.d_coef, nb * sizeof(int16_t)));
+        JHIP(d, hipMemsetAsync(S.d_coef, 0, nb * sizeof(int16_t), d->st));
+        JHIP(d, hipMalloc((void**)&S.d_msk, (size_t)d->max_frames * blocks * sizeof(uint32_t)));
+        JHIP(d, hipMemsetAsync(S.d_msk, 0, (size_t)d->max_frames * blocks * sizeof(uint32_t), d->st));
+        JHIP(d, hipMalloc((void**)&S.d_planes, (size_t)d->max_frames * g.frame_plane));
+        JHIP(d, hipMalloc((void**)&S.d_qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t)));
+    }
     for (auto& H : d->hs)
         JHIP(d, hipHostMalloc((void**)&H.qt, (size_t)d->max_frames * kMaxComp * 64 * sizeof(uint16_t), hipHostMallocDefault));
     JHIP(d, hipStreamSynchronize(d->st));
@@ -1360,7 +1365,10 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
         H.tabs_cap = 4;
         JHIP(d, hipEventCreateWithFlags(&H.done, hipEventDisableTiming));
     }
-    JHIP(d, hipEventCreateWithFlags(&d->last_ev, hipEventDisableTiming));
+    for (auto& S : d->ds) {
+        JHIP(d, hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+        JHIP(d, hipEventCreateWithFlags(&S.done, hipEventDisableTiming));
+    }
     d->pool = new FramePool(std::max(0, std::min(7, (int)std::thread::hardware_concurrency() - 1)));
     return FM_OK;
 }
@@ -1368,15 +1376,21 @@ int fm_mjpeg_create(int device, int width, int height, int max_frames, fm_mjpeg*
 void fm_mjpeg_destroy(fm_mjpeg* d) {
     if (!d) return;
     if (d->st) (void)hipStreamSynchronize(d->st);
-    for (void* p : {(void*)d->d_stream, (void*)d->d_segs, (void*)d->d_tabs, (void*)d->d_qt, (void*)d->d_coef, (void*)d->d_msk,
-                    (void*)d->d_planes, (void*)d->d_out, (void*)d->d_chunk0, (void*)d->d_ts, (void*)d->d_stamps})
+    for (auto& S : d->ds) {
+        if (S.st) (void)hipStreamSynchronize(S.st);
+        for (void* p : {(void*)S.d_stream, (void*)S.d_segs, (void*)S.d_tabs, (void*)S.d_qt, (void*)S.d_coef, (void*)S.d_msk,
+                        (void*)S.d_planes, (void*)S.d_chunk0, (void*)S.d_ts})
+            if (p) (void)hipFree(p);
+        if (S.done) (void)hipEventDestroy(S.done);
+        if (S.st) (void)hipStreamDestroy(S.st);
+    }
+    for (void* p : {(void*)d->d_out, (void*)d->d_stamps})
         if (p) (void)hipFree(p);
     for (auto& H : d->hs) {
         for (void* p : {(void*)H.stream, (void*)H.segs, (void*)H.tabs, (void*)H.qt, (void*)H.chunk0})
             if (p) (void)hipHostFree(p);
         if (H.done) (void)hipEventDestroy(H.done);
     }
-    if (d->last_ev) (void)hipEventDestroy(d->last_ev);
     delete d->pool;
     if (d->e0) (void)hipEventDestroy(d->e0);
     if (d->e1) (void)hipEventDestroy(d->e1);
@@ -1416,12 +1430,15 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         return jfail(d, FM_EINVAL, "n %d outside [1, max_frames=%d] or null buffers", n, d->max_frames);
     if (!d->pool) return jfail(d, FM_ESTATE, "decoder not initialised (fm_mjpeg_create failed)");
     JHIP(d, hipSetDevice(d->device));
-    if (!st) st = d->st;
-    // the staging set's previous uploads must be done before it is refilled; the device buffers are
-    // reused in stream order (a call on another stream than the previous one waits for its kernels)
+    // The call runs on its device set's stream (the set of the call before the previous one: stream
+    // order reuses its buffers) and the caller's stream waits for it at the end; work queued on the
+    // caller's stream before the call is not waited for (the output buffer must be free already).
+    // The host staging set's previous uploads must be done before it is refilled.
+    const hipStream_t cst = st ? st : d->st;
     auto& H = d->hs[d->cur];
+    auto& S = d->ds[d->cur];
+    st = S.st;
     if (H.used) JHIP(d, hipEventSynchronize(H.done));
-    if (d->last_st && d->last_st != st) JHIP(d, hipStreamWaitEvent(st, d->last_ev, 0));
     std::vector<ParsedJpeg> P(n);
     for (int i = 0; i < n; i++)
         if (!jpegs[i]) return jfail(d, FM_EINVAL, "frame %d: null", i);
@@ -1582,10 +1599,10 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     run_tile[nruns] = ntiles;
     H.chunk0[nseg] = (uint32_t)nchunks;
     if (nchunks >= (size_t)INT32_MAX / 2) return jfail(d, FM_ENOTSUP, "compressed batch too large");
-    if (int rc = grow_dev(d, &d->d_stream, d->stream_cap, w + kStreamSlack)) return rc;  // look-ahead reads
-    if (int rc = grow_dev(d, &d->d_segs, d->segs_cap, segs.size())) return rc;
-    if (int rc = grow_dev(d, &d->d_chunk0, d->chunk0_cap, (size_t)nseg + 1)) return rc;
-    if (int rc = grow_dev(d, &d->d_ts, d->ts_cap, ntiles + nruns)) return rc;  // + one tile counter per run
+    if (int rc = grow_dev(d, &S.d_stream, S.stream_cap, w + kStreamSlack)) return rc;  // look-ahead reads
+    if (int rc = grow_dev(d, &S.d_segs, S.segs_cap, segs.size())) return rc;
+    if (int rc = grow_dev(d, &S.d_chunk0, S.chunk0_cap, (size_t)nseg + 1)) return rc;
+    if (int rc = grow_dev(d, &S.d_ts, S.ts_cap, ntiles + nruns)) return rc;  // + one tile counter per run
 #ifdef FM_DEV_SWITCHES
     if (getenv("FM_JPEG_STAMPS")) {
         if (int rc = grow_dev(d, &d->d_stamps, d->stamps_cap, ntiles * 6)) return rc;
@@ -1593,15 +1610,13 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
         JHIP(d, hipMemsetAsync(d->d_stamps, 0, ntiles * 6 * sizeof(uint64_t), st));
     }
 #endif
-    size_t tcap = d->tabs_cap;
-    if (int rc = grow_dev(d, &d->d_tabs, tcap, (size_t)nruns * 4)) return rc;
-    d->tabs_cap = (int)tcap;
-    JHIP(d, hipMemcpyAsync(d->d_stream, H.stream, w, hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_segs, H.segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_chunk0, H.chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemsetAsync(d->d_ts, 0, (ntiles + nruns) * sizeof(TileState), st));  // flags + the tile counters
-    JHIP(d, hipMemcpyAsync(d->d_tabs, H.tabs, (size_t)nruns * 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
-    JHIP(d, hipMemcpyAsync(d->d_qt, H.qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
+    if (int rc = grow_dev(d, &S.d_tabs, S.tabs_cap, (size_t)nruns * 4)) return rc;
+    JHIP(d, hipMemcpyAsync(S.d_stream, H.stream, w, hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(S.d_segs, H.segs, segs.size() * sizeof(Seg), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(S.d_chunk0, H.chunk0, ((size_t)nseg + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemsetAsync(S.d_ts, 0, (ntiles + nruns) * sizeof(TileState), st));  // flags + the tile counters
+    JHIP(d, hipMemcpyAsync(S.d_tabs, H.tabs, (size_t)nruns * 4 * sizeof(HuffDev), hipMemcpyHostToDevice, st));
+    JHIP(d, hipMemcpyAsync(S.d_qt, H.qt, (size_t)n * kMaxComp * 64 * sizeof(uint16_t), hipMemcpyHostToDevice, st));
     JHIP(d, hipEventRecord(H.done, st));
     H.used = true;
     d->cur ^= 1;
@@ -1622,10 +1637,10 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
             gr.ucomp2 |= (uint32_t)c << (2 * u);
         }
         hipLaunchKernelGGL(k_jpeg_huff, dim3((unsigned)((nt + kHuffWaves - 1) / kHuffWaves)), dim3(64 * kHuffWaves), 0, st,
-                           d->d_stream, (uint32_t)w, d->d_segs + run_seg[r], run_seg[r + 1] - run_seg[r],
-                           d->d_chunk0 + run_seg[r], (int)run_chunk[r], (int)run_end[r], d->d_tabs + 4 * r, gr,
-                           d->CB, d->OV, d->d_ts + run_tile[r], reinterpret_cast<uint32_t*>(d->d_ts + ntiles + r),
-                           d->d_coef, d->d_msk, d->d_stamps ? d->d_stamps + 6 * run_tile[r] : nullptr);
+                           S.d_stream, (uint32_t)w, S.d_segs + run_seg[r], run_seg[r + 1] - run_seg[r],
+                           S.d_chunk0 + run_seg[r], (int)run_chunk[r], (int)run_end[r], S.d_tabs + 4 * r, gr,
+                           d->CB, d->OV, S.d_ts + run_tile[r], reinterpret_cast<uint32_t*>(S.d_ts + ntiles + r),
+                           S.d_coef, S.d_msk, d->d_stamps ? d->d_stamps + 6 * run_tile[r] : nullptr);
     }
     JHIP(d, hipGetLastError());
     const long long nb = (long long)n * g.frame_blocks;
@@ -1670,11 +1685,11 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     const long long nbi = (long long)n * ((long long)g.frame_blocks - skip);
     if (nbi > 0)
         hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nbi + 32 * kIdctGroups - 1) / (32 * kIdctGroups))), dim3(256), 0, st,
-                           d->d_coef, d->d_msk, d->d_qt, d->g, skip, (int)nbi, d->d_planes);
+                           S.d_coef, S.d_msk, S.d_qt, d->g, skip, (int)nbi, S.d_planes);
     {
         const dim3 cgrid((unsigned)((g.H + rb - 1) / rb), (unsigned)n);
 #define FM_JP_COLOR(M, F) \
-    hipLaunchKernelGGL((k_jpeg_color<M, F>), cgrid, dim3(256), lds, st, d->d_planes, d->g, rb, (int)ys_off, (int)ws_off, out, 0, d->d_coef, d->d_msk, d->d_qt)
+    hipLaunchKernelGGL((k_jpeg_color<M, F>), cgrid, dim3(256), lds, st, S.d_planes, d->g, rb, (int)ys_off, (int)ws_off, out, 0, S.d_coef, S.d_msk, S.d_qt)
         if (fuse) {
             if (mode == 3) FM_JP_COLOR(3, true);
             else if (mode == 2) FM_JP_COLOR(2, true);
@@ -1690,8 +1705,8 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     }
     JHIP(d, hipGetLastError());
     if (d->timing) JHIP(d, hipEventRecord(d->e1, st));
-    JHIP(d, hipEventRecord(d->last_ev, st));
-    d->last_st = st;
+    JHIP(d, hipEventRecord(S.done, st));
+    JHIP(d, hipStreamWaitEvent(cst, S.done, 0));
     return FM_OK;
 }
 
