@@ -264,8 +264,10 @@ double fm_mjpeg_last_ms(const fm_mjpeg* dec);
 /* The frame size, device and max_frames the decoder was created with. */
 int fm_mjpeg_geometry(const fm_mjpeg* dec, int* width, int* height, int* device, int* max_frames);
 /* fm_submit from compressed frames: n_frames x n_streams JPEGs in [t][s]
- * order, decoded by dec (created for this context's src_w x src_h) on the
- * context's input stream into the batch's device buffer, then processed as
+ * order, decoded by dec (created for this context's src_w x src_h) into the
+ * batch's device buffer -- on the decoder's own two streams, used in turn, so one
+ * batch's Huffman pass overlaps the previous batch's IDCT / colour kernels; the
+ * context's input stream waits for the decode -- then processed as
  * fm_submit (frames, n_frames, on_device = 1) would.  The host buffers may be
  * reused when the call returns.  FM_EINVAL (nothing enqueued) when dec was
  * created for another frame size or device, or for fewer than
