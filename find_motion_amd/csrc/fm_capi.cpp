@@ -894,7 +894,7 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // slot -> stream map put every fourth pair of consecutive chains on one stream, one after
         // the other (the last batch's chain waited ≈130 µs for its predecessor's)
 #ifndef FM_CCL_ROTATE
-#define FM_CCL_ROTATE 1
+#define FM_CCL_ROTATE 0  // rotation: +2 % on one box, equal on another (369.9 vs 369.0 k, 5 rounds) with 8 % longer pixel launches: off
 #endif
         if (FM_CCL_ROTATE) {
             B.ccl_stream = c->ccl_streams[c->ccl_next];
