@@ -175,7 +175,7 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
 }
 
 #ifndef FM_CCL_DPP_SCAN
-#define FM_CCL_DPP_SCAN 0  // DPP scans: neutral at 20 steps, -1 % at 60 (398-402 k vs 403-407 k, 4 alternating rounds)
+#define FM_CCL_DPP_SCAN 1  // with raised contour priorities -1 % at 60 steps; at priority 0 +1.5 % (373.0 vs 367.6 k, 4 rounds)
 #endif
 // Wave-wide inclusive prefix sum by DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then
 // row_bcast 15 / 31 across rows): six VALU adds, where a __shfl_up loop is six ds_bpermute
