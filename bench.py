@@ -24,6 +24,9 @@ import os
 import sys
 import time
 
+# the package's default (find_motion_amd/__init__.py), set before torch makes the first HIP call
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

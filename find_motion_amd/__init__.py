@@ -8,6 +8,15 @@ through the C ABI in include/find_motion_amd.h; there is no CPU fallback.
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# Hardware queues per process: HIP's default of 4 puts the decoder's two streams, the contour
+# streams and the input / aux streams on shared queues (a shared queue runs its packets in order);
+# with 8 every stream the engine and the MJPEG decoder use has a queue of its own (MJPEG-fed
+# pipeline 72-73 k -> 79-81 k frames/s, the device-resident figure unchanged).
+# Only effective when this is imported before the process's first HIP call.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 from ._native import (  # noqa: F401
     CascadeClassifier,
     Contour,
