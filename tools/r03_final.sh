@@ -14,6 +14,6 @@ tail -1 gpurun_out/bench_$TAG.log | cut -c1-600
 tools/profile.sh $TAG --steps 20 --warmup 5 || exit 1
 python tools/pmc_summary.py gpurun_out/prof_$TAG > gpurun_out/pmc_$TAG.txt 2>&1
 echo "final $TAG done"
-C5="--width 3840 --height 2160 --blur-scale 183 --streams 4 --batch 64 --ring 64 --ring-period 16 --steps 10 --warmup 3"
+C5="--width 3840 --height 2160 --blur-scale 183 --streams 4 --batch 64 --ring 64 --ring-period 16 --steps 20 --warmup 10"
 timeout -k 10 300 python bench.py $C5 --no-cpu-baseline --no-host-fed --no-mjpeg > gpurun_out/bench_${TAG}_c5.log 2>&1 || { tail -5 gpurun_out/bench_${TAG}_c5.log; exit 1; }
 tail -1 gpurun_out/bench_${TAG}_c5.log | cut -c1-300
