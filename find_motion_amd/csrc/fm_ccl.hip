@@ -333,6 +333,10 @@ __device__ __forceinline__ int run_at(int base, uint64_t starts, int p) {
 
 enum : int { TCCL_OK = 0, TCCL_RUNS = 1, TCCL_NODES = 2 };
 
+#ifndef FM_CCL_FULL
+#define FM_CCL_FULL 1  // fully set tiles take a closed-form record (no run labelling)
+#endif
+
 // the tile's node ids: n consecutive ids from its frame's quota (one counter per frame, so
 // the tiles of different frames never contend on one atomic), or past the quota from the
 // slot's shared overflow pool; -1 (TCCL_NODES) when that is exhausted too: the frame is
@@ -385,6 +389,31 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             nrec.parent = nb;
             nrec.flags = outer ? 2u : 0u;
             nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+            a.nodes[nb] = nrec;
+        }
+        return TCCL_OK;
+    }
+    // full tile (every pixel set after dilation; tiles cut by the image edge never are): one
+    // foreground component whose root is run 0 = row 0, columns 0..63, and no background -- what the
+    // labelling below ends with after its ~7 pointer-jumping rounds over the 64-run chain
+    if (FM_CCL_FULL && __ballot(m != ~0ull) == 0) {
+        const int nb = take_nodes(a, f, 1, ln);
+        if (nb < 0) return TCCL_NODES;
+        TR->edges[ln] = 0x8000u;
+        TR->edges[64 + ln] = 0x8000u;
+        TR->edges[128 + ln] = 0x8000u;
+        TR->edges[192 + ln] = 0x8000u;
+        if (ln == 0) {
+            TR->nroots = 1;
+            TR->nbase = nb;
+            NodeRec nrec;
+            nrec.key = ((uint64_t)(uint32_t)(y0 * w + x0) << 32) | (x0 == 0 ? REF_OUTER : REF_EDGE);
+            nrec.parent = nb;
+            nrec.flags = 1u;
+            nrec.minx = x0;
+            nrec.maxx = x0 + TS - 1;
+            nrec.maxy = y0 + TS - 1;
+            nrec.pad = 0;
             a.nodes[nb] = nrec;
         }
         return TCCL_OK;

@@ -168,6 +168,32 @@ def test_heavy_tiles_stripes_and_rings():
     run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
 
 
+@pytest.mark.parametrize("k", [1, 5])
+@pytest.mark.parametrize("W,H", [(320, 256), (300, 204)])
+def test_full_tiles(W, H, k):
+    """Tiles whose dilated mask is all set take the contour pass's closed-form record: full tiles on
+    the left image edge (outer reference) and inside the image (edge reference), next to holes,
+    diagonal neighbours, a whole-frame foreground (edge tiles cut by the image never count as full)."""
+    pats = []
+    p = np.zeros((H, W), bool)
+    p[10:H - 6, 0:W - 20] = True
+    p[100:120, 150:170] = False                 # a hole inside the block ...
+    p[110, 160] = True                          # ... with a dot in it
+    pats.append(p)
+    pats.append(np.ones((H, W), bool))
+    p = np.zeros((H, W), bool)
+    p[2:62, 2:62] = True                        # dilates to exactly tile (0, 0)
+    p[66:126, 66:126] = True                    # and tile (1, 1): corner-to-corner neighbours
+    p[130:190, 200:W - 1] = True
+    pats.append(p)
+    p = np.zeros((H, W), bool)
+    p[64:192, 64:256] = True                    # full tiles away from the image edge
+    p[5, 5] = True
+    pats.append(p)
+    frames = _pattern_frames(pats)
+    run_pair(W, H, W, ksize=k, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
+
+
 # --- committed golden fixtures through the C ABI -------------------------------
 
 from golden_cases import boxes_of, chain_files, contour_cases, load_chain, origins_of  # noqa: E402
