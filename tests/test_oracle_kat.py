@@ -13,6 +13,7 @@ The reference has no tests and OpenCV is not installed here (SURVEY.md §4,
 Each test names the reference call site (fm.py = find_motion/find_motion.py).
 CPU only.
 """
+import math
 from fractions import Fraction
 
 import numpy as np
@@ -63,6 +64,57 @@ def test_gauss_taps_all_odd_sizes_sum_256_symmetric_and_match_numpy():
         assert (c == c[::-1]).all(), k
         assert (c >= 0).all(), k
         assert c.tolist() == onp.gauss_coeffs(k).tolist(), k
+
+
+def _gauss_taps_variant(k, exp_ulps, sigma_ulps=0, reciprocal=False):
+    """getGaussianKernelBitExact + the 8-bit error-diffusion rounding (smooth.dispatch.cpp), with
+    every exp() result moved by exp_ulps[i] ulps, sigma by sigma_ulps, and the normalisation by a
+    division or by a multiply with 1/sum.  Everything but exp is IEEE-exact (softdouble and the
+    hardware double give the same bits); exp is the one function whose last bit may differ."""
+    def step(v, u):
+        for _ in range(abs(u)):
+            v = float(np.nextafter(v, np.inf if u > 0 else -np.inf))
+        return v
+    sigma = step(float(Fraction(k) * Fraction(0.15) + Fraction(0.35)), sigma_ulps)  # mulAdd, one rounding
+    s2 = -0.125 / (sigma * sigma)
+    n2 = (k - 1) // 2
+    vals = [step(math.exp(float(x * x) * s2), int(exp_ulps[i])) for i, x in enumerate(range(1 - k, 1 - k + 2 * n2, 2))]
+    tot = 0.0
+    for v in vals:
+        tot += v
+    tot = tot * 2.0 + 1.0
+    if reciprocal:
+        m = 1.0 / tot
+        kd = [v * m for v in vals]
+    else:
+        kd = [v / tot for v in vals]
+    out, err, s = [0] * k, 0.0, 0
+    for i in range(k // 2):
+        adj = kd[i] * 256.0 + err
+        v0 = round(adj)
+        err = adj - v0
+        out[i] = out[k - 1 - i] = v0
+        s += v0
+    out[k // 2] = 256 - 2 * s
+    return out
+
+
+def test_gauss_taps_do_not_depend_on_the_exp_implementation():
+    """Pins the k > 9 taps (k = 21 at config 5, 97 / 193 with the CLI's default blur scale) without
+    OpenCV: the oracle uses libm exp, OpenCV softdouble's exp; both are within an ulp of the true
+    value.  Moving every exp result by up to 4 ulps (all together or independently at random), sigma
+    by an ulp, or normalising by 1/sum instead of a division leaves every 8-bit tap of every odd
+    k in 11..255 unchanged, so the restatement's taps are OpenCV's."""
+    rng = np.random.default_rng(0)
+    for k in range(11, 256, 2):
+        ref = oracle.gauss_coeffs(k).tolist()
+        n2 = (k - 1) // 2
+        trials = [np.full(n2, d) for d in (-4, -1, 1, 4)] + [rng.integers(-4, 5, n2) for _ in range(6)]
+        for u in trials:
+            assert _gauss_taps_variant(k, u) == ref, (k, u.tolist())
+            assert _gauss_taps_variant(k, u, reciprocal=True) == ref, (k, "1/sum", u.tolist())
+        for su in (-1, 1):
+            assert _gauss_taps_variant(k, np.zeros(n2, int), sigma_ulps=su) == ref, (k, "sigma", su)
 
 
 def test_gauss_even_size_rejected():
