@@ -706,23 +706,46 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
 #ifndef FM_CCL_NVGPR
 #define FM_CCL_NVGPR 0  // cap on k_tile_ccl's VGPRs (0: none), so more of its waves fit beside the pixel kernel's
 #endif
+#ifndef FM_CCL_WPE
+#define FM_CCL_WPE 6  // k_tile_ccl compiled for 6 waves per SIMD: 80 VGPRs (was 96, no spills), so two of its
+                      // workgroups fit beside two k_pix5 workgroups (4 x 88 VGPRs per SIMD): +1.2 %, 4 rounds
+#endif
 #if FM_CCL_NVGPR
 #define FM_CCL_ATTR __attribute__((amdgpu_num_vgpr(FM_CCL_NVGPR)))
+#elif FM_CCL_WPE
+#define FM_CCL_ATTR __attribute__((amdgpu_waves_per_eu(FM_CCL_WPE)))
 #else
 #define FM_CCL_ATTR
 #endif
+// scratch as dynamic LDS (FM_CCL_DYN): the compiler then takes its occupancy from FM_CCL_WPE, not
+// from a static 30 KB (see k_tile_heavy)
+#ifndef FM_CCL_DYN
+#define FM_CCL_DYN 1
+#endif
+constexpr size_t TC_WAVE_LDS = ((size_t)(6 * LIGHT + 66) * 4 + 2 * LIGHT + 3 * LIGHT + 15) / 16 * 16;
+constexpr size_t TC_LDS = CW * TC_WAVE_LDS;
 template <bool DILATE>
 __global__ __launch_bounds__(64 * CW) FM_CCL_ATTR void k_tile_ccl(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#if FM_CCL_DYN
+    // per wave: par, amin, amax, ay, pairs (u32), rb | ord (u16) | rx0, rx1, rf (u8)
+    extern __shared__ __attribute__((aligned(16))) int tc_lds[];
+    int* wb = tc_lds + (size_t)wv * (TC_WAVE_LDS / 4);
+    uint16_t* word = reinterpret_cast<uint16_t*>(wb + 6 * LIGHT + 66);
+    uint8_t* wbyte = reinterpret_cast<uint8_t*>(word + LIGHT);
+    const Scratch sc{wb, wb + LIGHT, wb + 2 * LIGHT, wb + 3 * LIGHT, wbyte, wbyte + LIGHT, wbyte + 2 * LIGHT,
+                     wb + 6 * LIGHT, word, reinterpret_cast<uint32_t*>(wb + 4 * LIGHT)};
+#else
     __shared__ int par[CW][LIGHT], amin[CW][LIGHT], amax[CW][LIGHT], ay[CW][LIGHT];
     __shared__ uint8_t rx0[CW][LIGHT], rx1[CW][LIGHT], rf[CW][LIGHT];
     __shared__ uint16_t ord[CW][LIGHT];
     __shared__ uint32_t pairs[CW][2 * LIGHT];
     __shared__ int rb[CW][66];
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
+#endif
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     const int nc = a.ncr[2 * f];
-    const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
     if (FM_OOB(a, nc >= 0 && nc <= a.ntiles, 1)) return;
     if (FM_CCL_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_PRIO);
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
@@ -757,12 +780,44 @@ constexpr int NHW = kHeavyWaves;
 #ifndef FM_HEAVY_WPE
 #define FM_HEAVY_WPE 1
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FM_HEAVY_WPE))) void k_tile_heavy(FusedArgs a) {
+#ifndef FM_HEAVY_NVGPR
+#define FM_HEAVY_NVGPR 0  // explicit VGPR budget of k_tile_heavy (0: the compiler's)
+#endif
+#if FM_HEAVY_NVGPR
+#define FM_HEAVY_ATTR __attribute__((amdgpu_num_vgpr(FM_HEAVY_NVGPR)))
+#else
+#define FM_HEAVY_ATTR
+#endif
+// The scratch is dynamic LDS: with a static 46 KB the compiler derives an occupancy of one wave per
+// SIMD from the LDS alone and then sizes the kernel's VGPR allocation for that occupancy (264
+// registers for 67 used), which no CU holding two k_pix5 workgroups (4 waves x 88 VGPRs per SIMD)
+// can fit: every batch's heavy tiles then waited for the pixel kernel to end (trace r03h: 300-370 us
+// beside it, 26 us alone).  Sized at launch, the allocation is what the code uses.
+#ifndef FM_HEAVY_DYN
+#define FM_HEAVY_DYN 1
+#endif
+constexpr int HV_INT = 4 * MAXR + 2 * MAXR + 68;   // par, amin, amax, ay | pairs (u32) | rb
+constexpr size_t HEAVY_LDS = (size_t)HV_INT * 4 + 3 * MAXR + 2 * MAXR;  // + rx0, rx1, rf (u8), ord (u16)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FM_HEAVY_WPE))) FM_HEAVY_ATTR void k_tile_heavy(FusedArgs a) {
+#if FM_HEAVY_DYN
+    extern __shared__ __attribute__((aligned(16))) int hv_lds[];
+    int* par = hv_lds;
+    int* amin = par + MAXR;
+    int* amax = amin + MAXR;
+    int* ay = amax + MAXR;
+    uint32_t* pairs = reinterpret_cast<uint32_t*>(ay + MAXR);
+    int* rb = reinterpret_cast<int*>(pairs + 2 * MAXR);
+    uint16_t* ord = reinterpret_cast<uint16_t*>(rb + 68);
+    uint8_t* rx0 = reinterpret_cast<uint8_t*>(ord + MAXR);
+    uint8_t* rx1 = rx0 + MAXR;
+    uint8_t* rf = rx1 + MAXR;
+#else
     __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
     __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
     __shared__ uint16_t ord[MAXR];
     __shared__ uint32_t pairs[2 * MAXR];
     __shared__ int rb[68];
+#endif
     const size_t F = (size_t)a.T * a.S;
     const int n = a.count[2 * F + 1];
     const int ln = threadIdx.x;
@@ -1117,9 +1172,9 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), rg_lds, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("tile_ccl", st) : -1;
-    if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), 0, st, a);
-    else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), 0, st, a);
-    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), 0, st, a);
+    if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
+    else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
+    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), FM_HEAVY_DYN ? cc::HEAVY_LDS : 0, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
