@@ -65,7 +65,7 @@ struct BatchSlot {
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
-    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr;
+    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr, ev_lab = nullptr;  // ev_lab: labelling done
     hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
     FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
@@ -86,6 +86,7 @@ struct fm_ctx {
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
     hipStream_t rs_stream = nullptr;  // input stream: host copies + resize, ahead of the pixel stream
     hipStream_t ccl_streams[kSlots] = {};
+    int lab_prev = -1;  // slot of the last batch whose labelling was enqueued (FM_CCL_GATE)
     int nccl = 1;
     int ccl_next = 0;  // the next batch's contour stream
     KernelTimer timer;
@@ -575,6 +576,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_rs, hipEventDisableTiming));
+        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_lab, hipEventDisableTiming));
     }
     // pixel-level CCL: the whole batch on the v1 path, one frame for the fused path's overflow fallback
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
@@ -661,6 +663,7 @@ void fm_destroy(fm_ctx* c) {
         if (b.ev_pix) (void)hipEventDestroy(b.ev_pix);
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
+        if (b.ev_lab) (void)hipEventDestroy(b.ev_lab);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_one); dfree(c->d_rec_all); dfree(c->d_area);
@@ -893,6 +896,9 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // consecutive batches on different contour streams: with 4 slots on 3 streams a fixed
         // slot -> stream map put every fourth pair of consecutive chains on one stream, one after
         // the other (the last batch's chain waited ≈130 µs for its predecessor's)
+#ifndef FM_CCL_GATE
+#define FM_CCL_GATE 1  // +1.5 % (388.1 vs 382.3 k, 4 alternating rounds, tools/r03_call4.sh)
+#endif
 #ifndef FM_CCL_ROTATE
 #define FM_CCL_ROTATE 0  // rotation: +2 % on one box, equal on another (369.9 vs 369.0 k, 5 rounds) with 8 % longer pixel launches: off
 #endif
@@ -903,7 +909,12 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         hipStream_t cs = c->serial ? ps : B.ccl_stream;
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
         HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
-        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer));  // counts land in mapped h_count / h_overflow
+        // FM_CCL_GATE: one batch's labelling kernel at a time (the previous batch's, on another contour
+        // stream, is waited for), so the labelling of consecutive chains never bunches beside a pixel launch
+        hipEvent_t gate_wait = nullptr;
+        if (FM_CCL_GATE && !c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
+        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, FM_CCL_GATE ? B.ev_lab : nullptr));
+        c->lab_prev = si;  // counts land in mapped h_count / h_overflow
         B.fa = fa;
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));
     } else {

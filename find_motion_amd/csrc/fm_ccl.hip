@@ -1162,7 +1162,8 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
     return hipGetLastError();
 }
 
-hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm) {
+hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm, hipEvent_t gate_wait,
+                           hipEvent_t gate_done) {
     if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;
     const unsigned F = (unsigned)(a.T * a.S);
     const dim3 gf(cc::GW, F);
@@ -1171,9 +1172,17 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), rg_lds, st, a);
     else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), rg_lds, st, a);
     if (tm) tm->end(tok);
+    if (gate_wait) {
+        const hipError_t e = hipStreamWaitEvent(st, gate_wait, 0);
+        if (e != hipSuccess) return e;
+    }
     tok = tm ? tm->begin("tile_ccl", st) : -1;
     if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
     else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
+    if (gate_done) {
+        const hipError_t e = hipEventRecord(gate_done, st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), FM_HEAVY_DYN ? cc::HEAVY_LDS : 0, st, a);
     if (tm) tm->end(tok);
     tok = tm ? tm->begin("merge", st) : -1;
