@@ -46,8 +46,9 @@ constexpr int MAXR = kTileMaxRuns;
 constexpr int LIGHT = FM_CCL_LIGHT;  // runs held by the light pass
 constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k_merge
 #ifndef FM_CCL_GW
-#define FM_CCL_GW 8  // measured: 8 > 16 > 32 > 4 (r02: 266k vs 262k vs 251k vs 257k frames/s at the bench default);
-                     // re-checked at v21 (batch 192, raised priorities), 3 alternating rounds: 8 382k, 6 381k, 16 370k
+#define FM_CCL_GW 4  // measured: 8 > 16 > 32 > 4 (r02: 266k vs 262k vs 251k vs 257k frames/s at the bench default);
+                     // re-checked at v21 (batch 192, raised priorities), 3 alternating rounds: 8 382k, 6 381k, 16 370k;
+                     // with the labelling gate (round 3): 4 392.3k, 6 389.0k, 8 388.4k (4 alternating rounds)
 #endif
 constexpr int GW = FM_CCL_GW;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
 constexpr int RG = 512;         // k_regions threads
