@@ -37,7 +37,8 @@ enum class ResizeMode { Identity, Fast, General };
 // contour passes of consecutive batches overlap each other and the next
 // batches' pixel kernels.
 #ifndef FM_SLOTS
-#define FM_SLOTS 4
+#define FM_SLOTS 6  // with the labelling gate a chain finishes later, and 4 slots left the pixel stream idle
+                    // while the host waited to reuse one: 6 slots 406.4 vs 396.4 k frames/s (4 alternating rounds)
 #endif
 constexpr int kSlots = FM_SLOTS;
 struct BatchSlot {
@@ -65,7 +66,7 @@ struct BatchSlot {
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
-    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr, ev_lab = nullptr;  // ev_lab: labelling done
+    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr, ev_lab = nullptr, ev_mrg = nullptr;  // labelling / merge done
     hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
     FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
@@ -577,6 +578,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_rs, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_lab, hipEventDisableTiming));
+        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_mrg, hipEventDisableTiming));
     }
     // pixel-level CCL: the whole batch on the v1 path, one frame for the fused path's overflow fallback
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
@@ -664,6 +666,7 @@ void fm_destroy(fm_ctx* c) {
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
         if (b.ev_lab) (void)hipEventDestroy(b.ev_lab);
+        if (b.ev_mrg) (void)hipEventDestroy(b.ev_mrg);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_one); dfree(c->d_rec_all); dfree(c->d_area);
@@ -899,6 +902,9 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
 #ifndef FM_CCL_GATE
 #define FM_CCL_GATE 1  // +1.5 % (388.1 vs 382.3 k, 4 alternating rounds, tools/r03_call4.sh)
 #endif
+#ifndef FM_MERGE_GATE
+#define FM_MERGE_GATE 0
+#endif
 #ifndef FM_CCL_ROTATE
 #define FM_CCL_ROTATE 0  // rotation: +2 % on one box, equal on another (369.9 vs 369.0 k, 5 rounds) with 8 % longer pixel launches: off
 #endif
@@ -913,7 +919,10 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // stream, is waited for), so the labelling of consecutive chains never bunches beside a pixel launch
         hipEvent_t gate_wait = nullptr;
         if (FM_CCL_GATE && !c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
-        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, FM_CCL_GATE ? B.ev_lab : nullptr));
+        hipEvent_t mgate_wait = nullptr;  // FM_MERGE_GATE: the merge kernels likewise
+        if (FM_MERGE_GATE && !c->serial && c->lab_prev >= 0 && c->lab_prev != si) mgate_wait = c->slots[c->lab_prev].ev_mrg;
+        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, FM_CCL_GATE ? B.ev_lab : nullptr, mgate_wait,
+                                   FM_MERGE_GATE ? B.ev_mrg : nullptr));
         c->lab_prev = si;  // counts land in mapped h_count / h_overflow
         B.fa = fa;
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));

@@ -1164,7 +1164,7 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
 }
 
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm, hipEvent_t gate_wait,
-                           hipEvent_t gate_done) {
+                           hipEvent_t gate_done, hipEvent_t mgate_wait, hipEvent_t mgate_done) {
     if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;
     const unsigned F = (unsigned)(a.T * a.S);
     const dim3 gf(cc::GW, F);
@@ -1186,9 +1186,17 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     }
     hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), FM_HEAVY_DYN ? cc::HEAVY_LDS : 0, st, a);
     if (tm) tm->end(tok);
+    if (mgate_wait) {
+        const hipError_t e = hipStreamWaitEvent(st, mgate_wait, 0);
+        if (e != hipSuccess) return e;
+    }
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
     if (tm) tm->end(tok);
+    if (mgate_done) {
+        const hipError_t e = hipEventRecord(mgate_done, st);
+        if (e != hipSuccess) return e;
+    }
     tok = tm ? tm->begin("fold_emit", st) : -1;
     hipLaunchKernelGGL(cc::k_fold, gf, dim3(64 * cc::CW), 0, st, a);
     hipLaunchKernelGGL(cc::k_emit, gf, dim3(64 * cc::CW), 0, st, a);

@@ -176,7 +176,8 @@ bool pix_supported(int ksize);
 // gate_wait / gate_done (optional): the labelling kernel waits for gate_wait (the previous batch's
 // labelling) and gate_done is recorded after it, so that one batch's labelling runs at a time
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer,
-                           hipEvent_t gate_wait = nullptr, hipEvent_t gate_done = nullptr);
+                           hipEvent_t gate_wait = nullptr, hipEvent_t gate_done = nullptr,
+                           hipEvent_t mgate_wait = nullptr, hipEvent_t mgate_done = nullptr);
 // every external-contour record of frame f of a finished batch (all of them, unlike the
 // capped k_emit), into rec [cap][5]; *cnt must be 0 before
 hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap);
