@@ -8,7 +8,7 @@ allows, so full-size sequences finish in seconds).
   k_pix<5, false, false> (no planes kept), fm_max_inflight batches submitted
   before the first wait, a ring wrap onto reused batch slots;
 * configs[2]: 8 x 1080p streams on one GPU, batches in flight -- also at the
-  perf shape quoted for it (T = 128 per launch, 4 in flight, device ring);
+  perf shape quoted for it (T = 128 per launch, 4 in flight, 7 batches on 6 slots, device ring);
 * configs[4] geometry: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the two
   MASK_SCHEMA polygons (find_motion.py:86-100) -- also at its perf shape
   (T = 64, 2 in flight);
@@ -46,7 +46,7 @@ def _check_frame(eng, res, t, s, f, tag, mask=True):
 def test_bench_shape_inflight_ring_wrap():
     """bench.py's exact workload through the production kernel, against the oracle on every frame."""
     torch = pytest.importorskip("torch")
-    W, H, T, NB = 1920, 1080, 128, 6
+    W, H, T = 1920, 1080, 128
     uniq = batch(W, H, 1, 0, 64)                      # bench: 64 synthetic frames cycled through a 128 ring
     ring_h = np.concatenate([uniq, uniq])              # [128][1][H][W][3]
     ring = torch.from_numpy(ring_h).to("cuda:0")
@@ -55,7 +55,8 @@ def test_bench_shape_inflight_ring_wrap():
     assert not eng.keep_planes
     orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=5))
     depth = eng.max_inflight
-    assert depth == 4
+    assert depth == 6
+    NB = depth + 2                                     # two batches onto reused slots
     for b in range(depth):
         eng.submit_device(ring.data_ptr(), T)
     total = 0
@@ -104,9 +105,9 @@ def _run_streams(W, H, box, k, S, T, NB, masks=None, start=0, mask_every=7, thre
 
 
 def test_config3_eight_1080p_streams_inflight():
-    """configs[2]: 8 x 1080p streams batched on one GPU, per-stream background, 5 batches of 8 frames
-    (4 in flight, one slot reused)."""
-    _run_streams(1920, 1080, 1920, 5, S=8, T=8, NB=5, start=40, threads=2)
+    """configs[2]: 8 x 1080p streams batched on one GPU, per-stream background, 7 batches of 8 frames
+    (6 in flight, one slot reused)."""
+    _run_streams(1920, 1080, 1920, 5, S=8, T=8, NB=7, start=40, threads=2)
 
 
 def test_config5_four_4k_streams_k21_masks():
@@ -163,8 +164,9 @@ def _run_ring(W, H, box, k, S, T, NB, depth, period, masks=None, mask_every=23, 
 @pytest.mark.timeout(400)
 def test_config3_perf_shape_eight_streams_t128():
     """configs[2] at the shape its throughput is quoted on (bench.py --streams 8 --batch 128): 8 x 1080p
-    streams, 128 frames per stream per launch, 4 batches in flight, 5 batches (slot reuse)."""
-    _run_ring(1920, 1080, 1920, 5, S=8, T=128, NB=5, depth=4, period=64)
+    streams, 128 frames per stream per launch, 4 batches in flight, 7 batches (the 6 slots used round-robin:
+    the last batch reuses the first's slot)."""
+    _run_ring(1920, 1080, 1920, 5, S=8, T=128, NB=7, depth=4, period=64)
 
 
 @pytest.mark.timeout(400)

@@ -326,10 +326,10 @@ def test_batches_in_flight_match_sequential():
                        keep_planes=True)
     cfg = oracle.OracleConfig(H=H, W=W, box=W, ksize=5)
     orc = [oracle.OracleStream(cfg) for _ in range(S)]
-    NB = 6
-    batches = [batch(W, H, S, 90 + T * b, T) for b in range(NB)]
     depth = eng.max_inflight
     assert depth >= 2
+    NB = depth + 2  # the last two batches reuse slots
+    batches = [batch(W, H, S, 90 + T * b, T) for b in range(NB)]
     for b in range(depth):
         eng.submit(batches[b])
     with pytest.raises(Exception):
