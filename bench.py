@@ -225,10 +225,12 @@ def main() -> None:
     ap.add_argument("--blur-scale", type=int, default=None,
                     help="-b override (config 5: --width 3840 --height 2160 --blur-scale 183 -> k 21)")
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU")
-    # 192 frames per launch: measured best at the bench shape (r02: 64 326k, 128 357k, 160 368k, 192 376k,
-    # 224 364k, 256 375k frames/s) -- each batch boundary costs a pixel-kernel tail and a dependent launch
-    ap.add_argument("--batch", type=int, default=192, help="frames per stream per step (one pixel-kernel launch)")
-    ap.add_argument("--ring", type=int, default=192, help="device-resident frames per stream")
+    # 256 frames per launch: r02 (60 steps) 64 326k, 128 357k, 160 368k, 192 376k, 224 364k, 256 375k frames/s;
+    # round 3 with the labelling gate and 6 slots at the driver's 20 steps, 3 alternating rounds: 192 396.3k,
+    # 256 412.3k, 320 415.0k -- each batch boundary costs a pixel-kernel tail and a dependent launch, and the
+    # last batch's contour chain after the last pixel launch is a smaller share of 20 longer steps
+    ap.add_argument("--batch", type=int, default=256, help="frames per stream per step (one pixel-kernel launch)")
+    ap.add_argument("--ring", type=int, default=256, help="device-resident frames per stream")
     ap.add_argument("--ring-period", type=int, default=64,
                     help="synthetic frames in the ring's cycle: ring slot t holds frame t %% period")
     ap.add_argument("--cpu-frames", type=int, default=16)
