@@ -423,7 +423,9 @@ def main() -> None:
     # page-locked batches, fm_max_inflight batches in flight, every batch waited and its contours read.
     # PCIe-inclusive, so it is reported beside `value`, never as it.
     host_fed = None
-    if not args.no_host_fed:
+    # per-GPU figure, measured in the 1-GPU run only: every rank would page-lock (depth + 2) batches of
+    # T frames (≈12.7 GB at 6 slots x 256 frames of 1080p), ≈100 GB of pinned host memory on an 8-GPU node
+    if not args.no_host_fed and world == 1:
         from find_motion_amd import videoio
         from find_motion_amd.feeder import BatchFeeder
 
