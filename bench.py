@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+PCIE_GBS = 63.0  # PCIe Gen5 x16, one direction
 METRIC = "frames/sec on 1080p synthetic video at 1/2/4/8 MI355X; achieved HBM GB/s %peak"
 
 
@@ -50,6 +51,26 @@ def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
     if kernel in ("resize_area", "resize_area_fast"):
         return S * T * (H * W * 3 + h * w * 3)
     return None
+
+
+def moved_bytes(kernel: str, cfg: dict) -> float | None:
+    """Bytes ONE launch of the pixel kernel must move as it is built (not §8(d)'s accounting): the BGR
+    read (3 B/px-frame), the threshold bits it writes instead of a u8 mask (1/8 B/px-frame), 32 B of tile
+    flags per 64x64 tile-frame, and the f64 background read + written once per launch (16 B/px)."""
+    if kernel not in ("fused", "pix"):
+        return None
+    S, T, h, w = cfg["streams_per_gpu"], cfg["frames_per_step"], cfg["h"], cfg["w"]
+    tiles = ((h + 63) // 64) * ((w + 63) // 64)
+    return S * T * (h * w * (3 + 1 / 8) + tiles * 32) + S * h * w * 16
+
+
+def path_bytes_per_frame(cfg: dict) -> int:
+    """SURVEY.md §8(d) algorithmic bytes of the whole path per frame: mode D 3·W·H + 17·h·w (BGR frame read,
+    resized image, mask and the reference's per-frame f64 background traffic); mode F W·H·(4 + 16/T)."""
+    H, W, h, w, T = cfg["H"], cfg["W"], cfg["h"], cfg["w"], cfg["frames_per_step"]
+    if (h, w) != (H, W):
+        return 3 * W * H + 17 * h * w
+    return int(h * w * (4 + 16 / T))
 
 
 def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | None]:
@@ -143,7 +164,7 @@ def mjpeg_fed(eng, host: np.ndarray, T: int, S: int, quality: int = 75) -> dict 
     from find_motion_amd.feeder import BatchFeeder
     R, H, W = host.shape[0], host.shape[2], host.shape[3]
     enc = []
-    for t in range(min(R, 64)):
+    for t in range(min(R, 64)):  # host: the ring's distinct frames
         b = io.BytesIO()
         Image.fromarray(np.ascontiguousarray(host[t, 0][..., ::-1])).save(b, "JPEG", quality=quality)
         enc.append(b.getvalue())
@@ -280,20 +301,25 @@ def main() -> None:
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
            "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
 
-    # synthetic ring [R][S][H][W][3], distinct streams per rank (stream s -> rank s // S)
+    # synthetic ring [R][S][H][W][3] on the device, distinct streams per rank (stream s -> rank s // S):
+    # ring slot t holds synthetic frame t % P; only the P distinct frames exist on the host (at 8 streams a
+    # host copy of the whole ring would be 12.7 GB per rank)
+    P = max(1, min(args.ring_period, R))
     vids = [SyntheticVideo(W, H, stream=g) for g in dist.rank_streams(pl, S)]
-    host = np.empty((R, S, H, W, 3), np.uint8)
-    for t in range(R):
-        if t >= args.ring_period:  # the ring cycles the first ring_period synthetic frames
-            host[t] = host[t % args.ring_period]
-            continue
+    host = np.empty((P, S, H, W, 3), np.uint8)
+    for t in range(P):
         for s in range(S):
             host[t, s] = vids[s].frame(t)
-    ring = torch.from_numpy(host).to(f"cuda:{local}")
+    uniq = torch.from_numpy(host).to(f"cuda:{local}")
+    ring = torch.empty((R, S, H, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
+    for t in range(R):
+        ring[t].copy_(uniq[t % P])
+    del uniq
     frame_bytes = S * H * W * 3
 
     eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
                        max_batch=T, max_contours=1 << 14, profile=False if args.no_ktimes else True if args.all_ktimes else "pix", device=local)
+    footprint = dict(eng.footprint(), ring_bytes=R * frame_bytes)
     base = ring.data_ptr()
     n_batches = R // T
 
@@ -338,8 +364,12 @@ def main() -> None:
     total_frames = world * S * T * args.steps
     value = total_frames / elapsed
 
-    # roofline of the dominant kernel
+    # roofline of the dominant kernel; in mode D the INTER_AREA resize, the one kernel there that streams
+    # whole frames (the pixel kernel's 100 x 56 work image is two tiles: latency, not bandwidth)
     dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+    for rk in ("resize_area", "resize_area_fast"):
+        if rk in ktimes and ktimes[rk][1] > 0:
+            dom = rk
     roof = None
     kernels = {}
     for name, (ms, n) in ktimes.items():
@@ -357,6 +387,10 @@ def main() -> None:
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3)}
+            mv = moved_bytes(dom, cfg)
+            if mv is not None:  # the same launches priced on the bytes the kernel must move as built
+                roof["moved_bytes_per_launch"] = int(mv)
+                roof["frac_moved"] = round(mv / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             if traffic is not None:
                 roof["traffic_source"] = f"{tsrc}: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 16-B read correction)"
             if sq:
@@ -390,7 +424,7 @@ def main() -> None:
         # PCIe-inclusive rates (never `value`): pageable numpy batches, then page-locked
         # batches from the engine (asynchronous DMA on the input stream, overlapped with
         # the previous batches' kernels), pipelined like the device-resident loop
-        host_batch = np.ascontiguousarray(host[:T])
+        host_batch = np.ascontiguousarray(np.stack([host[t % P] for t in range(T)]))
         t0 = time.perf_counter()
         for _ in range(5):
             eng.submit(host_batch)
@@ -398,7 +432,8 @@ def main() -> None:
         hf = 5 * S * T / (time.perf_counter() - t0)
         pinned = [eng.host_buffer(T) for _ in range(min(depth, 2))]
         for k, pb in enumerate(pinned):
-            pb[:] = host[(k * T) % R:(k * T) % R + T]
+            for t in range(T):
+                pb[t] = host[(k * T + t) % P]
         n_hf = 8
 
         def run_pinned() -> None:
@@ -429,21 +464,28 @@ def main() -> None:
         from find_motion_amd import videoio
         from find_motion_amd.feeder import BatchFeeder
 
-        n_hf = max(4 * T, 256)
-        caps = [videoio.ArrayCapture([host[t % R, s] for t in range(n_hf)]) for s in range(S)]
-        warm = [videoio.ArrayCapture([host[t % R, s] for t in range(2 * T)]) for s in range(S)]
-        bufs = BatchFeeder.make_buffers(eng, T)  # page-locked once, outside the timed run
-        for _ in BatchFeeder(eng, warm, T, buffers=bufs):
+        # batches of Th frames per stream, 3 in flight + 2 being filled / consumed: at most ~3.2 GB
+        # page-locked (1080p: 128 frames x 1 stream, 16 x 8 streams)
+        Th = max(1, min(T, (128 * 1920 * 1080) // (S * H * W)))
+        depth_hf = min(3, eng.max_inflight)
+        n_hf = max(8 * Th, 512 // S)
+        caps = [videoio.ArrayCapture([host[t % P, s] for t in range(n_hf)]) for s in range(S)]
+        warm = [videoio.ArrayCapture([host[t % P, s] for t in range(2 * Th)]) for s in range(S)]
+        bufs = BatchFeeder.make_buffers(eng, Th, depth_hf)  # page-locked once, outside the timed run
+        for _ in BatchFeeder(eng, warm, Th, depth=depth_hf, buffers=bufs):
             pass
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ncont = 0
-        for b in BatchFeeder(eng, caps, T, buffers=bufs):
+        for b in BatchFeeder(eng, caps, Th, depth=depth_hf, buffers=bufs):
             ncont += int(eng.counts().sum())
         dt = time.perf_counter() - t0
-        host_fed = {"frames_per_s": round(n_hf * S / dt, 1), "gb_per_s": round(n_hf * S * H * W * 3 / dt / 1e9, 2),
-                    "frames": n_hf * S, "mode": "BatchFeeder: pre-decoded frames -> page-locked batches -> "
-                                                 "hipMemcpyAsync + kernels, fm_max_inflight in flight"}
+        gbs = n_hf * S * H * W * 3 / dt / 1e9
+        host_fed = {"frames_per_s": round(n_hf * S / dt, 1), "gb_per_s": round(gbs, 2),
+                    "pcie_frac": round(gbs / PCIE_GBS, 3), "frames": n_hf * S, "batch": Th, "in_flight": depth_hf,
+                    "pinned_bytes": int(len(bufs) * Th * S * H * W * 3),
+                    "mode": "BatchFeeder: pre-decoded frames -> page-locked batches -> hipMemcpyAsync + kernels"}
+        del bufs
 
     # MJPEG-fed (the decode side): the synthetic frames as baseline JPEGs (Pillow,
     # quality 75, 4:2:0, no restart markers), read by BatchFeeder in JPEG mode: compressed bytes parsed on
@@ -455,7 +497,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, host.reshape(R * S, H, W, 3), min(args.cpu_frames, R * S))
+        cpu = cpu_baseline(cfg, host.reshape(P * S, H, W, 3), min(args.cpu_frames, P * S))
 
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
@@ -463,7 +505,11 @@ def main() -> None:
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "host_fed_per_gpu": host_fed,
-               "mjpeg_fed_per_gpu": mjpeg,
+               "mjpeg_fed_per_gpu": mjpeg, "footprint_per_gpu": footprint,
+               "path_hbm": {"bytes_per_frame": path_bytes_per_frame(cfg),
+                            "achieved": round(value / world * path_bytes_per_frame(cfg) / 1e9, 1), "unit": "GB/s",
+                            "frac": round(value / world * path_bytes_per_frame(cfg) / 1e9 / HBM_PEAK_GBS, 4),
+                            "note": "whole-path frames/s per GPU x SURVEY.md §8(d) bytes per frame"},
                "contour_pass": {"heavy_tiles_per_batch": round(ccl["heavy_tiles"] / max(ccl["batches"], 1), 2),
                                 "shared_nodes_max": ccl["shared_nodes_max"],
                                 "fallback_frames": ccl["fallback_frames"]}}

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("FM_HIP_LIB", LIB_PATH)
 
 FM_OK, FM_EINVAL, FM_EHIP, FM_ENOMEM, FM_ESTATE, FM_ENOTSUP = 0, -1, -2, -3, -4, -5
 FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE, FM_FLAG_PROFILE_PIX, FM_FLAG_CONTOUR_AREA = 0x1, 0x2, 0x4, 0x8
-PLANE_GRAY, PLANE_BLUR, PLANE_DELTA = 0, 1, 2
+PLANE_GRAY, PLANE_BLUR, PLANE_DELTA, PLANE_SMALL = 0, 1, 2, 3
 
 EXPORTED = (
     "fm_abi_version", "fm_create", "fm_destroy", "fm_last_error", "fm_work_size", "fm_set_mask",
@@ -31,7 +31,7 @@ EXPORTED = (
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
     "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device", "fm_mjpeg_geometry",
-    "fm_submit_streams",
+    "fm_submit_streams", "fm_footprint",
 )
 
 
@@ -106,6 +106,7 @@ def load() -> C.CDLL:
     L.fm_max_inflight.argtypes = [vp]
     L.fm_last_fallbacks.argtypes = [vp]
     L.fm_last_ccl_stats.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
+    L.fm_footprint.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
     L.fm_haar_create.argtypes = [i32, C.POINTER(FMHaarDesc), C.POINTER(vp)]
     L.fm_haar_destroy.argtypes = [vp]
     L.fm_haar_destroy.restype = None
@@ -360,6 +361,12 @@ class MotionEngine:
         self._check(self._L.fm_last_ccl_stats(self._h, C.byref(a), C.byref(b)))
         return {"shared_nodes": a.value, "heavy_tiles": b.value}
 
+    def footprint(self) -> dict:
+        """Bytes the context holds: device memory and page-locked host memory (fm_footprint)."""
+        d, p = C.c_size_t(), C.c_size_t()
+        self._check(self._L.fm_footprint(self._h, C.byref(d), C.byref(p)))
+        return {"device_bytes": d.value, "pinned_bytes": p.value}
+
     def counts(self) -> np.ndarray:
         out = np.zeros((self.last_batch, self.n_streams), np.int32)
         self._check(self._L.fm_get_counts(self._h, _ptr(out)))
@@ -398,7 +405,8 @@ class MotionEngine:
         return int(p.value)
 
     def plane(self, which: int, frame: int, stream: int) -> np.ndarray:
-        out = np.empty(self.work_shape, np.uint8)
+        """gray / blur / frame_delta (h, w), or PLANE_SMALL: the resized BGR frame (h, w, 3) (fm.py:490)."""
+        out = np.empty(self.work_shape + ((3,) if which == PLANE_SMALL else ()), np.uint8)
         self._check(self._L.fm_read_plane(self._h, which, frame, stream, _ptr(out)))
         return out
 

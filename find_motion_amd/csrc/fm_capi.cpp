@@ -109,6 +109,9 @@ struct fm_ctx {
     size_t area_cap = 0;
     int32_t* d_rec_all = nullptr;  // k_emit_all records of one frame [rec_all_cap][5] + counter
     size_t rec_all_cap = 0;
+    int rec_cap = 0;          // records per frame in each slot's mapped buffer (the first fetch; more -> k_emit_all)
+    size_t dev_bytes = 0;     // fm_create's device allocations (fm_footprint)
+    size_t pinned_bytes = 0;  // and its page-locked host allocations
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;  // nnodes: per batch slot
@@ -246,7 +249,16 @@ int dalloc(fm_ctx* c, T** p, size_t count) {
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) return fail(c, FM_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+    if (c) c->dev_bytes += count * sizeof(T);
     return FM_OK;
+}
+
+// page-locked host memory of the context (counted for fm_footprint)
+template <class T>
+hipError_t halloc(fm_ctx* c, T** p, size_t bytes, unsigned flags) {
+    hipError_t e = hipHostMalloc((void**)p, bytes, flags);
+    if (e == hipSuccess) c->pinned_bytes += bytes;
+    return e;
 }
 
 template <class T>
@@ -369,7 +381,7 @@ namespace fm {
 int KernelTimer::begin(const char* name, hipStream_t st) {
     if (!enabled) return -1;
     if (!st) st = stream;
-    if (pixel_only && st != stream) return -1;
+    if (pixel_only && st != stream && st != stream2) return -1;
     int id = -1;
     for (size_t i = 0; i < names.size(); i++)
         if (names[i] == name || std::strcmp(names[i], name) == 0) id = (int)i;
@@ -504,6 +516,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
     c->timer.stream = c->stream;
+    c->timer.stream2 = c->rs_stream;
 
     const size_t S = p.n_streams, T = p.max_batch;
     c->work_plane = (size_t)c->h * c->w;
@@ -536,6 +549,15 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if (nn >= (size_t)INT32_MAX) return fail(nullptr, FM_ENOTSUP, "batch too large for 32-bit node ids (%zu)", nn);
         c->nnodes = (int)nn;
     }
+    // Contour records: the fused path's mapped buffer holds the first rec_cap records of each frame (a
+    // frame with more is re-emitted whole at fm_wait, so max_contours never changes the results): about
+    // 32 MB per slot however many frames a batch has -- [frames][max_contours] records of 20 B were 671 MB
+    // per slot at 8 streams x 256 frames and max_contours 1 << 14 (4 GB pinned per rank).  The per-frame
+    // path copies [frames][max_contours] records from the device and keeps that size.
+    c->rec_cap = p.max_contours;
+    if (c->use_fused)
+        c->rec_cap = (int)std::min<size_t>((size_t)p.max_contours,
+                                           std::max<size_t>(64, (size_t(32) << 20) / (frames * 5 * sizeof(int32_t))));
     for (int i = 0; i < c->nslots; i++) {
         BatchSlot& b = c->slots[i];
         if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &b.d_work, px * 3))) return rc;
@@ -554,16 +576,16 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         }
         // contour records: mapped pinned host memory written directly by the kernels
         // (only the records that exist cross PCIe)
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_rec, frames * p.max_contours * 5 * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, halloc(cp, &b.h_rec, frames * (size_t)c->rec_cap * 5 * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.d_rec, b.h_rec, 0));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_count, frames * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, halloc(cp, &b.h_count, frames * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_count, b.h_count, 0));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_overflow, frames * sizeof(int32_t), hipHostMallocMapped));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_stats, 2 * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, halloc(cp, &b.h_overflow, frames * sizeof(int32_t), hipHostMallocMapped));
+        HIP_TRY(cp, halloc(cp, &b.h_stats, 2 * sizeof(int32_t), hipHostMallocMapped));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_stats, b.h_stats, 0));
         HIP_TRY(cp, hipHostGetDevicePointer((void**)&b.dh_overflow, b.h_overflow, 0));
         if (b.d_tflag) HIP_TRY(cp, hipMemset(b.d_tflag, 0, frames * c->ntiles * 8 * sizeof(uint32_t)));
-        HIP_TRY(cp, hipHostMalloc((void**)&b.h_init, S));
+        HIP_TRY(cp, halloc(cp, &b.h_init, S, 0));
         if (i < c->nccl && ccl_qmode != 2) {
             if (ccl_qmode == 1) {
                 int lo = 0, hi = 0;
@@ -588,7 +610,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         (rc = dalloc(cp, &c->d_rec_one, (size_t)p.max_contours * 5)))
         return rc;
     c->rec_one_cap = (size_t)p.max_contours;
-    HIP_TRY(cp, hipHostMalloc((void**)&c->h_err, sizeof(int32_t), hipHostMallocMapped));
+    HIP_TRY(cp, halloc(cp, &c->h_err, sizeof(int32_t), hipHostMallocMapped));
     HIP_TRY(cp, hipHostGetDevicePointer((void**)&c->dh_err, c->h_err, 0));
     *c->h_err = 0;
     HIP_TRY(cp, hipMemset(c->d_has_keep, 0, S));
@@ -854,7 +876,7 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         fa.nnodes = c->nnodes;
         fa.nquota = c->nquota;
         fa.h_stats = B.dh_stats;
-        fa.cap = c->p.max_contours;
+        fa.cap = c->rec_cap;
         fa.cvt_simd = npx >= 16;
         fa.alpha = c->p.avg;
         fa.beta = 1.0 - c->p.avg;
@@ -1013,7 +1035,7 @@ int fm_wait(fm_ctx* c) {
         B.n = 0;
         return fail(c, FM_EHIP, "hipEventSynchronize: %s", hipGetErrorString(e));
     }
-    const int n = B.n, S = c->p.n_streams, cap = c->p.max_contours;
+    const int n = B.n, S = c->p.n_streams, cap = c->rec_cap;
     const size_t F = (size_t)n * S;
     // Frames whose records do not fit the cap are fetched whole, so len(frame.contours)
     // and the records kept never depend on max_contours (fm.py:674-694 counts them all).
@@ -1141,12 +1163,21 @@ int fm_read_mask(fm_ctx* c, int frame, int stream, uint8_t* out) {
 
 int fm_read_plane(fm_ctx* c, int plane, int frame, int stream, uint8_t* out) {
     if (!c || !out) return fail(c, FM_EINVAL, "null argument");
-    if (!(c->p.flags & FM_FLAG_KEEP_PLANES)) return fail(c, FM_ESTATE, "planes not kept: create with FM_FLAG_KEEP_PLANES");
-    if (plane < 0 || plane > 2) return fail(c, FM_EINVAL, "plane %d", plane);
+    if (plane < 0 || plane > FM_PLANE_SMALL) return fail(c, FM_EINVAL, "plane %d", plane);
+    if (plane == FM_PLANE_SMALL && c->rmode == ResizeMode::Identity)
+        return fail(c, FM_ESTATE, "no resize (box_size = frame width): the frame is the work image");
+    if (plane != FM_PLANE_SMALL && !(c->p.flags & FM_FLAG_KEEP_PLANES))
+        return fail(c, FM_ESTATE, "planes not kept: create with FM_FLAG_KEEP_PLANES");
     if (int rc = check_frame(c, frame, stream, true)) return rc;
     HIP_TRY(c, hipSetDevice(c->p.device));
     const BatchSlot& B = c->slots[c->ready_slot];
     const size_t f = (size_t)frame * c->p.n_streams + stream;
+    if (plane == FM_PLANE_SMALL) {  // the INTER_AREA output, [T][S][h][w][3]
+        HIP_TRY(c, hipMemcpyAsync(out, B.d_work + f * c->work_plane * 3, c->work_plane * 3, hipMemcpyDeviceToHost,
+                                  c->aux_stream));
+        HIP_TRY(c, hipStreamSynchronize(c->aux_stream));
+        return FM_OK;
+    }
     const size_t Fcur = (size_t)c->ready * c->p.n_streams;
     HIP_TRY(c, hipMemcpyAsync(out, B.d_planes + ((size_t)plane * Fcur + f) * c->work_plane, c->work_plane,
                               hipMemcpyDeviceToHost, c->aux_stream));
@@ -1218,3 +1249,10 @@ int fm_reset_kernel_times(fm_ctx* c) {
 }
 
 }  // extern "C"
+
+int fm_footprint(const fm_ctx* c, size_t* device_bytes, size_t* pinned_bytes) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    if (device_bytes) *device_bytes = c->dev_bytes;
+    if (pinned_bytes) *pinned_bytes = c->pinned_bytes;
+    return FM_OK;
+}

@@ -197,6 +197,7 @@ struct KernelTimer {
     static constexpr int kSample = 4;
     std::vector<int64_t> calls;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // also sampled in the pixel-only mode: the input stream's resize
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;

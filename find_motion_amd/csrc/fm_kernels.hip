@@ -158,6 +158,108 @@ __global__ __launch_bounds__(RS_T) void k_resize_area_rows(const uint8_t* __rest
 #undef RS_STORE_ROW
 }
 
+// INTER_AREA, general path, register-resident (round 4): one thread per destination pixel
+// (dx, dy) of one frame, all three channels, no LDS and no barriers.  The thread walks its
+// ycnt[dy] source rows two at a time; for each row pair it loads the 3*NT bytes of its x taps
+// from both rows (per-frame buffer descriptor, 4-B aligned b128 loads, one v_alignbyte per
+// dword to take out the 0..3-byte misalignment), and runs OpenCV's float chain on packed f32:
+// lane (row j, row j+1) of one v_pk_mul_f32 / v_pk_add_f32 pair per (tap, channel), the tap
+// weight broadcast.  The x weights (padded with zeros to NT: 0 * S = +0 and buf + 0 = buf, so
+// the padding is exact) stay in registers for the whole walk.  The per-element order is
+// k_resize_area's: buf = sum_x S*alpha in xtab order, sum = beta_0*buf_0 + beta_1*buf_1 + ...
+// in ytab order, then saturate_cast (rne).
+typedef float rs_f2 __attribute__((ext_vector_type(2)));
+constexpr int RN_T = 256;
+template <int NT>
+__global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         int H, int W, int h, int w, const int32_t* __restrict__ xofs,
+                                                         const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
+                                                         int xtaps, const int32_t* __restrict__ yofs,
+                                                         const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
+                                                         int ytaps) {
+    constexpr int NB = 3 * NT;          // tap bytes of one row
+    constexpr int NA = (NB + 3) / 4;    // aligned dwords holding them
+    constexpr int ND = NA + 1;          // dwords loaded (a 0..3-byte misalignment)
+    constexpr int NQ = ND / 4, NR = ND % 4;
+    const int n = h * w;
+    const int item = blockIdx.x * RN_T + threadIdx.x;
+    const int it = item < n ? item : n - 1;
+    const int dy = it / w, dx = it - dy * w;
+    const uint32_t rowb = 3u * (uint32_t)W;
+    const uint32_t fbytes = rowb * (uint32_t)H;
+    const uint32_t lim = (fbytes + 3u) & ~3u;  // every dword holding a frame byte is in range
+    const uint8_t* F = src + (size_t)blockIdx.y * fbytes;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)F, 0, (int)lim, 0x00020000);
+    const int nx = xcnt[dx];
+    float wx[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) wx[t] = t < nx ? xwt[(size_t)dx * xtaps + t] : 0.f;
+    const uint32_t b0 = 3u * (uint32_t)xofs[dx];
+    const int sy0 = yofs[dy], ny = ycnt[dy];
+    const float* wy = ywt + (size_t)dy * ytaps;
+    float sum[3] = {0.f, 0.f, 0.f};
+    for (int j = 0; j < ny; j += 2) {
+        uint32_t o[2] = {(uint32_t)(sy0 + j) * rowb + b0, (uint32_t)(sy0 + j + 1) * rowb + b0};
+        uint32_t al[2][NA];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t a = o[r] & ~3u, sh = o[r] & 3u;
+            uint32_t d[ND];
+            if (a + 4u * ND <= lim) {
+#pragma unroll
+                for (int q = 0; q < NQ; q++) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(a + 16u * q), 0, 0);
+                    d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
+                }
+                if constexpr (NR == 1) {
+                    d[4 * NQ] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a + 16u * NQ), 0, 0);
+                } else if constexpr (NR == 2) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u * NQ), 0, 0);
+                    d[4 * NQ] = v[0]; d[4 * NQ + 1] = v[1];
+                } else if constexpr (NR == 3) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(a + 16u * NQ), 0, 0);
+                    d[4 * NQ] = v[0]; d[4 * NQ + 1] = v[1]; d[4 * NQ + 2] = v[2];
+                }
+            } else {  // the window runs past the frame (its last columns / a row past the walk): dwords
+                      // wholly out of range read as 0 and carry zero weights or are discarded.  One dword
+                      // per load, the step in soffset, so that the loads are not merged into multi-dword
+                      // ones (whose range check would not be per dword on every target)
+#pragma unroll
+                for (int q = 0; q < ND; q++) d[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)a, 4 * q, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < NA; q++) al[r][q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
+        }
+        rs_f2 acc[3];
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const int k = 3 * t + c, q = k >> 2, s = 8 * (k & 3);
+                const rs_f2 p = {(float)(uint8_t)(al[0][q] >> s), (float)(uint8_t)(al[1][q] >> s)};
+                const rs_f2 m = p * wx[t];
+                acc[c] = t == 0 ? m : acc[c] + m;  // 0 + m == m: OpenCV's zeroed buf
+            }
+        }
+        const float by0 = wy[j];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float term = __fmul_rn(by0, acc[c].x);
+            sum[c] = j == 0 ? term : __fadd_rn(sum[c], term);
+        }
+        if (j + 1 < ny) {
+            const float by1 = wy[j + 1];
+#pragma unroll
+            for (int c = 0; c < 3; c++) sum[c] = __fadd_rn(sum[c], __fmul_rn(by1, acc[c].y));
+        }
+    }
+    if (item < n) {
+        uint8_t* D = dst + ((size_t)blockIdx.y * n + item) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; c++) D[c] = sat_u8(__float2int_rn(sum[c]));
+    }
+}
+
 // INTER_AREA integer-scale path (resizeAreaFast): 2x2 => (sum+2)>>2,
 // otherwise cvRound(sum * (1.f/area)).
 __global__ __launch_bounds__(256) void k_resize_area_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -178,6 +280,21 @@ __global__ __launch_bounds__(256) void k_resize_area_fast(const uint8_t* __restr
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W, int h, int w,
                               const int32_t* xofs, const int32_t* xcnt, const float* xwt, int xtaps,
                               const int32_t* yofs, const int32_t* ycnt, const float* ywt, int ytaps) {
+    const int nt = (xtaps + 1) & ~1;
+    if (nt <= 32 && (size_t)3 * W * H < (1u << 31)) {
+        const dim3 g((h * w + RN_T - 1) / RN_T, F);
+        switch (nt) {
+#define RN_CASE(N)                                                                                                      \
+    case N:                                                                                                            \
+        hipLaunchKernelGGL(k_resize_area_nt<N>, g, dim3(RN_T), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs, \
+                           ycnt, ywt, ytaps);                                                                          \
+        break;
+            RN_CASE(2) RN_CASE(4) RN_CASE(6) RN_CASE(8) RN_CASE(10) RN_CASE(12) RN_CASE(14) RN_CASE(16)
+            RN_CASE(18) RN_CASE(20) RN_CASE(22) RN_CASE(24) RN_CASE(26) RN_CASE(28) RN_CASE(30) RN_CASE(32)
+#undef RN_CASE
+        }
+        return hipGetLastError();
+    }
     dim3 grid(h, F);
     const int rowb = 3 * W;
     if (rowb % 16 == 0 && ((uintptr_t)src & 15) == 0 && rowb <= RS_MAXROW && w * 3 <= RS_T * RS_EPT &&

@@ -51,6 +51,8 @@ extern "C" {
 #define FM_PLANE_GRAY 0  /* VideoFrame.gray        (fm.py:493) */
 #define FM_PLANE_BLUR 1  /* VideoFrame.blur, masked (fm.py:494, 619-636) */
 #define FM_PLANE_DELTA 2 /* VideoFrame.frame_delta (fm.py:250) */
+#define FM_PLANE_SMALL 3 /* the INTER_AREA-resized BGR frame `small` (fm.py:490), h*w*3 bytes; resize modes only,
+                            no FM_FLAG_KEEP_PLANES needed */
 
 typedef struct fm_ctx fm_ctx;
 
@@ -156,7 +158,8 @@ int fm_last_ccl_stats(const fm_ctx* ctx, int32_t* shared_nodes, int32_t* heavy_t
 /* Dilated threshold mask (VideoFrame.thresh after find_contours, fm.py:266), h*w bytes. */
 int fm_read_mask(fm_ctx* ctx, int frame, int stream, uint8_t* out);
 
-/* gray / blur / frame_delta planes (needs FM_FLAG_KEEP_PLANES), h*w bytes. */
+/* gray / blur / frame_delta planes (needs FM_FLAG_KEEP_PLANES), h*w bytes; FM_PLANE_SMALL: the
+ * resized BGR frame, h*w*3 bytes (FM_ESTATE when box_size = frame width). */
 int fm_read_plane(fm_ctx* ctx, int plane, int frame, int stream, uint8_t* out);
 
 /* Background model (VideoMotion.ref_frame, float64, fm.py:652, 659), h*w doubles. */
@@ -166,6 +169,11 @@ int fm_write_background(fm_ctx* ctx, int stream, const double* in);
 /* Launch on the caller's HIP stream (hipStream_t) instead of the context's own
  * stream; NULL restores the context stream. */
 int fm_set_hip_stream(fm_ctx* ctx, void* hip_stream);
+
+/* Memory the context holds: device bytes (fm_create's buffers, plus input staging allocated on the
+ * first host submit) and page-locked host bytes (the mapped contour records and counters).  No
+ * reference counterpart (sizing for many streams per GPU). */
+int fm_footprint(const fm_ctx* ctx, size_t* device_bytes, size_t* pinned_bytes);
 
 /* FM_FLAG_PROFILE: per-kernel accumulated device time since the last reset.
  * names[i] (static strings), ms[i], launches[i] for i < returned count. */

@@ -3,10 +3,10 @@ cases do not reach, against the CPU oracle (oracle.OracleStream.run: the same
 arithmetic as step(), frames scheduled in parallel where find_diff's data flow
 allows, so full-size sequences finish in seconds).
 
-* the bench workload itself: 1080p, mode F, T = 128 frames per launch from a
-  device-resident ring cycling 64 synthetic frames, the production
-  k_pix<5, false, false> (no planes kept), fm_max_inflight batches submitted
-  before the first wait, a ring wrap onto reused batch slots;
+* the bench workload itself: 1080p, mode F, T = 256 frames per launch from a
+  256-frame device-resident ring cycling 64 synthetic frames, the production
+  k_pix5 (no planes kept), fm_max_inflight (6) batches submitted before the
+  first wait, 8 batches so that slots are reused;
 * configs[2]: 8 x 1080p streams on one GPU, batches in flight -- also at the
   perf shape quoted for it (T = 128 per launch, 4 in flight, 7 batches on 6 slots, device ring);
 * configs[4] geometry: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the two
@@ -44,14 +44,18 @@ def _check_frame(eng, res, t, s, f, tag, mask=True):
 
 
 def test_bench_shape_inflight_ring_wrap():
-    """bench.py's exact workload through the production kernel, against the oracle on every frame."""
+    """bench.py's exact workload (its defaults: --batch 256 --ring 256 --ring-period 64, max_contours 1 << 14,
+    fm_max_inflight batches submitted before the first wait) through the production kernel, against the
+    oracle on every frame: 256-frame launches from a 256-frame device ring cycling 64 synthetic frames, six
+    batches in flight, eight batches so that two slots are reused, node pools sized for 256 frames."""
     torch = pytest.importorskip("torch")
-    W, H, T = 1920, 1080, 128
-    uniq = batch(W, H, 1, 0, 64)                      # bench: 64 synthetic frames cycled through a 128 ring
-    ring_h = np.concatenate([uniq, uniq])              # [128][1][H][W][3]
+    W, H, T, PERIOD = 1920, 1080, 256, 64
+    uniq = batch(W, H, 1, 0, PERIOD)                   # bench: ring slot t holds synthetic frame t % 64
+    ring_h = np.concatenate([uniq] * (T // PERIOD))    # [256][1][H][W][3]
     ring = torch.from_numpy(ring_h).to("cuda:0")
     torch.cuda.synchronize()
-    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T,
+                       max_contours=1 << 14)
     assert not eng.keep_planes
     orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=5))
     depth = eng.max_inflight

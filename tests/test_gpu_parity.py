@@ -86,6 +86,54 @@ def test_mode_d_resize_paths():
     run_pair(640, 480, 100, S=2, T=2, n_batches=2)
 
 
+@pytest.mark.parametrize("W,H,box,S,T", [
+    (1920, 1080, 100, 1, 5),   # mode D, the reference CLI default (-B 100): 22-tap register kernel
+    (1920, 1080, 300, 2, 3),   # find_objects' ROI width (fm.py:706): 8 taps
+    (3840, 2160, 300, 1, 2),   # config 5's ROI resize: 14 taps
+    (3840, 2160, 100, 1, 2),   # 40 taps: past the register kernel, the LDS-staged one
+    (640, 480, 100, 2, 3),     # configs[0] geometry: 8 taps
+    (642, 481, 100, 1, 3),     # 3*W % 4 == 2: rows start at every byte alignment
+    (337, 203, 100, 3, 2),     # odd width, ragged taps, three streams
+    (101, 40, 100, 1, 4),      # scale just above 1: 2 taps, most of them partial
+    (2000, 300, 7, 1, 2),      # one destination row, 287 taps a pixel
+])
+def test_resize_area_bytes_vs_oracle(W, H, box, S, T):
+    """The INTER_AREA output itself (`small`, fm.py:490), every byte of every frame of every stream, against
+    the oracle's restatement of cv2.resize(INTER_AREA): the tap order of each float chain is OpenCV's, so the
+    bytes must be identical.  The last frame of the batch ends the input buffer, so the last columns' windows
+    run past it (their out-of-range dwords carry zero weights)."""
+    if int(H * (box / float(W))) < 1:
+        pytest.skip("work height 0")
+    from find_motion_amd._native import PLANE_SMALL
+    k = make_gaussian(box, 20)
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=T)
+    for b in range(2):
+        fr = batch(W, H, S, 7 + b * T, T)
+        eng.submit(fr)
+        eng.wait()
+        for t in range(T):
+            for s in range(S):
+                _eq(eng.plane(PLANE_SMALL, t, s), oracle.resize_area_bgr(fr[t, s], box), f"small b{b} t{t} s{s}")
+    eng.close()
+
+
+def test_resize_area_bytes_from_device_ring_end():
+    """Device-resident input whose last frame ends exactly at the end of its allocation (the caller's ring,
+    fm_submit on_device = 1): the windows of the last row's last columns reach past the allocation."""
+    import torch
+
+    from find_motion_amd._native import PLANE_SMALL
+    W, H, box, T = 1920, 1080, 100, 4
+    fr = batch(W, H, 1, 3, T)
+    dev = torch.from_numpy(fr).to("cuda")
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=box, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    eng.submit_device(dev.data_ptr(), T)
+    eng.wait()
+    for t in range(T):
+        _eq(eng.plane(PLANE_SMALL, t, 0), oracle.resize_area_bgr(fr[t, 0], box), f"small t{t}")
+    eng.close()
+
+
 def test_mode_f_1080p_k5():
     run_pair(1920, 1080, 1920, blur_scale=384, T=2, n_batches=2)
 
