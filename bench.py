@@ -24,7 +24,8 @@ import os
 import sys
 import time
 
-# the package's default (find_motion_amd/__init__.py), set before torch makes the first HIP call
+# eight hardware queues (find_motion_amd.use_hw_queues, the CLI's setting), before torch makes the first HIP
+# call; the value in effect is recorded in the JSON line
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np
@@ -34,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 PCIE_GBS = 63.0  # PCIe Gen5 x16, one direction
+CONFIG5_MASKS = [((0, 0), (639, 359)), ((3839, 2159), (3200, 2159), (3839, 1600))]
 METRIC = "frames/sec on 1080p synthetic video at 1/2/4/8 MI355X; achieved HBM GB/s %peak"
 
 
@@ -90,7 +92,7 @@ def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | 
     return int(k["traffic_bytes"]), e.get("source"), k.get("sq")
 
 
-def config_name(S: int, W: int, H: int, mode: str, k: int) -> str:
+def config_name(S: int, W: int, H: int, mode: str, k: int, haar: bool = False) -> str:
     """Which BASELINE.json config the run's shape is (configs[1] is the headline; the others are the parity
     configurations run at their quoted perf shapes), so a line is never filed under the wrong one."""
     if (W, H) == (1920, 1080):
@@ -100,7 +102,7 @@ def config_name(S: int, W: int, H: int, mode: str, k: int) -> str:
             return "configs[2]" if mode == "F" else "configs[2] (mode D)"
         return f"{S} x 1080p streams (configs[2]/[3] family)"
     if (W, H) == (3840, 2160) and k == 21:
-        return "configs[4] geometry (no Haar stage)"
+        return "configs[4]" if haar else "configs[4] geometry (no Haar stage)"
     return "custom shape"
 
 
@@ -198,6 +200,31 @@ def mjpeg_fed(eng, host: np.ndarray, T: int, S: int, quality: int = 75) -> dict 
             "mode": "BatchFeeder JPEG mode: JPEG bytes -> host parse -> H2D -> GPU Huffman/IDCT/colour -> hot path"}
 
 
+class RoiSelector:
+    """Which frames of one stream reach the cascade, by the reference's rule: find_movement counts the
+    contours (fm.py:665-700), decide_output writes the frame when movement_counter >= min_movement_frames
+    or movement_decay > 0 and then calls find_objects (fm.py:549-575), whose counter runs the cascades on
+    every 15th call (skip = 15, fm.py:703-713).  VideoMotion defaults: fps 30, cache_time 2.0 (decay 60
+    frames), min_time 0.5 (15 contour-frames)."""
+
+    def __init__(self, fps: int = 30, cache_time: float = 2.0, min_time: float = 0.5, skip: int = 15):
+        self.cache_frames, self.min_frames, self.skip = int(cache_time * fps), int(min_time * fps), skip
+        self.counter = self.decay = self.obj = 0
+
+    def step(self, count: int) -> bool:
+        movement = count > 0
+        self.decay -= 1 if self.decay > 0 else 0
+        self.counter = self.counter + int(count) if movement else 0
+        if self.counter >= self.min_frames or self.decay > 0:
+            if movement:
+                self.decay = self.cache_frames
+            self.obj += 1
+            if self.obj == self.skip:
+                self.obj = 0
+                return True
+        return False
+
+
 def spawn_ranks(n: int) -> int:
     """bench.py --gpus N without a launcher: start N ranks of this script (one per GPU, RANK = LOCAL_RANK =
     device ordinal, rendezvous on 127.0.0.1) before any GPU call in this process, and return the worst
@@ -260,6 +287,13 @@ def main() -> None:
     ap.add_argument("--no-host-fed", action="store_true", help="skip the host-fed decode-ahead pipeline figure")
     ap.add_argument("--no-ktimes", action="store_true", help="no HIP event timing at all (no roofline)")
     ap.add_argument("--no-mjpeg", action="store_true", help="skip the MJPEG-fed (GPU decode) figure")
+    ap.add_argument("--masks", action="store_true",
+                    help="configs[4]'s polygon masks on every stream: a rectangle and a triangle in 3840x2160 frame "
+                         "coordinates, given in the MASK_SCHEMA form (find_motion.py:86-100), the polygons of the "
+                         "configs[4] parity tests; implied by --haar")
+    ap.add_argument("--haar", action="store_true",
+                    help="configs[4]: run the reference's frontalface_default cascade on every 15th written frame "
+                         "of each stream (find_objects, fm.py:549-575, 703-731) inside the timed steps")
     ap.add_argument("--all-ktimes", action="store_true",
                     help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
@@ -295,7 +329,7 @@ def main() -> None:
     k = make_gaussian(box, blur_scale)
     S, T = args.streams, args.batch
     R = max(args.ring - args.ring % T, T)
-    cfg = {"workload": f"{config_name(S, W, H, args.mode, k)}: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
+    cfg = {"workload": f"{config_name(S, W, H, args.mode, k, args.haar)}: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
                        f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
                        + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
@@ -320,6 +354,12 @@ def main() -> None:
     eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
                        max_batch=T, max_contours=1 << 14, profile=False if args.no_ktimes else True if args.all_ktimes else "pix", device=local)
     footprint = dict(eng.footprint(), ring_bytes=R * frame_bytes)
+    if args.masks or args.haar:  # mask_off_areas (fm.py:611-636): rasterised once, applied in the pixel kernel
+        from find_motion_amd import rasterize_masks
+        keep = rasterize_masks(cfg["h"], cfg["w"], box / W, CONFIG5_MASKS)
+        for s in range(S):
+            eng.set_mask(s, keep)
+        cfg["masks"] = [list(map(list, m)) for m in CONFIG5_MASKS]
     base = ring.data_ptr()
     n_batches = R // T
 
@@ -335,11 +375,39 @@ def main() -> None:
 
     ccl = {"heavy_tiles": 0, "shared_nodes_max": 0, "fallback_frames": 0, "batches": 0}
 
+    # configs[4]'s object-ROI stage: the frames find_objects hands to the cascade, gathered from the ring
+    # (still in HBM) after each waited batch and detected in one call (INTER_AREA to 300 px + detectMultiScale)
+    det, sel = None, [RoiSelector() for _ in range(S)]
+    haar = {"calls": 0, "roi_frames": 0, "detections": 0, "wall_s": 0.0, "device_ms": 0.0}
+    if args.haar:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from golden_cases import load_frontalface  # the reference's cascade, as committed fixture arrays
+
+        from find_motion_amd import CascadeClassifier
+        det = CascadeClassifier(load_frontalface()[0], device=local)
+
+    def objects(i: int) -> None:
+        cnt = eng.counts()
+        base_t = (i % n_batches) * T
+        pick = [(t, s) for t in range(T) for s in range(S) if sel[s].step(int(cnt[t, s]))]
+        if not pick:
+            return
+        t0 = time.perf_counter()
+        roi = torch.stack([ring[base_t + t, s] for t, s in pick])
+        found = det.detect_frames(roi, 300, 1.1, 5)
+        haar["wall_s"] += time.perf_counter() - t0
+        haar["device_ms"] += det.last_ms()
+        haar["calls"] += 1
+        haar["roi_frames"] += len(pick)
+        haar["detections"] += sum(len(f) for f in found)
+
     def run(first: int, n: int) -> None:
         for i in range(min(depth, n)):
             submit(first + i)
         for i in range(n):
             eng.wait()  # completes batch i and frees its slot
+            if det is not None:
+                objects(first + i)
             st = eng.ccl_stats()  # two mapped-memory words: no device sync
             ccl["heavy_tiles"] += st["heavy_tiles"]
             ccl["shared_nodes_max"] = max(ccl["shared_nodes_max"], st["shared_nodes"])
@@ -355,10 +423,14 @@ def main() -> None:
     dist.barrier(active)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    haar.update(calls=0, roi_frames=0, detections=0, wall_s=0.0, device_ms=0.0)
     run(args.warmup, args.steps)
     torch.cuda.synchronize()
     dist.barrier(active)
-    elapsed = dist.max_over_ranks(time.perf_counter() - t0, active, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+    wall = time.perf_counter() - t0
+    elapsed = dist.max_over_ranks(wall, active, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+    if det is not None:
+        det.close()
 
     ktimes = eng.kernel_times()
     total_frames = world * S * T * args.steps
@@ -506,6 +578,13 @@ def main() -> None:
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "host_fed_per_gpu": host_fed,
                "mjpeg_fed_per_gpu": mjpeg, "footprint_per_gpu": footprint,
+               "hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+               "haar_stage": None if det is None else {
+                   "cascade": "haarcascade_frontalface_default (reference XML as tests/golden fixture arrays)",
+                   "rule": "every 15th written frame per stream (find_objects skip=15, fm.py:549-575, 703-731)",
+                   "calls": haar["calls"], "roi_frames": haar["roi_frames"], "detections": haar["detections"],
+                   "wall_ms": round(1e3 * haar["wall_s"], 3), "device_ms": round(haar["device_ms"], 3),
+                   "share_of_step_time": round(haar["wall_s"] / wall, 4)},
                "path_hbm": {"bytes_per_frame": path_bytes_per_frame(cfg),
                             "achieved": round(value / world * path_bytes_per_frame(cfg) / 1e9, 1), "unit": "GB/s",
                             "frac": round(value / world * path_bytes_per_frame(cfg) / 1e9 / HBM_PEAK_GBS, 4),

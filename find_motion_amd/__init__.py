@@ -10,12 +10,18 @@ __version__ = "0.1.0"
 
 import os as _os
 
-# Hardware queues per process: HIP's default of 4 puts the decoder's two streams, the contour
-# streams and the input / aux streams on shared queues (a shared queue runs its packets in order);
-# with 8 every stream the engine and the MJPEG decoder use has a queue of its own (MJPEG-fed
-# pipeline 72-73 k -> 79-81 k frames/s, the device-resident figure unchanged).
-# Only effective when this is imported before the process's first HIP call.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+def use_hw_queues(n: int = 8) -> int:
+    """Opt in to n hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4).  With 4, the MJPEG
+    decoder's two streams, the contour-pass streams and the input / aux streams share queues, and a shared
+    queue runs its packets in order; with 8 each has its own (MJPEG-fed pipeline 72-73 k -> 79-81 k
+    frames/s, the device-resident figure unchanged).  It changes the queue setup of every
+    HIP user in the process (torch included) and takes effect only before the process's first HIP call, so
+    it is never set on import: the CLI and bench.py call this first thing.  A value already in the
+    environment wins.  Returns the value in effect."""
+    _os.environ.setdefault("GPU_MAX_HW_QUEUES", str(int(n)))
+    return int(_os.environ["GPU_MAX_HW_QUEUES"])
+
 
 from ._native import (  # noqa: F401
     CascadeClassifier,

@@ -161,6 +161,22 @@ class BatchFeeder:
         finally:
             self._full.put(None)
 
+    def _submit_jpeg(self, b: Batch) -> None:
+        """fm_submit_jpeg, or, when the GPU decoder refuses a frame of the batch (FM_ENOTSUP: a layout
+        it does not take, e.g. separate component scans in a stream whose first frame it took), the
+        batch decoded on the host and submitted as frames -- its results and VideoFrame.raw (read back
+        from the engine's input slot) are the same."""
+        from ._native import FM_ENOTSUP, FMError
+        from .videoio import host_decode_jpeg
+        try:
+            self.engine.submit_jpeg(self.decoder, b.jpegs)
+        except FMError as e:
+            if e.code != FM_ENOTSUP:
+                raise
+            S = len(self.caps)
+            fr = np.stack([host_decode_jpeg(j) for j in b.jpegs])
+            self.engine.submit(fr.reshape((b.T, S) + fr.shape[1:]))
+
     # -- consumer -------------------------------------------------------------------
     def __iter__(self):
         eng = self.engine
@@ -174,7 +190,7 @@ class BatchFeeder:
                         done = True
                         break
                     if b.jpegs is not None:
-                        eng.submit_jpeg(self.decoder, b.jpegs)
+                        self._submit_jpeg(b)
                     else:
                         eng.submit(b.buf[:b.T])
                     inflight.append(b)

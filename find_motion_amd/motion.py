@@ -410,7 +410,7 @@ class VideoMotion:
                 return eng.read_frame(t, s)
             if self._jpeg_dec is None:
                 self._jpeg_dec = MJpegDecoder(self.frame_width, self.frame_height, 1, device=self.device)
-            return self._jpeg_dec.decode([jpeg])[0]
+            return videoio.decode_one(self._jpeg_dec, jpeg)
         return load
 
     def bind_results(self, vfs, eng, stream: int) -> None:

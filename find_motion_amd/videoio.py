@@ -127,7 +127,7 @@ class JpegListCapture:
         if self._dec is None:
             from ._native import MJpegDecoder
             self._dec = MJpegDecoder(self.w, self.h, max_frames=1)
-        return True, self._dec.decode([j])[0]
+        return True, decode_one(self._dec, j)
 
     def get(self, prop: int) -> float:
         return {CAP_PROP_FRAME_COUNT: float(len(self._jpegs)), CAP_PROP_FRAME_WIDTH: float(self.w),
@@ -159,11 +159,13 @@ def jpeg_layout(data: bytes):
 def jpeg_gpu_supported(data: bytes) -> bool:
     """Whether the GPU decoder takes this JPEG's layout (fm_jpeg.hip parse_jpeg / setup_geometry):
     SOF0/SOF1 Huffman, 8-bit, one component or three with Cb, Cr at 1x1 and Y at 1x1, 2x1 or 2x2,
-    one interleaved scan."""
+    one interleaved scan: the first SOS names every component of the frame (a file whose components
+    come in separate scans is refused by parse_jpeg)."""
     try:
         i = 2
         if data[:2] != b"\xff\xd8":
             return False
+        nc = None
         while i + 4 <= len(data):
             if data[i] != 0xFF:
                 return False
@@ -180,15 +182,29 @@ def jpeg_gpu_supported(data: bytes) -> bool:
                     return False
                 nc = seg[5]
                 hv = [(seg[7 + 3 * c] >> 4, seg[7 + 3 * c] & 15) for c in range(nc)]
-                if nc == 1:
-                    return 1 <= hv[0][0] <= 4 and 1 <= hv[0][1] <= 4
-                return nc == 3 and hv[1] == hv[2] == (1, 1) and hv[0] in ((1, 1), (2, 1), (2, 2))
-            if m == 0xDA:
-                return False
+                ok = (1 <= hv[0][0] <= 4 and 1 <= hv[0][1] <= 4) if nc == 1 else \
+                    (nc == 3 and hv[1] == hv[2] == (1, 1) and hv[0] in ((1, 1), (2, 1), (2, 2)))
+                if not ok:
+                    return False
+            if m == 0xDA:  # the first scan: interleaved over every component of the frame
+                return nc is not None and len(seg) >= 1 and seg[0] == nc
             i += ln
     except IndexError:
         return False
     return False
+
+
+def decode_one(dec, data: bytes) -> np.ndarray:
+    """One frame through a one-frame GPU decoder, or on the host when the GPU decoder refuses this frame's
+    layout (FM_ENOTSUP: a later frame of a stream whose first frame it took may be coded differently)."""
+    from ._native import FM_ENOTSUP, FMError
+    try:
+        return dec.decode([data])[0]
+    except FMError as e:
+        if e.code != FM_ENOTSUP:
+            raise
+        log.info("JPEG frame not supported by the GPU decoder (%s); decoding it on the host", e)
+        return host_decode_jpeg(data)
 
 
 def host_decode_jpeg(data: bytes) -> np.ndarray:
@@ -468,7 +484,7 @@ class MjpegAviCapture(RawAviCapture):
         if self._dec is None:
             from ._native import MJpegDecoder
             self._dec = MJpegDecoder(self.w, self.h, max_frames=1, device=self._device)
-        return True, self._dec.decode([j])[0]
+        return True, decode_one(self._dec, j)
 
     def release(self) -> None:
         super().release()

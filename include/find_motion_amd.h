@@ -264,7 +264,8 @@ void fm_mjpeg_destroy(fm_mjpeg* dec);
 const char* fm_mjpeg_last_error(const fm_mjpeg* dec);
 /* Decode n JPEGs (host memory: jpegs[i], sizes[i] bytes) into [n][H][W][3] BGR
  * frames at out: device memory when out_on_device, else host memory.
- * Synchronous. */
+ * Synchronous.  It runs on the decoder's own streams: a device `out` must not be
+ * in use by work the caller queued on other streams (as for hipMemcpy). */
 int fm_mjpeg_decode(fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n, uint8_t* out,
                     int out_on_device);
 /* Device time of the last fm_mjpeg_decode's kernels (HIP events), ms. */
@@ -277,7 +278,11 @@ int fm_mjpeg_geometry(const fm_mjpeg* dec, int* width, int* height, int* device,
  * batch's Huffman pass overlaps the previous batch's IDCT / colour kernels; the
  * context's input stream waits for the decode -- then processed as
  * fm_submit (frames, n_frames, on_device = 1) would.  The host buffers may be
- * reused when the call returns.  FM_EINVAL (nothing enqueued) when dec was
+ * reused when the call returns.  The decode does not wait for work queued earlier on the context's
+ * streams: it writes the batch slot's input buffer, which is idle by construction (fm_wait
+ * synchronised the slot's previous batch before the slot is handed out again) -- a waited-for-entry
+ * event would serialise consecutive calls, whose Huffman pass overlaps the previous call's IDCT and
+ * colour kernels.  FM_EINVAL (nothing enqueued) when dec was
  * created for another frame size or device, or for fewer than
  * n_frames x n_streams frames per call. */
 int fm_submit_jpeg(fm_ctx* ctx, fm_mjpeg* dec, const uint8_t* const* jpegs, const size_t* sizes, int n_frames);

@@ -125,3 +125,17 @@ def test_config5_masks_and_union():
 def test_polygon_with_one_point_rejected():
     with pytest.raises(_native.FMError):
         _native.rasterize_masks(10, 10, 1.0, [[(1, 1)]])
+
+
+def test_import_leaves_hw_queues_alone():
+    """Importing the package does not touch GPU_MAX_HW_QUEUES (it would change the queue setup of every HIP
+    user in the process); use_hw_queues() is the explicit opt-in the CLI and bench.py make."""
+    import os
+    import subprocess
+    import sys
+    code = ("import os, find_motion_amd as f; a = os.environ.get('GPU_MAX_HW_QUEUES'); "
+            "b = f.use_hw_queues(); print(a, b, os.environ['GPU_MAX_HW_QUEUES'])")
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["None", "8", "8"], out.stdout + out.stderr

@@ -264,6 +264,36 @@ def test_per_frame_path_more_contours_than_cap_over_batches():
     eng.close()
 
 
+@pytest.mark.parametrize("S", [2, 8])
+def test_submit_streams_1080p_large_pitch(S):
+    """fm_submit_streams at 1080p: each stream's copy is one 2-D copy whose row is a whole 6.2 MB frame and
+    whose pitch is S frames (50 MB at S = 8) -- the batch's input slot must hold exactly the frames, from
+    host and from device buffers, and the results equal fm_submit's."""
+    torch = pytest.importorskip("torch")
+    W, H, T = 1920, 1080, 3
+    kw = dict(n_streams=S, src_w=W, src_h=H, box_size=W, ksize=5, threshold=12, avg=0.1, max_batch=T)
+    a, b, c = (MotionEngine(**kw) for _ in range(3))
+    f = batch(W, H, S, 5, T)
+    per = [np.ascontiguousarray(f[:, s]) for s in range(S)]
+    dev = [torch.from_numpy(p).to("cuda:0") for p in per]
+    torch.cuda.synchronize()
+    a.submit(f)
+    b.submit_streams(per)
+    c.submit_streams([t.data_ptr() for t in dev], on_device=True, n_frames=T)
+    for x in (a, b, c):
+        x.wait()
+    for t in range(T):
+        for s in range(S):
+            for x in (b, c):
+                assert np.array_equal(x.read_frame(t, s), f[t, s]), (t, s)
+    for x in (b, c):
+        assert np.array_equal(a.counts(), x.counts())
+        for s in range(S):
+            assert np.array_equal(a.background(s), x.background(s))
+    for x in (a, b, c):
+        x.close()
+
+
 def test_submit_streams_equals_submit():
     """fm_submit_streams (one frame buffer per stream) == fm_submit of the same frames gathered
     into [t][s] order: host buffers, device buffers, and one stream's device buffer read in place."""

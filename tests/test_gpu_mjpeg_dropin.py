@@ -73,6 +73,37 @@ def test_lazy_raw_frames_written_uncompressed(tmp_path):
         assert np.array_equal(g, reference_decode(jp[i])), i
 
 
+def test_unsupported_frames_mid_stream_decode_on_the_host(tmp_path):
+    """A stream whose first frame the GPU decoder takes but whose later frames it refuses (progressive
+    JPEGs from frame 10 on): the batches holding them are decoded on the host and submitted as frames
+    (feeder), cached frames of overwritten batches too (one-frame decoder) -- decisions and every written
+    raw frame equal the oracle's on the libjpeg-turbo-decoded frames, nothing raises."""
+    W, H, n = 320, 240, 40
+    vid = SyntheticVideo(W, H, 3)
+    jp = [encode(vid.frame(i), quality=85, progressive=10 <= i < 30) for i in range(n)]
+    src = tmp_path / "v.avi"
+    w = videoio.MjpegAviWriter(str(src), 30, (W, H))
+    for j in jp:
+        w.write_jpeg(j)
+    w.release()
+    vm = motion.VideoMotion(filename=str(src), box_size=100, threshold=12, cache_time=0.3, min_time=0.1,
+                            batch=8, outdir=str(tmp_path), codec="DIB ", gpu_decode=True)
+    assert isinstance(vm.cap, videoio.MjpegAviCapture) and vm.cap.gpu_decode
+    vm.find_motion()
+    want = _oracle_written(jp, W, H, 100)
+    assert want and vm.written_indices == want
+    assert any(10 <= i < 30 for i in want)
+    got = _read_all(videoio.RawAviCapture(vm.outfile_name))
+    assert len(got) == len(want)
+    for g, i in zip(got, want):
+        assert np.array_equal(g, reference_decode(jp[i])), i
+    cap = videoio.JpegListCapture(jp[8:12])
+    for k in range(4):  # the one-frame GPU decoder: baseline frames on the GPU, progressive ones on the host
+        ok, f = cap.read()
+        assert ok and np.array_equal(f, reference_decode(jp[8 + k])), k
+    cap.release()
+
+
 def test_stream_group_on_mjpeg(tmp_path):
     W, H, n, S = 320, 180, 24, 3
     srcs = [tmp_path / f"s{s}.avi" for s in range(S)]

@@ -169,6 +169,24 @@ def test_jpeg_gpu_supported_layouts():
     assert not videoio.jpeg_gpu_supported(b"not a jpeg")
 
 
+def _marker_stream(ns, nc=3):
+    """SOI, SOF0 (8-bit, 16x16, nc components at 1x1), SOS naming ns of them: the markers only."""
+    sof = bytes([8, 0, 16, 0, 16, nc]) + b"".join(bytes([c + 1, 0x11, 0]) for c in range(nc))
+    sos = bytes([ns]) + b"".join(bytes([c + 1, 0]) for c in range(ns)) + bytes([0, 63, 0])
+    seg = lambda m, body: bytes([0xFF, m]) + (len(body) + 2).to_bytes(2, "big") + body  # noqa: E731
+    return b"\xff\xd8" + seg(0xC0, sof) + seg(0xDA, sos) + b"\x00" * 8 + b"\xff\xd9"
+
+
+def test_jpeg_gpu_supported_needs_one_interleaved_scan():
+    """A frame whose components come in separate scans (first SOS with Ns < Nf) is refused up front, as
+    parse_jpeg (fm_jpeg.hip) would refuse it (the advisor's round-3 finding)."""
+    from find_motion_amd import videoio
+    assert videoio.jpeg_gpu_supported(_marker_stream(3))
+    assert not videoio.jpeg_gpu_supported(_marker_stream(1))
+    assert not videoio.jpeg_gpu_supported(_marker_stream(2))
+    assert videoio.jpeg_gpu_supported(_marker_stream(1, nc=1))
+
+
 class _StubCv2:
     """Just enough of cv2 for open_capture's choice: VideoCapture records what it was opened on."""
 
