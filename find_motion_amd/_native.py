@@ -15,7 +15,7 @@ import numpy as np
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libfm_hip.so")
 # development override: an alternative build of the same library (A/B kernel variants)
-LIB_PATH = os.environ.get("FM_HIP_LIB", LIB_PATH)
+LIB_PATH = os.environ.get("FM_HIP_LIB") or LIB_PATH  # unset or empty: the in-tree product library
 
 FM_OK, FM_EINVAL, FM_EHIP, FM_ENOMEM, FM_ESTATE, FM_ENOTSUP = 0, -1, -2, -3, -4, -5
 FM_FLAG_KEEP_PLANES, FM_FLAG_PROFILE, FM_FLAG_PROFILE_PIX, FM_FLAG_CONTOUR_AREA = 0x1, 0x2, 0x4, 0x8

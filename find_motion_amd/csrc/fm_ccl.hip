@@ -840,101 +840,132 @@ __device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
 // node of the component with edge label e of candidate tile `tile`
 __device__ __forceinline__ int enode(const TileRec* TR, int tile, uint16_t e) { return TR[tile].nbase + (e & 0x7FFF); }
 
+// Union-find policies of the edge merge: over the global NodeRec parents (any frame), or over a
+// frame's nodes mirrored in LDS (k_resolve's fast path: local id = region tile, or ntiles + the
+// node's place in the frame's quota).
+struct GlobalUF {
+    NodeRec* N;
+    __device__ void uni(int x, int y) const { gunion(N, x, y); }
+    __device__ bool outer(int n) const { return (N[n].flags & 2) != 0; }
+    __device__ void mark_outer(int n) const { atomicOr(&N[n].flags, 2u); }
+};
+struct LocalUF {
+    int* par;
+    uint32_t* fl;
+    int rb0, qbase, nt;  // region node ids: rb0 + tile; quota node ids: qbase + i
+    __device__ int loc(int g) const { return g < qbase ? g - rb0 : g - qbase + nt; }
+    __device__ void uni(int x, int y) const { lunion(par, loc(x), loc(y)); }
+    __device__ bool outer(int n) const { return (fl[loc(n)] & 2) != 0; }
+    __device__ void mark_outer(int n) const { atomicOr(&fl[loc(n)], 2u); }
+};
+
 // Background component `nd` of a candidate touches empty region `rep`.  An outer
 // region only contributes its outer-ness, so the node is marked directly (no union:
 // every candidate around a moving object borders the big outer background, and
 // unions into that one root serialise on its atomics); an enclosed region is unioned.
-__device__ __forceinline__ void touch_region(NodeRec* N, int nd, int rnode) {
-    // (rnode = f*ntiles + a representative tile < F*ntiles: regrep is written for every
-    // empty tile by k_regions of this batch)
-    if (N[rnode].flags & 2) atomicOr(&N[nd].flags, 2u);
-    else gunion(N, nd, rnode);
+// (rnode = f*ntiles + a representative tile < F*ntiles: regrep is written for every
+// empty tile by k_regions of this batch)
+template <class UF>
+__device__ __forceinline__ void touch_region(const UF& U, int nd, int rnode) {
+    if (U.outer(rnode)) U.mark_outer(nd);
+    else U.uni(nd, rnode);
 }
 
-// one wave per candidate, lane = edge position
+// candidate tile t of frame f, lane = edge position: unions along its right / bottom edges with
+// candidate neighbours, its corner diagonals, and every edge against empty regions
+template <class UF>
+__device__ __forceinline__ void merge_tile(const FusedArgs& a, size_t f, int t, int ln, const UF& U) {
+    const int ntx = a.ntx, nt = a.ntiles;
+    const uint8_t* cf = a.candf + f * nt;
+    const int32_t* rr = a.regrep + f * nt;
+    const TileRec* TR = a.tiles + f * nt;
+    const int rb0 = (int)(f * nt);  // region node ids of this frame: rb0 + representative tile
+    const int tx = t % ntx, ty = t / ntx;
+    const bool hasR = tx + 1 < ntx, hasD = ty + 1 < a.nty;
+    // right edge
+    if (hasR) {
+        const uint16_t A = TR[t].edges[64 + ln];
+        const int Ap = lane_up1((int)A);
+        if (cf[t + 1]) {
+            const uint16_t B = TR[t + 1].edges[ln];
+            const int Bp = lane_up1((int)B);
+            if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) U.uni(enode(TR, t, A), enode(TR, t + 1, B));
+            if (efg(A)) {
+                if (ln > 0) {
+                    const uint16_t Bu = TR[t + 1].edges[ln - 1];
+                    if (efg(Bu) && Bu != B) U.uni(enode(TR, t, A), enode(TR, t + 1, Bu));
+                }
+                if (ln < 63) {
+                    const uint16_t Bd = TR[t + 1].edges[ln + 1];
+                    if (efg(Bd) && Bd != B) U.uni(enode(TR, t, A), enode(TR, t + 1, Bd));
+                }
+            }
+        } else if (!efg(A) && !(ln > 0 && Ap == A)) {
+            touch_region(U, enode(TR, t, A), rb0 + rr[t + 1]);
+        }
+    }
+    // bottom edge
+    if (hasD) {
+        const int n = t + ntx;
+        const uint16_t A = TR[t].edges[192 + ln];
+        const int Ap = lane_up1((int)A);
+        if (cf[n]) {
+            const uint16_t B = TR[n].edges[128 + ln];
+            const int Bp = lane_up1((int)B);
+            if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) U.uni(enode(TR, t, A), enode(TR, n, B));
+            if (efg(A)) {
+                if (ln > 0) {
+                    const uint16_t Bl = TR[n].edges[128 + ln - 1];
+                    if (efg(Bl) && Bl != B) U.uni(enode(TR, t, A), enode(TR, n, Bl));
+                }
+                if (ln < 63) {
+                    const uint16_t Br = TR[n].edges[128 + ln + 1];
+                    if (efg(Br) && Br != B) U.uni(enode(TR, t, A), enode(TR, n, Br));
+                }
+            }
+        } else if (!efg(A) && !(ln > 0 && Ap == A)) {
+            touch_region(U, enode(TR, t, A), rb0 + rr[n]);
+        }
+        // corner diagonals (foreground only: both tiles candidates)
+        if (ln == 0 && hasR && cf[n + 1]) {  // (63,63) <-> (0,0) of the down-right tile
+            const uint16_t P = TR[t].edges[192 + 63], Q = TR[n + 1].edges[128];
+            if (efg(P) && efg(Q)) U.uni(enode(TR, t, P), enode(TR, n + 1, Q));
+        }
+        if (ln == 0 && tx > 0 && cf[n - 1]) {  // (0,63) <-> (63,0) of the down-left tile
+            const uint16_t P = TR[t].edges[192], Q = TR[n - 1].edges[128 + 63];
+            if (efg(P) && efg(Q)) U.uni(enode(TR, t, P), enode(TR, n - 1, Q));
+        }
+    }
+    // left / top edges against empty regions (candidate pairs are done by the neighbour)
+    if (tx > 0 && !cf[t - 1]) {
+        const uint16_t A = TR[t].edges[ln];
+        const int Ap = lane_up1((int)A);
+        if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(U, enode(TR, t, A), rb0 + rr[t - 1]);
+    }
+    if (ty > 0 && !cf[t - ntx]) {
+        const uint16_t A = TR[t].edges[128 + ln];
+        const int Ap = lane_up1((int)A);
+        if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(U, enode(TR, t, A), rb0 + rr[t - ntx]);
+    }
+}
+
+// one wave per candidate, lane = edge position (the global-memory merge; k_resolve below replaces it
+// in the product chain)
 __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     if (a.count[F + f]) return;
     if (FM_MERGE_PRIO) __builtin_amdgcn_s_setprio(FM_MERGE_PRIO);
-    const int ntx = a.ntx, nt = a.ntiles;
-    const uint8_t* cf = a.candf + f * nt;
-    const int32_t* rr = a.regrep + f * nt;
+    const int nt = a.ntiles;
     const TileRec* TR = a.tiles + f * nt;
-    NodeRec* N = a.nodes;
-    const int rb0 = (int)(f * nt);  // region node ids of this frame: rb0 + representative tile
+    (void)TR;  // (read by the bounds check of the checked build)
     const int nc = a.ncr[2 * f];
+    const GlobalUF U{a.nodes};
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int t = a.clist[f * nt + k];
         if (FM_OOB(a, t >= 0 && t < nt && TR[t].nbase >= 0 && TR[t].nbase + TR[t].nroots <= a.nnodes, 5)) continue;
-        const int tx = t % ntx, ty = t / ntx;
-        const bool hasR = tx + 1 < ntx, hasD = ty + 1 < a.nty;
-        // right edge
-        if (hasR) {
-            const uint16_t A = TR[t].edges[64 + ln];
-            const int Ap = lane_up1((int)A);
-            if (cf[t + 1]) {
-                const uint16_t B = TR[t + 1].edges[ln];
-                const int Bp = lane_up1((int)B);
-                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, t + 1, B));
-                if (efg(A)) {
-                    if (ln > 0) {
-                        const uint16_t Bu = TR[t + 1].edges[ln - 1];
-                        if (efg(Bu) && Bu != B) gunion(N, enode(TR, t, A), enode(TR, t + 1, Bu));
-                    }
-                    if (ln < 63) {
-                        const uint16_t Bd = TR[t + 1].edges[ln + 1];
-                        if (efg(Bd) && Bd != B) gunion(N, enode(TR, t, A), enode(TR, t + 1, Bd));
-                    }
-                }
-            } else if (!efg(A) && !(ln > 0 && Ap == A)) {
-                touch_region(N, enode(TR, t, A), rb0 + rr[t + 1]);
-            }
-        }
-        // bottom edge
-        if (hasD) {
-            const int n = t + ntx;
-            const uint16_t A = TR[t].edges[192 + ln];
-            const int Ap = lane_up1((int)A);
-            if (cf[n]) {
-                const uint16_t B = TR[n].edges[128 + ln];
-                const int Bp = lane_up1((int)B);
-                if (efg(A) == efg(B) && !(ln > 0 && Ap == A && Bp == B)) gunion(N, enode(TR, t, A), enode(TR, n, B));
-                if (efg(A)) {
-                    if (ln > 0) {
-                        const uint16_t Bl = TR[n].edges[128 + ln - 1];
-                        if (efg(Bl) && Bl != B) gunion(N, enode(TR, t, A), enode(TR, n, Bl));
-                    }
-                    if (ln < 63) {
-                        const uint16_t Br = TR[n].edges[128 + ln + 1];
-                        if (efg(Br) && Br != B) gunion(N, enode(TR, t, A), enode(TR, n, Br));
-                    }
-                }
-            } else if (!efg(A) && !(ln > 0 && Ap == A)) {
-                touch_region(N, enode(TR, t, A), rb0 + rr[n]);
-            }
-            // corner diagonals (foreground only: both tiles candidates)
-            if (ln == 0 && hasR && cf[n + 1]) {  // (63,63) <-> (0,0) of the down-right tile
-                const uint16_t P = TR[t].edges[192 + 63], Q = TR[n + 1].edges[128];
-                if (efg(P) && efg(Q)) gunion(N, enode(TR, t, P), enode(TR, n + 1, Q));
-            }
-            if (ln == 0 && tx > 0 && cf[n - 1]) {  // (0,63) <-> (63,0) of the down-left tile
-                const uint16_t P = TR[t].edges[192], Q = TR[n - 1].edges[128 + 63];
-                if (efg(P) && efg(Q)) gunion(N, enode(TR, t, P), enode(TR, n - 1, Q));
-            }
-        }
-        // left / top edges against empty regions (candidate pairs are done by the neighbour)
-        if (tx > 0 && !cf[t - 1]) {
-            const uint16_t A = TR[t].edges[ln];
-            const int Ap = lane_up1((int)A);
-            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - 1]);
-        }
-        if (ty > 0 && !cf[t - ntx]) {
-            const uint16_t A = TR[t].edges[128 + ln];
-            const int Ap = lane_up1((int)A);
-            if (!efg(A) && !(ln > 0 && Ap == A)) touch_region(N, enode(TR, t, A), rb0 + rr[t - ntx]);
-        }
+        merge_tile(a, f, t, ln, U);
     }
 }
 
@@ -1042,6 +1073,180 @@ __global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
 __global__ __launch_bounds__(64 * CW) void k_emit_all(FusedArgs a, int f, int32_t* recs, int32_t* cnt, int cap) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     emit_frame(a, (size_t)f, blockIdx.x * CW + wv, gridDim.x * CW, ln, recs, cnt, cap);
+}
+
+// ---------------------------------------------------------------------------
+// k_resolve: k_merge + k_fold + k_emit + k_counts of one frame in one workgroup (round 4).  The
+// frame's union-find lives in LDS -- its empty-region nodes (local id = tile) and the nodes its
+// candidate tiles took from the frame's quota (local id = ntiles + place in the quota) -- so every
+// find and link is an LDS round trip instead of a chain of agent-scope loads and atomics through L2
+// (k_merge spent 88 % of its wave cycles waiting on those), and one launch replaces four.  Foreground
+// bboxes and raster-first keys fold into the root records in HBM with atomics that return nothing;
+// the global parents and the roots' outer flags are written back, so k_emit_all and the contour-area
+// pass read the same records as after k_fold.  A frame whose tiles took nodes from the shared pool,
+// or has more nodes than RV_CAP, runs the same steps on the global union-find.
+constexpr int RV_CAP = 2048;  // LDS nodes per frame: 16 KB (parents + flags)
+__device__ __forceinline__ void agent_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+__device__ __forceinline__ void agent_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+
+__global__ __launch_bounds__(64 * CW) void k_resolve(FusedArgs a) {
+    __shared__ int par[RV_CAP];
+    __shared__ uint32_t fl[RV_CAP];
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+    const size_t f = blockIdx.x;
+    const size_t F = (size_t)a.T * a.S;
+    const int nt = a.ntiles;
+    if (a.tflag_waves == 1)  // the k_fused path's tile flags, cleared for the slot's next batch
+        for (int t = tid; t < nt; t += 64 * CW) a.tflag[f * nt + t] = 0;
+    if (tid == 0) {
+        s_cnt = 0;
+        if (f == 0) {
+            a.h_stats[0] = a.count[2 * F];
+            a.h_stats[1] = a.count[2 * F + 1];
+        }
+    }
+    if (a.count[F + f]) {  // relabelled by the host's pixel-level fallback
+        if (tid == 0) {
+            a.h_count[f] = 0;
+            a.h_overflow[f] = 1;
+        }
+        return;
+    }
+    NodeRec* N = a.nodes;
+    const TileRec* TRf = a.tiles + f * nt;
+    const uint8_t* cf = a.candf + f * nt;
+    const int32_t* rr = a.regrep + f * nt;
+    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
+    const int rb0 = (int)(f * nt);
+    const long long q0 = (long long)F * nt;
+    const int qbase = (int)(q0 + (long long)f * a.nquota);
+    const int used = a.count[2 * F + 2 + f];  // this frame's quota fill (past nquota: the pool was used)
+    const int nl = nt + used;
+    int32_t* recs = a.rec + f * a.cap * 5;
+    const int cap = a.cap;
+    if (used > a.nquota || nl > RV_CAP) {
+        // ---- slow path: the same steps over the global union-find
+        const GlobalUF G{N};
+        for (int k = wv; k < nc; k += CW) {
+            const int t = a.clist[f * nt + k];
+            if (FM_OOB(a, t >= 0 && t < nt && TRf[t].nbase >= 0 && TRf[t].nbase + TRf[t].nroots <= a.nnodes, 5)) continue;
+            merge_tile(a, f, t, ln, G);
+        }
+        agent_release();
+        __syncthreads();
+        agent_acquire();
+        for (int k = wv; k < nc + nr; k += CW) {
+            if (k < nc) {
+                const int t = a.clist[f * nt + k];
+                if (FM_OOB(a, t >= 0 && t < nt, 1)) continue;
+                const int k1 = TRf[t].nroots, nb = TRf[t].nbase;
+                if (FM_OOB(a, nb >= 0 && (long long)nb + k1 <= a.nnodes, 5)) continue;
+                for (int i = ln; i < k1; i += 64) fold_node(N, nb + i);
+            } else if (ln == 0) {
+                const int r = a.rlist[f * nt + (k - nc)];
+                if (FM_OOB(a, r >= 0 && r < nt, 6)) continue;
+                fold_node(N, rb0 + r);
+            }
+        }
+        agent_release();
+        __syncthreads();
+        agent_acquire();
+        emit_frame(a, f, wv, CW, ln, recs, &s_cnt, cap);
+        __syncthreads();
+        if (tid == 0) {
+            a.count[f] = s_cnt;
+            a.h_count[f] = s_cnt;
+            a.h_overflow[f] = 0;
+        }
+        return;
+    }
+    // ---- fast path: the frame's nodes in LDS
+    const LocalUF U{par, fl, rb0, qbase, nt};
+    for (int i = tid; i < nl; i += 64 * CW) {
+        par[i] = i;
+        // region nodes: only the representatives' records are this batch's (the rest are never referenced)
+        fl[i] = i < nt ? (cf[i] == 0 && rr[i] == i ? N[rb0 + i].flags : 0u) : N[qbase + i - nt].flags;
+    }
+    __syncthreads();
+    for (int k = wv; k < nc; k += CW) {
+        const int t = a.clist[f * nt + k];
+        if (FM_OOB(a, t >= 0 && t < nt && TRf[t].nbase >= qbase && TRf[t].nbase + TRf[t].nroots <= qbase + used, 5))
+            continue;
+        merge_tile(a, f, t, ln, U);
+    }
+    __syncthreads();
+    // fold: every node to its root (par flattened), outer flags into the roots' LDS flags, foreground
+    // extents into the roots' records in HBM; global parents written back
+    for (int i = tid; i < nl; i += 64 * CW) {
+        if (i < nt && !(cf[i] == 0 && rr[i] == i)) continue;
+        const int rt = lfind(par, i);
+        par[i] = rt;
+        const int gi = i < nt ? rb0 + i : qbase + i - nt;
+        const int grt = rt < nt ? rb0 + rt : qbase + rt - nt;
+        if (rt == i) continue;
+        N[gi].parent = grt;
+        const uint32_t fi = fl[i];
+        if (fi & 1) {
+            const NodeRec nd = N[gi];
+            atomicMin((unsigned long long*)&N[grt].key, (unsigned long long)nd.key);
+            atomicMin(&N[grt].minx, nd.minx);
+            atomicMax(&N[grt].maxx, nd.maxx);
+            atomicMax(&N[grt].maxy, nd.maxy);
+        } else if (fi & 2) {
+            atomicOr(&fl[rt], 2u);
+        }
+    }
+    agent_release();
+    __syncthreads();
+    agent_acquire();  // the folded root records, as other CUs' atomics left them in L2
+    // emit: the external test at every foreground root, its record into mapped host memory; the roots'
+    // outer flags back into their records (k_emit_all / the area pass read them there)
+    for (int i = tid; i < nl; i += 64 * CW) {
+        if (i < nt && !(cf[i] == 0 && rr[i] == i)) continue;
+        if (par[i] != i) continue;
+        const int gi = i < nt ? rb0 + i : qbase + i - nt;
+        const uint32_t fi = fl[i];
+        if (!(fi & 1)) {
+            if (fi & 2) N[gi].flags = fi;
+            continue;
+        }
+        const uint64_t key = N[gi].key;
+        const uint32_t first = (uint32_t)(key >> 32), ref = (uint32_t)key;
+        const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
+        bool ext;
+        if (ref & REF_OUTER) {
+            ext = true;
+        } else {
+            const int tf = (fy / TS) * a.ntx + fx / TS;  // tile of the raster-first pixel (a candidate)
+            if (FM_OOB(a, tf >= 0 && tf < nt && (!(ref & REF_EDGE) || tf % a.ntx > 0), 7)) continue;
+            int bn;
+            if (ref & REF_EDGE) {
+                const int lt = tf - 1;
+                bn = cf[lt] ? U.loc(enode(TRf, lt, TRf[lt].edges[64 + (ref & 63)])) : rr[lt];
+            } else {
+                bn = U.loc(TRf[tf].nbase + (int)ref);
+            }
+            if (FM_OOB(a, bn >= 0 && bn < nl, 5)) continue;
+            ext = (fl[par[bn]] & 2) != 0;
+        }
+        if (!ext) continue;
+        const int id = atomicAdd(&s_cnt, 1);
+        if (id < cap) {
+            int32_t* rec = recs + (size_t)id * 5;
+            rec[0] = (int32_t)first;
+            rec[1] = N[gi].minx;
+            rec[2] = fy;
+            rec[3] = N[gi].maxx;
+            rec[4] = N[gi].maxy;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.count[f] = s_cnt;
+        a.h_count[f] = s_cnt;
+        a.h_overflow[f] = 0;
+    }
 }
 
 // one workgroup per frame: counts and overflow flags straight into mapped host memory
@@ -1189,6 +1394,19 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     if (mgate_wait) {
         const hipError_t e = hipStreamWaitEvent(st, mgate_wait, 0);
         if (e != hipSuccess) return e;
+    }
+#ifndef FM_CCL_RESOLVE
+#define FM_CCL_RESOLVE 1  // k_resolve (one workgroup per frame, LDS union-find) instead of merge / fold / emit / counts
+#endif
+    if (FM_CCL_RESOLVE) {
+        tok = tm ? tm->begin("resolve", st) : -1;
+        hipLaunchKernelGGL(cc::k_resolve, dim3(F), dim3(64 * cc::CW), 0, st, a);
+        if (tm) tm->end(tok);
+        if (mgate_done) {
+            const hipError_t e = hipEventRecord(mgate_done, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipGetLastError();
     }
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);

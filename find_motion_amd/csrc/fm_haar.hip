@@ -548,7 +548,13 @@ int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
     }
     h->device = device;
     HH(h, hipSetDevice(device));
-    HH(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    {   // the detector's stream at the pixel stream's (high) priority: a motion engine on the same device
+        // always has a pixel launch queued at high priority, and at normal priority the cascade's
+        // launches waited behind them (configs[4]: a 1 ms call took 4.4 ms of wall time)
+        int lo = 0, hi = 0;
+        HH(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HH(h, hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
+    }
     HH(h, hipEventCreate(&h->e0));
     HH(h, hipEventCreate(&h->e1));
     h->win_w = d->win_w;

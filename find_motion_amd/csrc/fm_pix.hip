@@ -213,6 +213,28 @@ __device__ __forceinline__ int swizzle_tile(int b, int n) {
     return (b & 7) * (full >> 3) + (b >> 3);
 }
 
+// XCD-aware 2-D order (round 4): as swizzle_tile, XCD x takes the x-th eighth of the tiles, but in
+// super-tile order -- 8 x 8 tile blocks, row-major over the blocks, row-major inside them (clipped at
+// the grid's right and bottom edges) -- so the 64 workgroups an XCD holds at once (2 per CU) form one
+// 8 x 8 block: their vertical halos are each other's rows too, read through that XCD's L2, where a
+// row-major run of 64 tiles shares only the horizontal ones.  A bijection on [0, ntx * nty).
+__device__ __forceinline__ int block_tile(int b, int ntx, int nty) {
+    const int full = (ntx * nty) & ~7;
+    const int j = b >= full ? b : (b & 7) * (full >> 3) + (b >> 3);  // place in super-tile order
+    const int sr = j / (8 * ntx), R = min(8, nty - 8 * sr);           // super-row, its tile rows
+    const int i = j - sr * 8 * ntx;
+    const int c8 = i / (8 * R), rem = i - 8 * R * c8;                 // column block (the last may be narrower)
+    const int wb = min(8, ntx - 8 * c8);
+    const int r = rem / wb, cc = rem - r * wb;
+    return (8 * sr + r) * ntx + 8 * c8 + cc;
+}
+#ifndef FM_PIX_ORDER
+#define FM_PIX_ORDER 1  // tile order of k_pix5 / k_pixw: 1 = block_tile (2-D), 0 = swizzle_tile (row-major runs)
+#endif
+__device__ __forceinline__ int pix_tile(int b, const FusedArgs& a) {
+    return FM_PIX_ORDER ? block_tile(b, a.ntx, a.nty) : swizzle_tile(b, a.ntiles);
+}
+
 // OpenCV's 8-bit fixed-point Gaussian taps (getGaussianKernelBitExact +
 // error-diffusion rounding, restated in fm_capi.cpp gaussian_taps); fixed at
 // compile time so they are instruction literals.  launch_pix checks them
@@ -691,20 +713,24 @@ template <int K> constexpr int tap_hi() {
     return i;
 }
 
-template <int KC>
+// NWB: waves of the workgroup, each over 8 rows: NWB = 8 the 64 x 64 tile, NWB = 16 a 64-wide, 128-row
+// band (two contour tiles: the 2R-row vertical halo is read once per 128 rows instead of per 64)
+template <int KC, int NWB = 8>
 struct PW {
     static constexpr int R = KC / 2;
     static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
-    static constexpr int GH = TS + 2 * R;          // gray rows (even)
+    static constexpr int NTB = 64 * NWB;           // threads
+    static constexpr int TH = RPWV * NWB;          // rows
+    static constexpr int GH = TH + 2 * R;          // gray rows (even)
     static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
     static constexpr int NG = GH * GQ;             // gray jobs per frame
     static constexpr int GSLOTS = (NG + 63) / 64;
-    static constexpr int gcnt(int w) { return (GSLOTS - w + NW - 1) / NW; }  // gray slots of wave w: i * NW + w
+    static constexpr int gcnt(int w) { return (GSLOTS - w + NWB - 1) / NWB; }  // gray slots of wave w: i * NWB + w
     static constexpr int GJ = gcnt(0);             // gray rounds per wave
     static constexpr int NHP = GH / 2;             // H row pairs
     static constexpr int NH = NHP * (TS / 4);      // tap jobs
-    static constexpr int HJ = (NH + NT - 1) / NT;
-    static constexpr int HLASTW = (NH - (HJ - 1) * NT + 63) / 64;  // waves with a job in the last round
+    static constexpr int HJ = (NH + NTB - 1) / NTB;
+    static constexpr int HLASTW = (NH - (HJ - 1) * NTB + 63) / 64;  // waves with a job in the last round
     static constexpr int GS = GQ;                  // gray row stride in LDS (dwords)
     static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
     static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
@@ -739,10 +765,12 @@ template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of o
 // chain_rows over H row pairs with even-aligned pair windows: output row j's window starts on an
 // even H row, absorbing a zero tap (outside the kernel, or one of OpenCV's zero end taps) on the
 // side the row parity needs, so no pair is rebuilt with v_alignbit
+// wv: the wave within its workgroup (H rows, image rows); wb: its 8-row slice of the 64-row contour
+// tile (flag rows: FLAG_T* from slice 0, FLAG_B* from slice 7) -- the same as wv for a 64-row workgroup
 template <int KC, bool KEEP, bool TAIL>
 __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
                                              int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
-                                             uint32_t& flags) {
+                                             uint32_t& flags, int wb) {
     using G = PW<KC>;
     uint32_t P[G::NP];
     const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
@@ -778,12 +806,12 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     tb &= cc.tbmask;
     colbits = tb;
     const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
-    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
-    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
+    const uint64_t top = wb == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = wb == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
     uint32_t fl = 0;
     if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
-    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
-    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    if (wb == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (wb == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
     flags = fl;
 }
 
@@ -856,72 +884,103 @@ __device__ __forceinline__ uint32_t hs_tap(const uint32_t (&q)[N], const uint32_
 // quad just outside the image from the mirrored quad beside it (REFLECT_101).
 // Needs w % 4 == 0 and w >= 8 (4-B aligned quads, one real quad each side);
 // one barrier per frame as in k_pix.
-constexpr int P5_GH = TS + 4;            // gray rows y0-2 .. y0+65
-constexpr int P5_GQ = 18;                // gray quads per row: columns x0-4 .. x0+67
-constexpr int P5_NG = P5_GH * P5_GQ;     // gray jobs per frame
-// Gray jobs go to waves in whole wave-slots of 64 jobs.  Waves 4..7 lose issue arbitration to
-// waves 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves 0..3 spent
-// ~30 % of their cycles in the barrier), so waves 0..3 take P5_GFAST slots each and waves 4..7 the
-// rest; the partial last slot goes to wave 3.
+#ifndef FM_P5_EVENP
+#define FM_P5_EVENP 1  // k_pix5's chain on even-aligned pair windows (chain_rows_w)
+#endif
 #ifndef FM_P5_GFAST
 #define FM_P5_GFAST 4  // (A/B: 4 >= 3 > 5)
 #endif
-constexpr int P5_GSLOTS = (P5_NG + 63) / 64;                                   // 20
-constexpr int P5_GFAST = FM_P5_GFAST;
-constexpr int P5_GSLOW = (P5_GSLOTS - 4 * P5_GFAST + 3) / 4;
-constexpr int P5_GJ = P5_GFAST > P5_GSLOW ? P5_GFAST : P5_GSLOW;                 // load rounds per wave
-static_assert(P5_GSLOW >= 0 && 4 * (P5_GFAST + P5_GSLOW) >= P5_GSLOTS, "gray slots");
 // Tap jobs cover 2 H rows x 4 columns and store them as row pairs (one ds_write_b128), which the chain
 // reads back as six dwords instead of twelve u16 reads and their merges (FM_P5_HPAIR 0: 1 x 4 jobs,
 // row-major H, as k_pix)
 #ifndef FM_P5_HPAIR
 #define FM_P5_HPAIR 1
 #endif
-constexpr int P5_HR = FM_P5_HPAIR ? 2 : 1;                 // H rows per tap job
-constexpr int P5_NH = (P5_GH / P5_HR) * (TS / 4);  // tap jobs per frame
 // tap jobs likewise (FM_P5_HFAST slots to each of waves 0..3); 0 keeps the round-robin deal
 #ifndef FM_P5_HFAST
 #define FM_P5_HFAST 0
 #endif
-constexpr int P5_HSLOTS = (P5_NH + 63) / 64;                                   // 17
-constexpr int P5_HFAST = FM_P5_HFAST;
-constexpr int P5_HSLOW = P5_HFAST ? (P5_HSLOTS - 4 * P5_HFAST + 3) / 4 : 0;
-constexpr int P5_HJ = P5_HFAST ? (P5_HFAST > P5_HSLOW ? P5_HFAST : P5_HSLOW) : (P5_NH + NT - 1) / NT;
-static_assert(!P5_HFAST || (P5_HSLOW >= 0 && 4 * (P5_HFAST + P5_HSLOW) >= P5_HSLOTS), "tap slots");
-// the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
-constexpr int P5_HLASTW = (P5_NH - (P5_HJ - 1) * NT + 63) / 64;  // 1 of 8
-constexpr int P5_GBUF = P5_NG + 64;      // + a pad slot per lane for the idle jobs' stores (branch-free)
-constexpr int P5_HROW = TS;              // u16 per H row
-constexpr int P5_HBUF = (P5_GH + P5_HR) * P5_HROW;  // + the pad row (pair) idle tap jobs store to
-constexpr int p5_lds_bytes() { return 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2 + 256 * 8; }
+// k_pix5 geometry for a workgroup of NWB waves over a band of 8 * NWB tile rows (NWB = 8: the 64 x 64
+// tile; small work images -- mode D's 100 x 56 is two tiles -- take bands of 8 or 16 rows so that more
+// workgroups share the per-frame critical path)
+template <int NWB>
+struct P5G {
+    static constexpr int NTB = 64 * NWB;                 // threads
+    static constexpr int TH = RPWV * NWB;                // band rows
+    static constexpr int GH = TH + 4;                    // gray rows y0-2 .. y0+TH+1
+    static constexpr int GQ = 18;                        // gray quads per row: columns x0-4 .. x0+67
+    static constexpr int NG = GH * GQ;                   // gray jobs per frame
+    // Gray jobs go to waves in whole wave-slots of 64 jobs.  In a 64-row workgroup waves 4..7 lose issue
+    // arbitration to waves 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves
+    // 0..3 spent ~30 % of their cycles in the barrier), so waves 0..3 take GFAST slots each and waves
+    // 4..7 the rest; the partial last slot goes to wave 3.  Narrower bands deal them round robin.
+    static constexpr int GSLOTS = (NG + 63) / 64;
+    static constexpr int GFAST = NWB == 8 ? FM_P5_GFAST : (GSLOTS + NWB - 1) / NWB;
+    static constexpr int GSLOW = NWB == 8 ? (GSLOTS - 4 * GFAST + 3) / 4 : GFAST;
+    static constexpr int GJ = GFAST > GSLOW ? GFAST : GSLOW;  // load rounds per wave
+    static constexpr int HR = FM_P5_HPAIR ? 2 : 1;       // H rows per tap job
+    static constexpr int NH = (GH / HR) * (TS / 4);      // tap jobs per frame
+    static constexpr int HFAST = NWB == 8 ? FM_P5_HFAST : 0;
+    static constexpr int HSLOTS = (NH + 63) / 64;
+    static constexpr int HSLOW = HFAST ? (HSLOTS - 4 * HFAST + 3) / 4 : 0;
+    static constexpr int HJ = HFAST ? (HFAST > HSLOW ? HFAST : HSLOW) : (NH + NTB - 1) / NTB;
+    // the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
+    static constexpr int HLASTW = (NH - (HJ - 1) * NTB + 63) / 64;
+    static constexpr int GBUF = NG + 64;                 // + a pad slot per lane for the idle jobs' stores (branch-free)
+    static constexpr int HROW = TS;                      // u16 per H row
+    static constexpr int HBUF = (GH + HR) * HROW;        // + the pad row (pair) idle tap jobs store to
+    static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
+};
+static_assert(P5G<8>::GSLOW >= 0 && 4 * (P5G<8>::GFAST + P5G<8>::GSLOW) >= P5G<8>::GSLOTS, "gray slots");
+static_assert(!P5G<8>::HFAST || (P5G<8>::HSLOW >= 0 && 4 * (P5G<8>::HFAST + P5G<8>::HSLOW) >= P5G<8>::HSLOTS), "tap slots");
+template <int NWB> constexpr int p5_lds_bytes() { return P5G<NWB>::bytes; }
 
+template <int GJ>
 struct P5Raw {
-    u32x3_t v[P5_GJ];  // one 96-bit value per job: one register triple the allocator keeps whole
+    u32x3_t v[GJ];  // one 96-bit value per job: one register triple the allocator keeps whole
 };
 
 // KEEP: some stream has a keep-mask (streams without one get all-keep bytes); TAIL: the image has
 // accumulateWeighted's scalar tail (h*w % 16 != 0), so some waves take the per-pixel test.  Fixed
 // per launch, so the common kernel has a single chain path: a per-wave 3-way branch inside the
 // frame loop made the background registers a phi and cost 8 v_mov_b64 per frame.
-template <bool KEEP, bool TAIL>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+template <int NWB, bool KEEP, bool TAIL>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+    using G = P5G<NWB>;
+    static_assert(FM_P5_EVENP || NWB == 8, "bands need the even-pair chain (its flag rows follow wb)");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int KC = 5, R = 2;
-    uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][P5_GBUF]
-    uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * P5_GBUF * 4);          // [2][P5_HBUF]
-    double* atab = reinterpret_cast<double*>(smem + 2 * P5_GBUF * 4 + 2 * P5_HBUF * 2);
+    uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
+    uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
+    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
-    const int ti = swizzle_tile(blockIdx.x, a.ntiles);
     const int h = a.h, w = a.w, S = a.S;
-    const int tx = ti % a.ntx, ty = ti / a.ntx;
-    const int x0 = tx * TS, y0 = ty * TS;
+    int ti, tx, y0, wb0;  // contour tile, its column, the band's first row, its first 8-row slice of the tile
+    if constexpr (NWB == 8) {
+        ti = pix_tile(blockIdx.x, a);
+        tx = ti % a.ntx;
+        y0 = (ti / a.ntx) * TS;
+        wb0 = 0;
+    } else {
+        const int nby = (h + G::TH - 1) / G::TH;
+        const int bt = FM_PIX_ORDER ? block_tile(blockIdx.x, a.ntx, nby) : swizzle_tile(blockIdx.x, a.ntx * nby);
+        tx = bt % a.ntx;
+        y0 = (bt / a.ntx) * G::TH;
+        ti = (y0 / TS) * a.ntx + tx;
+        wb0 = (y0 % TS) / RPWV;
+    }
+    const int x0 = tx * TS;
     const size_t plane = (size_t)h * w;
     const size_t fbytes = plane * 3;
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
-    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+    if constexpr (NWB >= 4) {
+        if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+    } else {
+        for (int i = tid; i < 256; i += G::NTB) atab[i] = __dmul_rn((double)i, a.alpha);
+    }
 #ifdef FM_DEV_SWITCHES
     // profiling only (FM_PTS, dev build): [hw_id | xcc_id << 32, realtime start, realtime end, memtime cycles]
     uint64_t* pts = (a.dbg_pts && tid == 0) ? a.dbg_pts + ((size_t)s * a.ntiles + ti) * 4 : nullptr;
@@ -934,42 +993,43 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #endif
 
     // ---- per-thread job plans (frame invariant)
-    uint32_t goff[P5_GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
-    uint32_t gdst[P5_GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
-    const int gjobs = wv < 4 ? P5_GFAST : P5_GSLOW;  // this wave's gray slots (wave-uniform)
+    uint32_t goff[G::GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
+    uint32_t gdst[G::GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
+    // this wave's gray slots (wave-uniform): the 4 / 4 deal in a 64-row workgroup, contiguous runs in a band
+    const int gjobs = NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : max(0, min(G::GFAST, G::GSLOTS - wv * G::GFAST));
 #pragma unroll
-    for (int i = 0; i < P5_GJ; i++) {
-        const int slot = wv >= 4 ? (wv - 4) * P5_GSLOW + i : 4 * P5_GSLOW + wv * P5_GFAST + i;
-        const int j = i < gjobs ? slot * 64 + ln : P5_NG;  // rounds past the wave's slots: idle (dummy load)
-        const int gr = j / P5_GQ, gq = j - gr * P5_GQ;
+    for (int i = 0; i < G::GJ; i++) {
+        const int slot = NWB == 8 ? (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i) : wv * G::GFAST + i;
+        const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
+        const int gr = j / G::GQ, gq = j - gr * G::GQ;
         const int x = x0 - 4 + 4 * gq;
-        const bool live = j < P5_NG && x >= 0 && x + 4 <= w;
+        const bool live = j < G::NG && x >= 0 && x + 4 <= w;
         const int y = reflect101(y0 - R + gr, h);
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < P5_NG ? (uint32_t)j : (uint32_t)(P5_NG + ln);
+        gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
     }
-    uint32_t hsrc[P5_HJ], hdst[P5_HJ];
-    const int hjobs = P5_HFAST ? (wv < 4 ? P5_HFAST : P5_HSLOW) : P5_HJ;  // this wave's tap rounds (wave-uniform)
+    uint32_t hsrc[G::HJ], hdst[G::HJ];
+    const int hjobs = G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < P5_HJ; i++) {
-        const int hslot = wv >= 4 ? (wv - 4) * P5_HSLOW + i : 4 * P5_HSLOW + wv * P5_HFAST + i;
-        const int j = P5_HFAST ? (i < hjobs ? hslot * 64 + ln : P5_NH) : tid + NT * i;
-        const bool live = j < P5_NH;
+    for (int i = 0; i < G::HJ; i++) {
+        const int hslot = wv >= 4 ? (wv - 4) * G::HSLOW + i : 4 * G::HSLOW + wv * G::HFAST + i;
+        const int j = G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
+        const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
-        hsrc[i] = (uint32_t)(P5_HR * hr * P5_GQ + hq);
+        hsrc[i] = (uint32_t)(G::HR * hr * G::GQ + hq);
         // FM_P5_HPAIR: u32 index of the pair's 4 columns, else u16 index of the row's
-        hdst[i] = FM_P5_HPAIR ? (uint32_t)((live ? hr : P5_GH / 2) * TS + 4 * hq)
-                              : (uint32_t)((live ? hr : P5_GH) * P5_HROW + 4 * hq);
+        hdst[i] = FM_P5_HPAIR ? (uint32_t)((live ? hr : G::GH / 2) * TS + 4 * hq)
+                              : (uint32_t)((live ? hr : G::GH) * G::HROW + 4 * hq);
     }
     // REFLECT_101 quads: left of column 0 (tile x0 = 0, tap quad 0 reads gray quad 0 = columns -4..-1:
     // bytes 2, 3 = gray(2), gray(1) from quad 1) and the quad starting at column w (bytes 0, 1 =
     // gray(w-2), gray(w-3) from the quad before it); further quads feed only columns past the image
     const bool edge_tile = x0 == 0 || x0 + TS + 4 > w;  // workgroup-uniform
     const int vq = (w - x0 + 4) / 4;  // gray quad index of the quad starting at column w
-    uint32_t hfix[P5_HJ];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
+    uint32_t hfix[G::HJ];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
 #pragma unroll
-    for (int i = 0; i < P5_HJ; i++) {
-        const int hq = (int)(hsrc[i] % P5_GQ);
+    for (int i = 0; i < G::HJ; i++) {
+        const int hq = (int)(hsrc[i] % G::GQ);
         hfix[i] = (x0 == 0 && hq == 0 ? 1u : 0u) | (hq + 1 == vq ? 2u : 0u) | (hq + 2 == vq ? 4u : 0u);
     }
 
@@ -1004,15 +1064,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #ifndef FM_HSHIFT
 #define FM_HSHIFT 1  // horizontal taps with shifted constants (HS) instead of v_alignbyte windows
 #endif
-#ifndef FM_P5_EVENP
-#define FM_P5_EVENP 1  // k_pix5's chain on even-aligned pair windows (chain_rows_w)
-#endif
     uint32_t cpk[2];
     cpk[0] = tap4<KC>(0);
     cpk[1] = tap4<KC>(1);
     uint32_t hcs[HS<KC>::NC];
     if (FM_HSHIFT) hs_consts<KC>(hcs);
-    P5Raw rw;
+    P5Raw<G::GJ> rw;
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
@@ -1020,21 +1077,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
-        for (int i = 0; i < P5_GJ; i++) {
+        for (int i = 0; i < G::GJ; i++) {
             load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < P5_GJ; i++) {
+        for (int i = 0; i < G::GJ; i++) {
             if (i >= gjobs) break;  // wave-uniform
             gb[gdst[i]] = gray4(rw.v[i].x, rw.v[i].y, rw.v[i].z);
         }
     };
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < P5_HJ; i++) {
-            if (P5_HFAST ? i >= hjobs : (i == P5_HJ - 1 && wv >= P5_HLASTW)) break;  // wave-uniform
+        for (int i = 0; i < G::HJ; i++) {
+            if (G::HFAST ? i >= hjobs : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
             if (edge_tile) {
@@ -1048,7 +1105,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             const uint32_t h2 = FM_HSHIFT ? hs_tap<KC, 2>(qv, hcs) : htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
             const uint32_t h3 = FM_HSHIFT ? hs_tap<KC, 3>(qv, hcs) : htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
             if (FM_P5_HPAIR) {  // the next gray row, then both rows' sums as row pairs
-                uint32_t qw[4] = {gb[hsrc[i] + P5_GQ], gb[hsrc[i] + P5_GQ + 1], gb[hsrc[i] + P5_GQ + 2], 0u};
+                uint32_t qw[4] = {gb[hsrc[i] + G::GQ], gb[hsrc[i] + G::GQ + 1], gb[hsrc[i] + G::GQ + 2], 0u};
                 if (edge_tile) {
                     if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
                     if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
@@ -1086,7 +1143,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
     load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
-    if (t0 + 1 < t1) gray_stage(gray + P5_GBUF);
+    if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
     load((size_t)min(t0 + 2, t1 - 1) * S + s);
 
     // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
@@ -1120,14 +1177,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
         var = __builtin_amdgcn_readfirstlane(var);
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
         // chain_rows reads H as row pairs (FM_P5_HPAIR) or as [row][RSH = 64] u16
-        const uint16_t* Hb = Hs + b * P5_HBUF;
+        const uint16_t* Hb = Hs + b * G::HBUF;
         if (!(skip & 2)) {
-            if (FM_P5_EVENP && FM_P5_HPAIR) {
+            if constexpr ((FM_P5_EVENP != 0) && (FM_P5_HPAIR != 0)) {
                 const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hb);
+                const int wbf = NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb0 + wv);
                 if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                    chain_rows_w<KC, KEEP, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
                 else
-                    chain_rows_w<KC, KEEP, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                    chain_rows_w<KC, KEEP, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
             } else if (!TAIL || var == 0) {
                 chain_rows<KC, false, false, KEEP, false, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
                                                                          colbits, fl);
@@ -1137,17 +1195,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
             }
         }
         P5_PH(ph1);
-        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * P5_GBUF, Hs + (b ^ 1) * P5_HBUF);
+        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         P5_PH(ph2);
         // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
         // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
         // makes every frame wait for the stores below before the next loads
-        if (!(skip & 1)) gray_stage(gray + b * P5_GBUF);
+        if (!(skip & 1)) gray_stage(gray + b * G::GBUF);
         // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
         // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
         // the prefetch would be waited for with it
-        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wb0 + wv] = (uint8_t)colbits;
+        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wb0 + wv] = fl;
         // unconditional (see load): past the batch's last frame it re-reads that frame
         if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
     }
@@ -1197,9 +1255,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))
 #ifndef FM_PIXW_WPE
 #define FM_PIXW_WPE 4  // 2 workgroups per CU (<= 128 VGPRs)
 #endif
-template <int KC, bool KEEP, bool TAIL>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
-    using G = PW<KC>;
+template <int KC, int NWB, bool KEEP, bool TAIL>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
+    using G = PW<KC, NWB>;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
@@ -1208,21 +1266,36 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE)
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
-    const int ti = swizzle_tile(blockIdx.x, a.ntiles);
     const int h = a.h, w = a.w, S = a.S;
-    const int tx = ti % a.ntx, ty = ti / a.ntx;
-    const int x0 = tx * TS, y0 = ty * TS;
+    int ti, tx, y0, wb;  // the wave's contour tile, the band's column, first row, the wave's 8-row slice of its tile
+    bool tile_ok = true;  // (a 128-row band's second tile may lie past the grid)
+    if constexpr (NWB == 8) {
+        ti = pix_tile(blockIdx.x, a);
+        tx = ti % a.ntx;
+        y0 = (ti / a.ntx) * TS;
+        wb = wv;
+    } else {
+        const int nby = (h + G::TH - 1) / G::TH;
+        const int bt = FM_PIX_ORDER ? block_tile(blockIdx.x, a.ntx, nby) : swizzle_tile(blockIdx.x, a.ntx * nby);
+        tx = bt % a.ntx;
+        y0 = (bt / a.ntx) * G::TH;
+        const int tyw = (y0 + RPWV * wv) / TS;
+        tile_ok = tyw < a.nty;
+        ti = tyw * a.ntx + tx;
+        wb = (RPWV * wv % TS) / RPWV;
+    }
+    const int x0 = tx * TS;
     const size_t plane = (size_t)h * w;
     const size_t fbytes = plane * 3;
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
-    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);  // (NWB >= 4)
 
     // ---- per-thread job plans (frame invariant)
     uint32_t goff[G::GJ], gdst[G::GJ];
 #pragma unroll
     for (int i = 0; i < G::GJ; i++) {
-        const int slot = i * NW + wv;
+        const int slot = i * NWB + wv;
         const int j = (i < G::gcnt(wv) && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
         const int gr = j / GQ, gq = j - gr * GQ;
         const int x = x0 - PC + 4 * gq;
@@ -1236,7 +1309,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE)
     int hqv[G::HJ];
 #pragma unroll
     for (int i = 0; i < G::HJ; i++) {
-        const int j = tid + NT * i;
+        const int j = tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
         hqv[i] = hq;
@@ -1350,13 +1423,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE)
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
         const uint32_t* Hb = Hs + b * G::HBUF;
         if (!TAIL || var == 0)
-            chain_rows_w<KC, KEEP, false>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            chain_rows_w<KC, KEEP, false>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
+                                          NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
         else
-            chain_rows_w<KC, KEEP, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            chain_rows_w<KC, KEEP, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
+                                         NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
         if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         gray_stage(gray + b * G::GBUF);
-        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        if (NWB == 8 || tile_ok) {
+            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wb] = (uint8_t)colbits;
+            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wb] = fl;
+        }
         load((size_t)min(t + 3, t1 - 1) * S + s);
     }
     double* bgo = a.bg_out + (size_t)s * plane;
@@ -1391,26 +1468,62 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
     if (!ok) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
     if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
-        px::p5_lds_bytes() <= 64 * 1024) {
+        px::p5_lds_bytes<8>() <= 64 * 1024) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
-        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
-        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
-        else hipLaunchKernelGGL((px::k_pix5<false, false>), grid, dim3(px::NT), px::p5_lds_bytes(), st, a);
+        // Small work images (mode D's 100 x 56 is two tiles, 256 frames in a row on two CUs): bands of
+        // 8 or 16 rows, so the per-frame critical path (barrier, chain, taps, gray) is spread over
+        // 8x / 4x the workgroups; 64-row tiles once the grid fills the chip
+        const int nwb = a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
+        const int nby = (a.h + 8 * nwb - 1) / (8 * nwb);
+        const dim3 bgrid(a.ntx * nby, a.S);
+#define FM_P5_LAUNCH(NWB)                                                                                          \
+    do {                                                                                                           \
+        const size_t lds = px::p5_lds_bytes<NWB>();                                                                \
+        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<NWB, true, true>), bgrid, dim3(64 * NWB), lds, st, a);    \
+        else if (keep) hipLaunchKernelGGL((px::k_pix5<NWB, true, false>), bgrid, dim3(64 * NWB), lds, st, a);      \
+        else if (tail) hipLaunchKernelGGL((px::k_pix5<NWB, false, true>), bgrid, dim3(64 * NWB), lds, st, a);      \
+        else hipLaunchKernelGGL((px::k_pix5<NWB, false, false>), bgrid, dim3(64 * NWB), lds, st, a);               \
+    } while (0)
+        if (nwb == 8) FM_P5_LAUNCH(8);
+        else if (nwb == 2) FM_P5_LAUNCH(2);
+        else FM_P5_LAUNCH(1);
+#undef FM_P5_LAUNCH
         return hipGetLastError();
     }
 #ifndef FM_PIXW
 #define FM_PIXW 1  // k = 21 steady state on k_pixw (0: k_pix<21>, the round-2 kernel)
 #endif
+#ifndef FM_PIXW_TALL
+#define FM_PIXW_TALL 1  // large grids: 128-row bands of 16 waves (one workgroup per CU) instead of 64 x 64 tiles
+#endif
     if (FM_PIXW && a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 &&
         ((uintptr_t)a.src & 3) == 0) {
-        using G = px::PW<21>;
-        static_assert(G::bytes <= 64 * 1024, "k_pixw LDS");
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        if (keep && tail) hipLaunchKernelGGL((px::k_pixw<21, true, true>), grid, dim3(px::NT), G::bytes, st, a);
-        else if (keep) hipLaunchKernelGGL((px::k_pixw<21, true, false>), grid, dim3(px::NT), G::bytes, st, a);
-        else if (tail) hipLaunchKernelGGL((px::k_pixw<21, false, true>), grid, dim3(px::NT), G::bytes, st, a);
-        else hipLaunchKernelGGL((px::k_pixw<21, false, false>), grid, dim3(px::NT), G::bytes, st, a);
+#define FM_PIXW_LAUNCH(NWB, GRID)                                                                                     \
+    do {                                                                                                              \
+        using G = px::PW<21, NWB>;                                                                                    \
+        static_assert(G::bytes <= 160 * 1024, "k_pixw LDS");                                                          \
+        if (keep && tail) {                                                                                           \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, true>), GRID, dim3(64 * NWB), G::bytes, st, a);             \
+        } else if (keep) {                                                                                            \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, false>), GRID, dim3(64 * NWB), G::bytes, st, a);            \
+        } else if (tail) {                                                                                            \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, true>), GRID, dim3(64 * NWB), G::bytes, st, a);            \
+        } else {                                                                                                      \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, false>), GRID, dim3(64 * NWB), G::bytes, st, a);           \
+        }                                                                                                             \
+    } while (0)
+        if (FM_PIXW_TALL && a.nty >= 4 && a.ntiles * a.S >= 2048) {
+            const dim3 tgrid(a.ntx * ((a.h + 127) / 128), a.S);
+            FM_PIXW_LAUNCH(16, tgrid);
+        } else {
+            FM_PIXW_LAUNCH(8, grid);
+        }
+#undef FM_PIXW_LAUNCH
         return hipGetLastError();
     }
 #define FM_PIX_LAUNCH(K, P, I)                                                                                \

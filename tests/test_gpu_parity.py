@@ -159,6 +159,14 @@ def test_4k_k21_masks_config5_geometry():
     run_pair(3840, 2160, 3840, blur_scale=183, T=1, n_batches=2, masks=masks, keep_planes=False)
 
 
+def test_k21_tall_bands_odd_tile_rows():
+    """k = 21 on k_pixw's 128-row bands (a grid of >= 2048 tile-streams: 16 x 15 tiles x 9 streams): 15 tile
+    rows, so the last band's second 64-row tile lies past the grid and its waves store nothing; masks on
+    every stream, REFLECT_101 at the band edges."""
+    masks = [((0, 0), (200, 150)), ((1023, 899), (700, 899), (1023, 600))]
+    run_pair(1024, 900, 1024, ksize=21, S=9, T=2, n_batches=2, masks=masks, keep_planes=False, start=40)
+
+
 @pytest.mark.parametrize("W,H,S", [(200, 131, 2), (40, 30, 1), (1000, 70, 1), (320, 240, 3), (203, 90, 1)])
 def test_k21_wide_kernel_geometries(W, H, S):
     """k = 21 steady state (k_pixw, no planes): a right tile 8 px wide, both REFLECT_101 edges in one tile
