@@ -964,7 +964,9 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
         y0 = (ti / a.ntx) * TS;
         wb0 = 0;
     } else {
-        const int nby = (h + G::TH - 1) / G::TH;
+        // the bands tile every contour tile whole: the slices of the last tile below the image are
+        // written as zeros (no bits, no flags) as the 64-row kernel writes them, not left stale
+        const int nby = a.nty * (TS / G::TH);
         const int bt = FM_PIX_ORDER ? block_tile(blockIdx.x, a.ntx, nby) : swizzle_tile(blockIdx.x, a.ntx * nby);
         tx = bt % a.ntx;
         y0 = (bt / a.ntx) * G::TH;
@@ -1474,7 +1476,7 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
         // 8 or 16 rows, so the per-frame critical path (barrier, chain, taps, gray) is spread over
         // 8x / 4x the workgroups; 64-row tiles once the grid fills the chip
         const int nwb = a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
-        const int nby = (a.h + 8 * nwb - 1) / (8 * nwb);
+        const int nby = a.nty * (8 / nwb);  // bands covering every 64-row contour tile whole
         const dim3 bgrid(a.ntx * nby, a.S);
 #define FM_P5_LAUNCH(NWB)                                                                                          \
     do {                                                                                                           \
