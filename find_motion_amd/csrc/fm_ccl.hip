@@ -1396,7 +1396,10 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
         if (e != hipSuccess) return e;
     }
 #ifndef FM_CCL_RESOLVE
-#define FM_CCL_RESOLVE 1  // k_resolve (one workgroup per frame, LDS union-find) instead of merge / fold / emit / counts
+#define FM_CCL_RESOLVE 0  // k_resolve (one workgroup per frame, LDS union-find) instead of merge / fold / emit / counts.
+                          // Measured (round 4, 2 alternating rounds): 401.6 vs 415.7 k frames/s, pixel launches
+                          // 619-773 vs 557-597 us beside the chains: the per-frame workgroups hold their CU slots
+                          // far longer than k_merge's short waves; off
 #endif
     if (FM_CCL_RESOLVE) {
         tok = tm ? tm->begin("resolve", st) : -1;

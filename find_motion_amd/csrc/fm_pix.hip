@@ -229,7 +229,9 @@ __device__ __forceinline__ int block_tile(int b, int ntx, int nty) {
     return (8 * sr + r) * ntx + 8 * c8 + cc;
 }
 #ifndef FM_PIX_ORDER
-#define FM_PIX_ORDER 1  // tile order of k_pix5 / k_pixw: 1 = block_tile (2-D), 0 = swizzle_tile (row-major runs)
+#define FM_PIX_ORDER 0  // tile order of k_pix5 / k_pixw: 1 = block_tile (2-D), 0 = swizzle_tile (row-major runs).
+                        // Measured (round 4, 2 alternating rounds): k_pixw at config 5 3.19 / 3.33 ms per launch
+                        // (row-major / 2-D), the driver's line 406.6 / 401.6 k frames/s: row-major stays
 #endif
 __device__ __forceinline__ int pix_tile(int b, const FusedArgs& a) {
     return FM_PIX_ORDER ? block_tile(b, a.ntx, a.nty) : swizzle_tile(b, a.ntiles);
@@ -1472,10 +1474,14 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
     if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
         px::p5_lds_bytes<8>() <= 64 * 1024) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        // Small work images (mode D's 100 x 56 is two tiles, 256 frames in a row on two CUs): bands of
-        // 8 or 16 rows, so the per-frame critical path (barrier, chain, taps, gray) is spread over
-        // 8x / 4x the workgroups; 64-row tiles once the grid fills the chip
-        const int nwb = a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
+        // FM_P5_BANDS: small work images (mode D's 100 x 56 is two tiles, 256 frames in a row on two CUs)
+        // on bands of 8 or 16 rows.  Measured (round 4): mode D 470 k -> 479 k frames/s, the pixel kernel
+        // 417 vs 320-466 us per 256 frames -- a frame's critical path is per wave (its 8-row chain and its
+        // share of gray and taps), which a band does not shorten; off
+#ifndef FM_P5_BANDS
+#define FM_P5_BANDS 0
+#endif
+        const int nwb = !FM_P5_BANDS || a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
         const int nby = a.nty * (8 / nwb);  // bands covering every 64-row contour tile whole
         const dim3 bgrid(a.ntx * nby, a.S);
 #define FM_P5_LAUNCH(NWB)                                                                                          \
@@ -1496,7 +1502,8 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
 #define FM_PIXW 1  // k = 21 steady state on k_pixw (0: k_pix<21>, the round-2 kernel)
 #endif
 #ifndef FM_PIXW_TALL
-#define FM_PIXW_TALL 1  // large grids: 128-row bands of 16 waves (one workgroup per CU) instead of 64 x 64 tiles
+#define FM_PIXW_TALL 0  // large grids on 128-row bands of 16 waves (one workgroup per CU) instead of 64 x 64 tiles.
+                        // Measured (round 4, 2 alternating rounds, config 5): 3.61 vs 3.33 ms per launch: off
 #endif
     if (FM_PIXW && a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 &&
         ((uintptr_t)a.src & 3) == 0) {
