@@ -393,8 +393,8 @@ def main() -> None:
         if not pick:
             return
         t0 = time.perf_counter()
-        roi = torch.stack([ring[base_t + t, s] for t, s in pick])
-        found = det.detect_frames(roi, 300, 1.1, 5)
+        # the ROI frames where they lie in the ring (written before the timed region): no gather copy
+        found = det.detect_frame_list([ring[base_t + t, s].data_ptr() for t, s in pick], H, W, 300, 1.1, 5)
         haar["wall_s"] += time.perf_counter() - t0
         haar["device_ms"] += det.last_ms()
         haar["calls"] += 1

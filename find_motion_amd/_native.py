@@ -31,7 +31,7 @@ EXPORTED = (
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
     "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device", "fm_mjpeg_geometry",
-    "fm_submit_streams", "fm_footprint",
+    "fm_submit_streams", "fm_footprint", "fm_haar_detect_frame_list",
 )
 
 
@@ -116,6 +116,7 @@ def load() -> C.CDLL:
     L.fm_haar_detect.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, i32, i32, i32, i32, vp, i32, vp]
     L.fm_haar_candidates.argtypes = [vp, vp, i32]
     L.fm_haar_detect_frames.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
+    L.fm_haar_detect_frame_list.argtypes = [vp, vp, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
     L.fm_haar_last_ms.argtypes = [vp]
     L.fm_haar_last_ms.restype = C.c_double
     L.fm_mjpeg_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -494,6 +495,28 @@ class CascadeClassifier:
             ptr, on_dev = _ptr(fr), 0
         n, H, W = (int(v) for v in fr.shape[:3])
         return self._detect_frames(L, ptr, n, H, W, on_dev, roi_w, scaleFactor, minNeighbors, cap)
+
+    def detect_frame_list(self, ptrs, H: int, W: int, roi_w: int = 300, scaleFactor=1.1, minNeighbors=5,
+                          cap: int = 256):
+        """find_objects on raw BGR frames already in device memory at separate addresses (e.g. the ROI frames
+        of many streams left in an engine's ring or input slots): `ptrs` = their device addresses, each
+        frame [H, W, 3].  The resize reads them in place (fm_haar_detect_frame_list); rects in ROI
+        coordinates.  The frames must be complete on the device (the caller synchronises its streams)."""
+        L = load()
+        n = len(ptrs)
+        arr = (C.c_void_p * n)(*[int(p) for p in ptrs])
+        rh = C.c_int32()
+        while True:
+            rects = np.zeros((n, cap, 4), np.int32)
+            counts = np.zeros(n, np.int32)
+            rc = L.fm_haar_detect_frame_list(self._h, C.cast(arr, C.c_void_p), n, int(H), int(W), int(roi_w),
+                                             float(scaleFactor), int(minNeighbors), _ptr(rects), cap, _ptr(counts),
+                                             C.byref(rh))
+            if rc != FM_OK:
+                raise FMError(rc, f"fm_haar_detect_frame_list: {L.fm_haar_last_error(self._h).decode()}")
+            if counts.max(initial=0) <= cap:
+                return [rects[i, :counts[i]].copy() for i in range(n)]
+            cap = int(counts.max())
 
     def _detect_frames(self, L, ptr, n, H, W, on_dev, roi_w, scaleFactor, minNeighbors, cap):
         rh = C.c_int32()

@@ -523,7 +523,10 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
         if (__ballot(ch) == 0) break;
     }
     FM_STAMP(6);
-    for (int i = base; i < base + nr; i++) {  // fold into roots (par[] is flat now)
+    // fold into roots (par[] is flat now); this row's roots (raster-first runs of their components)
+    // kept in a bit mask, so the ordinal and node loops below visit the roots only and re-read nothing
+    uint64_t rmask = 0;
+    for (int i = base; i < base + nr; i++) {
         const int rt = (par[i]);
         if (rt != i) {
             if (rf[i] & 1) {
@@ -533,13 +536,14 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
             } else if (rf[i] & 2) {
                 atomicOr(&amin[rt], 1);
             }
+        } else {
+            rmask |= 1ull << (i - base);
         }
     }
     lds_fence();
     FM_STAMP(7);
     // ordinals of the roots in raster order
-    int myr = 0;
-    for (int i = base; i < base + nr; i++) myr += ((par[i]) == i);
+    const int myr = __popcll(rmask);
     const int rin = wave_incl_sum(myr);
     const int nroots = lane_at(rin, 63);
     const int nb = take_nodes(a, f, nroots, ln);
@@ -550,18 +554,17 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
     }
     {
         int kk = rin - myr;
-        for (int i = base; i < base + nr; i++)
-            if ((par[i]) == i) ord[i] = (uint16_t)kk++;
+        for (uint64_t q = rmask; q; q &= q - 1) ord[base + __builtin_ctzll(q)] = (uint16_t)kk++;
     }
     lds_fence();
     if (FM_OOB(a, (long long)nb + nroots <= (long long)a.nnodes, 3)) return TCCL_NODES;
     NodeRec* NR = a.nodes + nb;
-    for (int i = base; i < base + nr; i++) {
-        const int pi = (par[i]);
-        if (pi != i) continue;
+    int kr = rin - myr;  // ordinal of the row's next root
+    for (uint64_t q = rmask; q; q &= q - 1, kr++) {
+        const int i = base + __builtin_ctzll(q);
         const int fg = rf[i] & 1;
         NodeRec nrec;
-        nrec.parent = nb + ord[i];
+        nrec.parent = nb + kr;
         nrec.key = 0;
         nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
         if (fg) {
@@ -578,7 +581,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
         } else {
             nrec.flags = amin[i] ? 2u : 0u;
         }
-        NR[ord[i]] = nrec;
+        NR[kr] = nrec;
     }
     const uint64_t mask_c = (2ull << ln) - 1;
     const uint64_t s0 = lane_at64(starts, 0), s63 = lane_at64(starts, 63);

@@ -434,6 +434,8 @@ struct fm_haar {
     size_t cap_live = 0;
     int2* d_taps = nullptr;
     uint8_t *d_raw = nullptr, *d_roi = nullptr;  // fm_haar_detect_frames: source frames, ROI frames
+    const uint8_t** d_fptr = nullptr;             // fm_haar_detect_frame_list: the frames' device addresses
+    size_t cap_fptr = 0;
     int32_t *d_axo = nullptr, *d_axc = nullptr, *d_ayo = nullptr, *d_ayc = nullptr;
     float *d_axw = nullptr, *d_ayw = nullptr;
     int area_key[4] = {0, 0, 0, 0};  // (W, H, w, h) the area tables are for
@@ -618,7 +620,7 @@ void fm_haar_destroy(fm_haar* h) {
     if (!h) return;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_blob, (void*)h->d_src, (void*)h->d_gray, (void*)h->d_rimg, (void*)h->d_S,
-                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw, (void*)h->d_live, (void*)h->d_nlive,
+                    (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw, (void*)h->d_fptr, (void*)h->d_live, (void*)h->d_nlive,
                     (void*)h->d_roi, (void*)h->d_axo, (void*)h->d_axc, (void*)h->d_ayo, (void*)h->d_ayc,
                     (void*)h->d_axw, (void*)h->d_ayw})
         if (p) (void)hipFree(p);
@@ -900,11 +902,15 @@ int fm_haar_candidates(const fm_haar* h, int32_t* rects, int cap) {
 
 double fm_haar_last_ms(const fm_haar* h) { return h ? h->last_ms : 0.; }
 
-int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W, int on_device, int roi_w,
-                          double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
-                          int* roi_h_out) {
+}  // extern "C"
+
+// find_objects' resize + detect over n frames: consecutive [n][H][W][3] frames at `frames` (host memory,
+// or device memory when on_device), or -- list != nullptr -- the n device frames at list[i]
+static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* const* list, int n, int H, int W,
+                              int on_device, int roi_w, double scale_factor, int min_neighbors, int32_t* rects,
+                              int cap, int32_t* counts, int* roi_h_out) {
     if (!h || !h->d_blob) return FM_EINVAL;
-    if (!frames || n < 1 || H < 1 || W < 1 || roi_w < 1)
+    if ((!frames && !list) || n < 1 || H < 1 || W < 1 || roi_w < 1)
         return hfail(h, FM_EINVAL, "bad arguments (n >= 1, frame and ROI sizes >= 1)");
     const int rw = roi_w, rh = (int)(H * ((double)roi_w / (double)W));  // imutils.resize(raw, width=roi_w)
     if (roi_h_out) *roi_h_out = rh;
@@ -917,7 +923,24 @@ int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W
     const size_t fb = (size_t)H * W * 3;
     const uint8_t* src = frames;
     int rc;
-    if (!on_device) {
+    // a frame list: the resize reads each frame where it lies (k_resize_area_nt's address table) when
+    // it can; otherwise the frames are gathered on the detector's stream first
+    const uint8_t* const* dlist = nullptr;
+    if (list) {
+        if ((rc = grow(h, &h->d_fptr, h->cap_fptr, (size_t)n))) return rc;
+        HH(h, hipMemcpyAsync(h->d_fptr, list, (size_t)n * sizeof(const uint8_t*), hipMemcpyHostToDevice, h->stream));
+        dlist = h->d_fptr;
+    }
+    auto gather = [&]() -> int {
+        int r = grow(h, &h->d_raw, h->cap_raw, n * fb);
+        if (r) return r;
+        for (int i = 0; i < n; i++)
+            HH(h, hipMemcpyAsync(h->d_raw + (size_t)i * fb, list[i], fb, hipMemcpyDeviceToDevice, h->stream));
+        src = h->d_raw;
+        dlist = nullptr;
+        return FM_OK;
+    };
+    if (!list && !on_device) {
         if ((rc = grow(h, &h->d_raw, h->cap_raw, n * fb))) return rc;
         HH(h, hipMemcpyAsync(h->d_raw, frames, n * fb, hipMemcpyHostToDevice, h->stream));
         src = h->d_raw;
@@ -927,6 +950,7 @@ int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W
         if ((rc = grow(h, &h->d_roi, h->cap_roi, (size_t)n * rh * rw * 3))) return rc;
         const int isx = (int)std::lrint(sx), isy = (int)std::lrint(sy);
         if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16) {
+            if (dlist && (rc = gather())) return rc;
             HH(h, fm::launch_resize_area_fast(h->stream, src, h->d_roi, n, H, W, rh, rw, isx, isy));
         } else {
             if (h->area_key[0] != W || h->area_key[1] != H || h->area_key[2] != rw || h->area_key[3] != rh) {
@@ -953,12 +977,36 @@ int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W
                 h->area_key[2] = rw;
                 h->area_key[3] = rh;
             }
+            const bool direct = dlist && ((h->ax.max_taps + 1) & ~1) <= 32 && fb < (1u << 31);
+            if (dlist && !direct && (rc = gather())) return rc;
             HH(h, fm::launch_resize_area(h->stream, src, h->d_roi, n, H, W, rh, rw, h->d_axo, h->d_axc, h->d_axw,
-                                         h->ax.max_taps, h->d_ayo, h->d_ayc, h->d_ayw, h->ay.max_taps));
+                                         h->ax.max_taps, h->d_ayo, h->d_ayc, h->d_ayw, h->ay.max_taps, dlist));
         }
         roi = h->d_roi;
+    } else if (dlist && (rc = gather())) {
+        return rc;
+    } else if (list) {
+        roi = src;
     }
     return fm_haar_detect(h, roi, n, rh, rw, 3, 1, scale_factor, min_neighbors, 0, 0, 0, 0, rects, cap, counts);
+}
+
+extern "C" {
+int fm_haar_detect_frames(fm_haar* h, const uint8_t* frames, int n, int H, int W, int on_device, int roi_w,
+                          double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
+                          int* roi_h_out) {
+    return detect_frames_impl(h, frames, nullptr, n, H, W, on_device, roi_w, scale_factor, min_neighbors, rects, cap,
+                              counts, roi_h_out);
+}
+
+int fm_haar_detect_frame_list(fm_haar* h, const uint8_t* const* frames, int n, int H, int W, int roi_w,
+                              double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
+                              int* roi_h_out) {
+    if (!frames) return h ? hfail(h, FM_EINVAL, "null frame list") : FM_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (!frames[i]) return hfail(h, FM_EINVAL, "frame %d: null address", i);
+    return detect_frames_impl(h, nullptr, frames, n, H, W, 1, roi_w, scale_factor, min_neighbors, rects, cap, counts,
+                              roi_h_out);
 }
 
 }  // extern "C"

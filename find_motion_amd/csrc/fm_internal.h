@@ -158,7 +158,7 @@ bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A);
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
                               int h, int w, const int32_t* xofs, const int32_t* xcnt, const float* xwt,
                               int xtaps, const int32_t* yofs, const int32_t* ycnt, const float* ywt,
-                              int ytaps);
+                              int ytaps, const uint8_t* const* srcs = nullptr);
 hipError_t launch_resize_area_fast(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
                                    int h, int w, int sx, int sy);
 hipError_t launch_pixel(hipStream_t st, const PixelArgs& a);

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restri
                                                          const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
                                                          int xtaps, const int32_t* __restrict__ yofs,
                                                          const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
-                                                         int ytaps) {
+                                                         int ytaps, const uint8_t* const* __restrict__ srcs) {
     constexpr int NB = 3 * NT;          // tap bytes of one row
     constexpr int NA = (NB + 3) / 4;    // aligned dwords holding them
     constexpr int ND = NA + 1;          // dwords loaded (a 0..3-byte misalignment)
@@ -188,7 +188,9 @@ __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restri
     const uint32_t rowb = 3u * (uint32_t)W;
     const uint32_t fbytes = rowb * (uint32_t)H;
     const uint32_t lim = (fbytes + 3u) & ~3u;  // every dword holding a frame byte is in range
-    const uint8_t* F = src + (size_t)blockIdx.y * fbytes;
+    // frame blockIdx.y: consecutive frames from src, or one address per frame (srcs: find_objects' ROI
+    // frames, read where the engine left them)
+    const uint8_t* F = srcs ? srcs[blockIdx.y] : src + (size_t)blockIdx.y * fbytes;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)F, 0, (int)lim, 0x00020000);
     const int nx = xcnt[dx];
     float wx[NT];
@@ -279,7 +281,8 @@ __global__ __launch_bounds__(256) void k_resize_area_fast(const uint8_t* __restr
 
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W, int h, int w,
                               const int32_t* xofs, const int32_t* xcnt, const float* xwt, int xtaps,
-                              const int32_t* yofs, const int32_t* ycnt, const float* ywt, int ytaps) {
+                              const int32_t* yofs, const int32_t* ycnt, const float* ywt, int ytaps,
+                              const uint8_t* const* srcs) {
     const int nt = (xtaps + 1) & ~1;
     if (nt <= 32 && (size_t)3 * W * H < (1u << 31)) {
         const dim3 g((h * w + RN_T - 1) / RN_T, F);
@@ -287,7 +290,7 @@ hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, 
 #define RN_CASE(N)                                                                                                      \
     case N:                                                                                                            \
         hipLaunchKernelGGL(k_resize_area_nt<N>, g, dim3(RN_T), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs, \
-                           ycnt, ywt, ytaps);                                                                          \
+                           ycnt, ywt, ytaps, srcs);                                                                    \
         break;
             RN_CASE(2) RN_CASE(4) RN_CASE(6) RN_CASE(8) RN_CASE(10) RN_CASE(12) RN_CASE(14) RN_CASE(16)
             RN_CASE(18) RN_CASE(20) RN_CASE(22) RN_CASE(24) RN_CASE(26) RN_CASE(28) RN_CASE(30) RN_CASE(32)
@@ -295,6 +298,7 @@ hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, 
         }
         return hipGetLastError();
     }
+    if (srcs) return hipErrorInvalidValue;  // per-frame addresses: the register kernel only (callers gather)
     dim3 grid(h, F);
     const int rowb = 3 * W;
     if (rowb % 16 == 0 && ((uintptr_t)src & 15) == 0 && rowb <= RS_MAXROW && w * 3 <= RS_T * RS_EPT &&

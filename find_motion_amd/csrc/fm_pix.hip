@@ -289,6 +289,21 @@ __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) 
     typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
     d = *(const __attribute__((address_space(1))) u3a*)(base + off);
 }
+// FM_PIX_BUFLD: the quad loads as buffer loads through a per-frame descriptor built from wave-uniform
+// values (frame base and size in SGPRs): the lane's 32-bit offset is the whole per-lane address, so the
+// 64-bit add per load (v_lshl_add_u64) is gone
+#ifndef FM_PIX_BUFLD
+#define FM_PIX_BUFLD 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* p, uint32_t bytes) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ void load12b(u32x3_t& d, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    d = __builtin_bit_cast(u32x3_t, __builtin_amdgcn_raw_buffer_load_b96(r, (int)off, 0, 0));
+}
 __device__ __forceinline__ gbytes_t frame_base(const uint8_t* p) {
 #if FM_PIX_SADDR
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
@@ -750,6 +765,7 @@ struct PW {
     }
     static constexpr int NP = np_max();            // pairs a wave's chain reads
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
+    static constexpr int dyn_bytes = bytes - 256 * 8;  // the blur x alpha table is static LDS
 };
 template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
     uint32_t v = 0;
@@ -792,12 +808,16 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
                                          __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
         });
         if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
-        const uint32_t blur = acc >> 16;
+        // the blur byte (byte 2: acc < 2^24) times 8, the table's byte offset, in ONE instruction: the
+        // compiler's v_bfe_u32 + v_lshl_add_u32 pair becomes a shift with an SDWA byte select
+        uint32_t boff;
+        asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(boff) : "v"(acc));
         const double b = bg[j];
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
         const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
         tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
-        const double bl = atab[blur];
+        const double bl = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(atab) + boff);
         double nb = bg_fma(b, beta, bl);
         if (TAIL) {
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
@@ -932,6 +952,7 @@ struct P5G {
     static constexpr int HROW = TS;                      // u16 per H row
     static constexpr int HBUF = (GH + HR) * HROW;        // + the pad row (pair) idle tap jobs store to
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
+    static constexpr int dyn_bytes = bytes - 256 * 8;  // the blur x alpha table is static LDS
 };
 static_assert(P5G<8>::GSLOW >= 0 && 4 * (P5G<8>::GFAST + P5G<8>::GSLOW) >= P5G<8>::GSLOTS, "gray slots");
 static_assert(!P5G<8>::HFAST || (P5G<8>::HSLOW >= 0 && 4 * (P5G<8>::HFAST + P5G<8>::HSLOW) >= P5G<8>::HSLOTS), "tap slots");
@@ -954,7 +975,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
-    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);
+    // blur x alpha (f64) as STATIC LDS at address 0: its byte offsets are then plain addresses (the
+    // dynamic array's base is a link-time symbol the compiler adds to every index)
+    __shared__ double atab_s[256];
+    double* atab = atab_s;
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1079,10 +1103,16 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        const gbytes_t src = frame_base(a.src + f * fbytes);
+        if constexpr (FM_PIX_BUFLD != 0) {
+            const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
-        for (int i = 0; i < G::GJ; i++) {
-            load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
+            for (int i = 0; i < G::GJ; i++) load12b(rw.v[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
+        } else {
+            const gbytes_t src = frame_base(a.src + f * fbytes);
+#pragma unroll
+            for (int i = 0; i < G::GJ; i++) {
+                load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
+            }
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
@@ -1266,7 +1296,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
     uint32_t* Hs = reinterpret_cast<uint32_t*>(smem + 2 * G::GBUF * 4);          // [2][HBUF]
-    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 4);
+    __shared__ double atab_s[256];  // static LDS at address 0 (see k_pix5)
+    double* atab = atab_s;
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1356,9 +1387,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        const gbytes_t src = frame_base(a.src + f * fbytes);
+        if constexpr (FM_PIX_BUFLD != 0) {
+            const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
-        for (int i = 0; i < G::GJ; i++) load12(rw[i], src, goff[i]);
+            for (int i = 0; i < G::GJ; i++) load12b(rw[i], rs, goff[i]);
+        } else {
+            const gbytes_t src = frame_base(a.src + f * fbytes);
+#pragma unroll
+            for (int i = 0; i < G::GJ; i++) load12(rw[i], src, goff[i]);
+        }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
@@ -1486,7 +1523,7 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
         const dim3 bgrid(a.ntx * nby, a.S);
 #define FM_P5_LAUNCH(NWB)                                                                                          \
     do {                                                                                                           \
-        const size_t lds = px::p5_lds_bytes<NWB>();                                                                \
+        const size_t lds = px::P5G<NWB>::dyn_bytes;                                                                \
         if (keep && tail) hipLaunchKernelGGL((px::k_pix5<NWB, true, true>), bgrid, dim3(64 * NWB), lds, st, a);    \
         else if (keep) hipLaunchKernelGGL((px::k_pix5<NWB, true, false>), bgrid, dim3(64 * NWB), lds, st, a);      \
         else if (tail) hipLaunchKernelGGL((px::k_pix5<NWB, false, true>), bgrid, dim3(64 * NWB), lds, st, a);      \
@@ -1513,17 +1550,17 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
         using G = px::PW<21, NWB>;                                                                                    \
         static_assert(G::bytes <= 160 * 1024, "k_pixw LDS");                                                          \
         if (keep && tail) {                                                                                           \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, true>), GRID, dim3(64 * NWB), G::bytes, st, a);             \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, true>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);             \
         } else if (keep) {                                                                                            \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, false>), GRID, dim3(64 * NWB), G::bytes, st, a);            \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, false>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);            \
         } else if (tail) {                                                                                            \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, true>), GRID, dim3(64 * NWB), G::bytes, st, a);            \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, true>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);            \
         } else {                                                                                                      \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, false>), GRID, dim3(64 * NWB), G::bytes, st, a);           \
+            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, false>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);           \
         }                                                                                                             \
     } while (0)
         if (FM_PIXW_TALL && a.nty >= 4 && a.ntiles * a.S >= 2048) {

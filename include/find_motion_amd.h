@@ -232,6 +232,14 @@ int fm_haar_detect(fm_haar* det, const uint8_t* images, int n, int H, int W, int
 int fm_haar_detect_frames(fm_haar* det, const uint8_t* frames, int n, int H, int W, int on_device, int roi_w,
                           double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
                           int* roi_h_out);
+/* fm_haar_detect_frames over n frames already in device memory at n separate
+ * addresses (frames[i]: [H][W][3] BGR; the frame list find_objects collects
+ * over many streams and batches, fm.py:703-731): the INTER_AREA resize reads
+ * each frame where it lies (no gather copy) whenever the tap table has at most
+ * 32 taps, and gathers the frames on the detector's stream otherwise. */
+int fm_haar_detect_frame_list(fm_haar* det, const uint8_t* const* frames, int n, int H, int W, int roi_w,
+                              double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
+                              int* roi_h_out);
 /* The ungrouped candidates of image 0 of the last fm_haar_detect (parity
  * tests); returns their number. */
 int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);

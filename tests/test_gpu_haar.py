@@ -96,6 +96,34 @@ def test_detect_frames_resizes_on_device(W, H):
     det.close()
 
 
+@pytest.mark.parametrize("W,H,roi_w", [(640, 360, 300),    # 6-tap INTER_AREA: read in place
+                                        (1920, 1080, 300),  # 8 taps (find_objects on 1080p)
+                                        (600, 338, 300),    # exact 2x: gathered, resizeAreaFast
+                                        (300, 169, 300),    # identity: gathered
+                                        (3840, 1280, 90)])  # 44 taps: gathered, the LDS-staged resize
+def test_detect_frame_list_reads_frames_in_place(W, H, roi_w):
+    """fm_haar_detect_frame_list: ROI frames at separate device addresses (out of order, in one big
+    buffer with gaps, as find_objects collects them over streams and batches) give the detections of
+    the contiguous call and of the restatement, on every resize path."""
+    import torch
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    raws = np.stack([_raw_frame(s, W, H) for s in range(4)])
+    det = CascadeClassifier(cs)
+    ring = torch.zeros((9, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    slots = [7, 2, 5, 0]  # frame i lives in ring slot slots[i]
+    for i, k in enumerate(slots):
+        ring[k].copy_(torch.from_numpy(raws[i]))
+    torch.cuda.synchronize()
+    got = det.detect_frame_list([ring[k].data_ptr() for k in slots], H, W, roi_w, 1.1, 3)
+    cont = det.detect_frames(raws, roi_w, 1.1, 3)
+    for i in range(len(raws)):
+        roi = oracle.resize_area_bgr(raws[i], roi_w) if W != roi_w else raws[i]
+        ref = haar.detect_multiscale(cs, roi, 1.1, 3)
+        assert [tuple(r) for r in got[i].tolist()] == ref, i
+        assert [tuple(r) for r in cont[i].tolist()] == ref, i
+    det.close()
+
+
 def test_detect_frames_device_input():
     # frames already resident in HBM (on_device = 1: no H2D copy) give the host path's and the
     # restatement's detections
