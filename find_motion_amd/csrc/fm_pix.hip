@@ -289,11 +289,26 @@ __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) 
     typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
     d = *(const __attribute__((address_space(1))) u3a*)(base + off);
 }
-// FM_PIX_BUFLD: the quad loads as buffer loads through a per-frame descriptor built from wave-uniform
-// values (frame base and size in SGPRs): the lane's 32-bit offset is the whole per-lane address, so the
-// 64-bit add per load (v_lshl_add_u64) is gone
-#ifndef FM_PIX_BUFLD
-#define FM_PIX_BUFLD 1
+// FM_P5_BUFLD / FM_PW_BUFLD: the quad loads of k_pix5 / k_pixw as buffer loads through a per-frame
+// descriptor built from wave-uniform values (frame base and size in SGPRs): the lane's 32-bit offset is
+// the whole per-lane address, so the 64-bit add per load (v_lshl_add_u64) is gone.
+// FM_P5_SDWA / FM_PW_SDWA: the blur x alpha table as static LDS at address 0, its byte offset from the
+// accumulator by ONE SDWA shift (byte 2 of acc times 8) instead of v_bfe_u32 + v_lshl_add_u32 (the
+// dynamic LDS array's base is a link-time symbol the compiler adds to every index).
+// Measured (round 4, 3 alternating rounds of the driver's command and 2 of config 5): both on in
+// k_pix5 cost 3.4 % (396.0 vs 410.1 k frames/s, pixel launches 612-653 vs 556-629 us); both on in
+// k_pixw gain 1.9 % (80.9 vs 79.5 k frames/s, 3.07-3.12 vs 3.16-3.17 ms per launch).
+#ifndef FM_P5_BUFLD
+#define FM_P5_BUFLD 0
+#endif
+#ifndef FM_P5_SDWA
+#define FM_P5_SDWA 0
+#endif
+#ifndef FM_PW_BUFLD
+#define FM_PW_BUFLD 1
+#endif
+#ifndef FM_PW_SDWA
+#define FM_PW_SDWA 1
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* p, uint32_t bytes) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
@@ -765,7 +780,7 @@ struct PW {
     }
     static constexpr int NP = np_max();            // pairs a wave's chain reads
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
-    static constexpr int dyn_bytes = bytes - 256 * 8;  // the blur x alpha table is static LDS
+    static constexpr int dyn_bytes = bytes - (FM_PW_SDWA ? 256 * 8 : 0);  // (FM_PW_SDWA: the table is static LDS)
 };
 template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
     uint32_t v = 0;
@@ -785,7 +800,7 @@ template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of o
 // side the row parity needs, so no pair is rebuilt with v_alignbit
 // wv: the wave within its workgroup (H rows, image rows); wb: its 8-row slice of the 64-row contour
 // tile (flag rows: FLAG_T* from slice 0, FLAG_B* from slice 7) -- the same as wv for a 64-row workgroup
-template <int KC, bool KEEP, bool TAIL>
+template <int KC, bool KEEP, bool TAIL, bool SDWA>
 __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
                                              int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
                                              uint32_t& flags, int wb) {
@@ -808,16 +823,20 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
                                          __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
         });
         if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
-        // the blur byte (byte 2: acc < 2^24) times 8, the table's byte offset, in ONE instruction: the
-        // compiler's v_bfe_u32 + v_lshl_add_u32 pair becomes a shift with an SDWA byte select
-        uint32_t boff;
-        asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-            : "=v"(boff) : "v"(acc));
+        // SDWA: the blur byte (byte 2: acc < 2^24) times 8, the table's byte offset, in ONE instruction
+        // (the table must then be static LDS at address 0); else the blur value indexes the table
+        uint32_t boff = 0, blur = 0;
+        if constexpr (SDWA)
+            asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+                : "=v"(boff) : "v"(acc));
+        else
+            blur = acc >> 16;
         const double b = bg[j];
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
         const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
         tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
-        const double bl = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(atab) + boff);
+        const double bl = SDWA ? *reinterpret_cast<const double*>(reinterpret_cast<const char*>(atab) + boff)
+                               : atab[blur];
         double nb = bg_fma(b, beta, bl);
         if (TAIL) {
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
@@ -952,7 +971,7 @@ struct P5G {
     static constexpr int HROW = TS;                      // u16 per H row
     static constexpr int HBUF = (GH + HR) * HROW;        // + the pad row (pair) idle tap jobs store to
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
-    static constexpr int dyn_bytes = bytes - 256 * 8;  // the blur x alpha table is static LDS
+    static constexpr int dyn_bytes = bytes - (FM_P5_SDWA ? 256 * 8 : 0);  // (FM_P5_SDWA: the table is static LDS)
 };
 static_assert(P5G<8>::GSLOW >= 0 && 4 * (P5G<8>::GFAST + P5G<8>::GSLOW) >= P5G<8>::GSLOTS, "gray slots");
 static_assert(!P5G<8>::HFAST || (P5G<8>::HSLOW >= 0 && 4 * (P5G<8>::HFAST + P5G<8>::HSLOW) >= P5G<8>::HSLOTS), "tap slots");
@@ -975,10 +994,13 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
-    // blur x alpha (f64) as STATIC LDS at address 0: its byte offsets are then plain addresses (the
-    // dynamic array's base is a link-time symbol the compiler adds to every index)
-    __shared__ double atab_s[256];
-    double* atab = atab_s;
+    double* atab;  // blur x alpha (f64): static LDS at address 0 with FM_P5_SDWA, else behind H
+    if constexpr (FM_P5_SDWA != 0) {
+        __shared__ double atab_s[256];
+        atab = atab_s;
+    } else {
+        atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);
+    }
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1103,7 +1125,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        if constexpr (FM_PIX_BUFLD != 0) {
+        if constexpr (FM_P5_BUFLD != 0) {
             const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
             for (int i = 0; i < G::GJ; i++) load12b(rw.v[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
@@ -1217,9 +1239,9 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
                 const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hb);
                 const int wbf = NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb0 + wv);
                 if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
+                    chain_rows_w<KC, KEEP, false, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
                 else
-                    chain_rows_w<KC, KEEP, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
+                    chain_rows_w<KC, KEEP, true, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
             } else if (!TAIL || var == 0) {
                 chain_rows<KC, false, false, KEEP, false, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
                                                                          colbits, fl);
@@ -1296,8 +1318,13 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
     uint32_t* Hs = reinterpret_cast<uint32_t*>(smem + 2 * G::GBUF * 4);          // [2][HBUF]
-    __shared__ double atab_s[256];  // static LDS at address 0 (see k_pix5)
-    double* atab = atab_s;
+    double* atab;  // blur x alpha (f64): static LDS at address 0 with FM_PW_SDWA, else behind H
+    if constexpr (FM_PW_SDWA != 0) {
+        __shared__ double atab_s[256];
+        atab = atab_s;
+    } else {
+        atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 4);
+    }
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1387,7 +1414,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        if constexpr (FM_PIX_BUFLD != 0) {
+        if constexpr (FM_PW_BUFLD != 0) {
             const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
             for (int i = 0; i < G::GJ; i++) load12b(rw[i], rs, goff[i]);
@@ -1464,10 +1491,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
         const uint32_t* Hb = Hs + b * G::HBUF;
         if (!TAIL || var == 0)
-            chain_rows_w<KC, KEEP, false>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
+            chain_rows_w<KC, KEEP, false, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
                                           NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
         else
-            chain_rows_w<KC, KEEP, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
+            chain_rows_w<KC, KEEP, true, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
                                          NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
         if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         gray_stage(gray + b * G::GBUF);

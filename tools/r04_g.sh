@@ -19,6 +19,12 @@ for round in 1 2 3; do
   done
 done
 for round in 1 2; do
+  for B in 256 384 512; do
+    FM_HIP_LIB=$PWD/abvar/v2/libfm_hip.so timeout -k 10 200 python bench.py --steps 20 --warmup 5 --batch $B --ring $B $J > gpurun_out/ab_${TAG}_b${B}_$round.log 2>&1 || { tail -20 gpurun_out/ab_${TAG}_b${B}_$round.log; exit 1; }
+    v gpurun_out/ab_${TAG}_b${B}_$round.log "F v2 batch $B r$round"
+  done
+done
+for round in 1 2; do
   for var in v0 v2; do
     FM_HIP_LIB=$PWD/abvar/$var/libfm_hip.so timeout -k 10 200 python bench.py $C5 $J > gpurun_out/ab_${TAG}_c5_${var}_$round.log 2>&1 || { tail -20 gpurun_out/ab_${TAG}_c5_${var}_$round.log; exit 1; }
     v gpurun_out/ab_${TAG}_c5_${var}_$round.log "C5 $var r$round"
