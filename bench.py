@@ -536,9 +536,9 @@ def main() -> None:
         from find_motion_amd import videoio
         from find_motion_amd.feeder import BatchFeeder
 
-        # batches of Th frames per stream, 3 in flight + 2 being filled / consumed: at most ~3.2 GB
-        # page-locked (1080p: 128 frames x 1 stream, 16 x 8 streams)
-        Th = max(1, min(T, (128 * 1920 * 1080) // (S * H * W)))
+        # batches of Th frames per stream, 3 in flight + 2 being filled / consumed: ~1 GB page-locked
+        # (1080p: 32 frames x 1 stream, 4 x 8 streams; each copy is still ~200 MB, PCIe-bound as at 128)
+        Th = max(1, min(T, (32 * 1920 * 1080) // (S * H * W)))
         depth_hf = min(3, eng.max_inflight)
         n_hf = max(8 * Th, 512 // S)
         caps = [videoio.ArrayCapture([host[t % P, s] for t in range(n_hf)]) for s in range(S)]

@@ -136,6 +136,8 @@ struct fm_ctx {
     std::string err;
     uint64_t* d_ts = nullptr;     // FM_TS: contour-pass phase stamps (profiling)
     uint64_t* d_pts = nullptr;    // FM_PTS=<file>: k_pix workgroup stamps of the last launch (profiling)
+    int pts_ring = 1;             // FM_PTS_RING=<n>: stamps of the last n launches, oldest first (profiling)
+    long long pts_launches = 0;
     int32_t* h_err = nullptr;     // mapped: FM_OOB violation bits (checked build), 0 otherwise
     int32_t* dh_err = nullptr;
     std::vector<double> ts_sum;   // summed phase deltas (cycles)
@@ -632,9 +634,11 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     if (const char* e = dev_env("FM_DEBUG_SKIP")) c->dbg_skip = std::atoi(e);
     c->serial = dev_env("FM_SERIAL") != nullptr;
     if (dev_env("FM_PTS") && c->use_pix) {
-        // [S][ntiles][4] workgroup stamps, then [S][ntiles][8 waves][4] k_pix5 phase cycles
-        if ((rc = dalloc(cp, &c->d_pts, (size_t)S * c->ntiles * 36))) return rc;
-        HIP_TRY(cp, hipMemset(c->d_pts, 0, (size_t)S * c->ntiles * 36 * sizeof(uint64_t)));
+        // per launch: [S][ntiles][4] workgroup stamps, then [S][ntiles][8 waves][4] k_pix5 phase cycles
+        if (const char* e = dev_env("FM_PTS_RING")) c->pts_ring = std::max(1, std::min(256, std::atoi(e)));
+        const size_t n = (size_t)S * c->ntiles * 36 * c->pts_ring;
+        if ((rc = dalloc(cp, &c->d_pts, n))) return rc;
+        HIP_TRY(cp, hipMemset(c->d_pts, 0, n * sizeof(uint64_t)));
     }
     if (dev_env("FM_TS") && c->use_fused) {
         if ((rc = dalloc(cp, &c->d_ts, frames * c->ntiles * 16))) return rc;
@@ -651,12 +655,14 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 void fm_destroy(fm_ctx* c) {
     if (!c) return;
     if (c->d_pts) {  // profiling: per-workgroup (hw_id, xcc_id, realtime start/end, memtime start/end) of the last k_pix
-        const size_t n = (size_t)c->p.n_streams * c->ntiles * 36;
+        const size_t rec = (size_t)c->p.n_streams * c->ntiles * 36, n = rec * c->pts_ring;
         std::vector<uint64_t> v(n);
         if (hipDeviceSynchronize() == hipSuccess &&
             hipMemcpy(v.data(), c->d_pts, n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess) {
-            if (FILE* fh = std::fopen(dev_env("FM_PTS"), "wb")) {  // dev build only (d_pts)
-                std::fwrite(v.data(), sizeof(uint64_t), n, fh);
+            if (FILE* fh = std::fopen(dev_env("FM_PTS"), "wb")) {  // dev build only (d_pts); oldest launch first
+                const size_t r0 = (size_t)(c->pts_launches % c->pts_ring);
+                for (int k = 0; k < c->pts_ring; k++)
+                    std::fwrite(v.data() + ((r0 + k) % c->pts_ring) * rec, sizeof(uint64_t), rec, fh);
                 std::fclose(fh);
             }
         }
@@ -884,7 +890,7 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         fa.any_keep = std::any_of(c->has_keep.begin(), c->has_keep.end(), [](uint8_t k) { return k != 0; }) ? 1 : 0;
         fa.dbg_skip = c->dbg_skip;
         fa.dbg_ts = c->d_ts;
-        fa.dbg_pts = c->d_pts;
+        fa.dbg_pts = c->d_pts ? c->d_pts + (size_t)(c->pts_launches++ % c->pts_ring) * S * c->ntiles * 36 : nullptr;
         fa.dbg_err = c->dh_err;
         if (c->d_ts) HIP_TRY(c, hipMemsetAsync(c->d_ts, 0, F * c->ntiles * 16 * sizeof(uint64_t), ps));
         for (int i = 0; i < c->p.ksize; i++) fa.coef[i] = c->coef[i];

@@ -1211,7 +1211,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
 #define FM_P5_PRIO 0  // issue priority of the pixel waves against the contour pass's (fm_ccl.hip FM_*_PRIO)
 #endif
     if (FM_P5_PRIO) __builtin_amdgcn_s_setprio(FM_P5_PRIO);
-#ifdef FM_DEV_SWITCHES
+#ifndef FM_P5_PHASES
+#define FM_P5_PHASES 1  // dev build: FM_PTS also takes the per-wave phase cycles (0: workgroup stamps only)
+#endif
+#if defined(FM_DEV_SWITCHES) && FM_P5_PHASES
     // profiling (FM_PTS, dev build): per-wave cycles in the frame barrier, chain, taps, gray+stores+loads
     uint64_t* phw = a.dbg_pts ? a.dbg_pts + (size_t)a.S * a.ntiles * 4 + (((size_t)s * a.ntiles + ti) * NW + wv) * 4 : nullptr;
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, tA = __builtin_amdgcn_s_memtime(), tB;
@@ -1265,7 +1268,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
         // unconditional (see load): past the batch's last frame it re-reads that frame
         if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
     }
-#ifdef FM_DEV_SWITCHES
+#if defined(FM_DEV_SWITCHES) && FM_P5_PHASES
     P5_PH(ph3);
     if (phw && ln == 0) {
         phw[0] = ph0;
