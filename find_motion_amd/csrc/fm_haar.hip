@@ -47,6 +47,12 @@ constexpr int MAXSC = 64;  // scales per call (1.1^64 > 400: far beyond any fram
 
 struct Node { int left, right, feat; float thr; };
 struct Feat { int r[3][4]; float w[3]; int tilted; };
+// k_hdetect's stump record (FM_HAAR_REC): the feature's 12 rectangle corners as offsets from the
+// window's corner in the LDS integral patch (row stride pw_max, a per-cascade constant), weights,
+// threshold and the two leaf values; 80 B, read by 5 vector loads one stump ahead (vmcnt, not
+// lgkmcnt: the prefetch does not hold up the corner reads from LDS)
+struct alignas(16) StumpRec { int off[12]; float w[3]; float thr, leaf_lt, leaf_ge; int flags, pad; };
+constexpr int kRecTilted = 1, kRecThree = 2;
 
 struct Geo {  // per scale, copied to the device as kernel arguments
     int n;                    // scales
@@ -181,6 +187,8 @@ struct CascadeDev {
     const Node* nodes;
     const float* leaves;
     const Feat* feats;
+    const StumpRec* recs;      // stumps only: one record per stump (k_hdetect), else nullptr
+    int n_recs;
 };
 
 __device__ __forceinline__ int32_t rsum(const uint32_t* I, int st, int x, int y, const int* r, bool tilted) {
@@ -250,17 +258,24 @@ __device__ __forceinline__ int run_stages(const CascadeDev& c, const Win& w, int
         if (c.stumps && FM_HAAR_PF) {
             // the next stump's node and feature records are loaded while this one is evaluated (scalar
             // loads: every lane evaluates the same stump); leaves are summed in stump order as OpenCV does
+            // The two leaves of a stump are the same in every lane too: loaded by scalar loads with the
+            // records, then selected per lane (a per-lane leaf gather stalled every stump on an L2 round trip)
             Node n = c.nodes[t0];
             Feat fe = c.feats[__builtin_amdgcn_readfirstlane(n.feat)];
+            float lf = c.leaves[__builtin_amdgcn_readfirstlane(2 * t0 - n.left)];
+            float rt = c.leaves[__builtin_amdgcn_readfirstlane(2 * t0 - n.right)];
             for (int t = t0; t < t0 + nt; ++t) {
                 const int tn = t + 1 < t0 + nt ? t + 1 : t;
                 const Node nn = c.nodes[tn];
                 const Feat fn = c.feats[__builtin_amdgcn_readfirstlane(nn.feat)];
+                const float nlf = c.leaves[__builtin_amdgcn_readfirstlane(2 * tn - nn.left)];
+                const float nrt = c.leaves[__builtin_amdgcn_readfirstlane(2 * tn - nn.right)];
                 const float v = feature(fe, w);
-                const int idx = v < n.thr ? n.left : n.right;
-                sum += (double)c.leaves[2 * t - idx];
+                sum += (double)(v < n.thr ? lf : rt);
                 n = nn;
                 fe = fn;
+                lf = nlf;
+                rt = nrt;
             }
         } else if (c.stumps) {
             for (int t = t0; t < t0 + nt; ++t) {
@@ -279,6 +294,64 @@ __device__ __forceinline__ int run_stages(const CascadeDev& c, const Win& w, int
                 } while (idx > 0);
                 sum += (double)c.leaves[c.tree_leaf_ofs[t] - idx];
             }
+        }
+        if (sum < (double)c.stage_thr[si]) return si;
+    }
+    return -1;
+}
+
+#ifndef FM_HAAR_REC
+#define FM_HAAR_REC 1  // k_hdetect on stump records (StumpRec) when the cascade is all stumps
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+struct RecV { u32x4_t o0, o1, o2, wt, lf; };  // corners 0-3, 4-7, 8-11; w0 w1 w2 thr; leaf_lt leaf_ge flags pad
+
+__device__ __forceinline__ RecV load_rec(__amdgpu_buffer_rsrc_t rs, int t) {
+    // buffer loads (vector memory): past the last record they read zeros
+    const int b = t * (int)sizeof(StumpRec);
+    return RecV{__builtin_amdgcn_raw_buffer_load_b128(rs, 0, b, 0), __builtin_amdgcn_raw_buffer_load_b128(rs, 0, b + 16, 0),
+                __builtin_amdgcn_raw_buffer_load_b128(rs, 0, b + 32, 0), __builtin_amdgcn_raw_buffer_load_b128(rs, 0, b + 48, 0),
+                __builtin_amdgcn_raw_buffer_load_b128(rs, 0, b + 64, 0)};
+}
+
+__device__ __forceinline__ int32_t rsum4(const uint32_t* P, u32x4_t o) {
+    return (int32_t)(P[(int)o.x] - P[(int)o.y] - P[(int)o.z] + P[(int)o.w]);
+}
+
+// one stump on the window whose patch corners start at PS / PT: feature (as feature()) -> leaf value
+__device__ __forceinline__ float stump_rec(const RecV& R, const uint32_t* PS, const uint32_t* PT, float vnf) {
+    const int fl = __builtin_amdgcn_readfirstlane((int)R.lf.z);
+    const uint32_t* P = (fl & kRecTilted) ? PT : PS;
+    float v = __fmul_rn(__uint_as_float(R.wt.x), (float)rsum4(P, R.o0));
+    v = __fadd_rn(v, __fmul_rn(__uint_as_float(R.wt.y), (float)rsum4(P, R.o1)));
+    if (fl & kRecThree) v = __fadd_rn(v, __fmul_rn(__uint_as_float(R.wt.z), (float)rsum4(P, R.o2)));
+    v = __fmul_rn(v, vnf);
+    return v < __uint_as_float(R.wt.w) ? __uint_as_float(R.lf.x) : __uint_as_float(R.lf.y);
+}
+
+// run_stages on stump records: stages [s0, s1) of the window whose corner is PS / PT in the LDS patch.
+// Stumps are visited in cascade order, so the next one's record is loaded while this one is evaluated
+// (two records in flight, renamed by a 2-way unrolled loop); leaves are summed in stump order.
+__device__ __forceinline__ int run_stages_rec(const CascadeDev& c, const uint32_t* PS, const uint32_t* PT, float vnf,
+                                              int s0, int s1) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)c.recs, 0, c.n_recs * (int)sizeof(StumpRec),
+                                                                        0x00020000);
+    int t = __builtin_amdgcn_readfirstlane(c.stage_first[s0]);
+    RecV A = load_rec(rs, t);
+    for (int si = s0; si < s1; ++si) {
+        const int t1 = t + __builtin_amdgcn_readfirstlane(c.stage_ntrees[si]);
+        double sum = 0.;
+        for (; t + 1 < t1; t += 2) {
+            const RecV B = load_rec(rs, t + 1);
+            sum += (double)stump_rec(A, PS, PT, vnf);
+            A = load_rec(rs, t + 2);
+            sum += (double)stump_rec(B, PS, PT, vnf);
+        }
+        if (t < t1) {
+            const RecV B = load_rec(rs, t + 1);
+            sum += (double)stump_rec(A, PS, PT, vnf);
+            A = B;
+            ++t;
         }
         if (sum < (double)c.stage_thr[si]) return si;
     }
@@ -380,7 +453,9 @@ __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict_
             ok = area * (double)w.vnf < 1e-1;
         }
         if (ok) {
-            const int f = run_stages(c, w, 0, split);
+            const int f = (FM_HAAR_REC && c.recs) ? run_stages_rec(c, patch + w.y * pw_max + w.x,
+                                                                   w.T ? w.T + w.y * pw_max + w.x : nullptr, w.vnf, 0, split)
+                                                  : run_stages(c, w, 0, split);
             if (f >= 0) out = f == 0 ? 0 : -1;
             else if (split < c.n_stages) live = true;
             else out = 1;
@@ -409,7 +484,11 @@ __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict_
         v.T = w.T;
         v.vnf = s_vnf[t2];
         const long long wi2 = (long long)img * g.NW + g.woff[s] + (long long)gy2 * g.gw[s] + gx2;
-        res[wi2] = run_stages(c, v, split, c.n_stages) >= 0 ? -1 : 1;
+        const int f = (FM_HAAR_REC && c.recs) ? run_stages_rec(c, patch + v.y * pw_max + v.x,
+                                                               v.T ? v.T + v.y * pw_max + v.x : nullptr, v.vnf, split,
+                                                               c.n_stages)
+                                              : run_stages(c, v, split, c.n_stages);
+        res[wi2] = f >= 0 ? -1 : 1;
     }
 }
 
@@ -604,15 +683,52 @@ int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
     std::memcpy(&blob[off[5]], nodes.data(), sz[5]);
     std::memcpy(&blob[off[6]], d->leaves, sz[6]);
     std::memcpy(&blob[off[7]], feats.data(), sz[7]);
+    int stumps = 1;
+    for (int t = 0; t < d->n_trees; ++t) stumps &= d->tree_nodes[t] == 1;
+    // stump records for k_hdetect: corners as offsets in its LDS patch, whose row stride is
+    // (TW - 1) * 2 + win_w + 1 (the widest step, 2) for every launch of this cascade
+    const size_t rec_off = tot;
+    if (stumps) {
+        const int st = (TW - 1) * 2 + d->win_w + 1;
+        std::vector<StumpRec> recs(d->n_trees);
+        for (int t = 0; t < d->n_trees; ++t) {  // stump t = node t, leaves 2t - left, 2t - right
+            const Node& n = nodes[t];
+            const Feat& f = feats[n.feat];
+            StumpRec r{};
+            for (int j = 0; j < 3; ++j) {
+                const int x = f.r[j][0], y = f.r[j][1], w = f.r[j][2], hh = f.r[j][3];
+                int* o = r.off + 4 * j;
+                if (!f.tilted) {
+                    o[0] = y * st + x;
+                    o[1] = y * st + x + w;
+                    o[2] = (y + hh) * st + x;
+                    o[3] = (y + hh) * st + x + w;
+                } else {
+                    o[0] = y * st + x;
+                    o[1] = (y + hh) * st + x - hh;
+                    o[2] = (y + w) * st + x + w;
+                    o[3] = (y + w + hh) * st + x + w - hh;
+                }
+                r.w[j] = f.w[j];
+            }
+            r.thr = n.thr;
+            r.leaf_lt = d->leaves[2 * t - n.left];
+            r.leaf_ge = d->leaves[2 * t - n.right];
+            r.flags = (f.tilted ? kRecTilted : 0) | (f.w[2] != 0.f ? kRecThree : 0);
+            recs[t] = r;
+        }
+        blob.resize(tot + recs.size() * sizeof(StumpRec));
+        std::memcpy(&blob[tot], recs.data(), recs.size() * sizeof(StumpRec));
+        tot = blob.size();
+    }
     HH(h, hipMalloc(&h->d_blob, tot));
     HH(h, hipMemcpy(h->d_blob, blob.data(), tot, hipMemcpyHostToDevice));
     auto* b = (uint8_t*)h->d_blob;
-    int stumps = 1;
-    for (int t = 0; t < d->n_trees; ++t) stumps &= d->tree_nodes[t] == 1;
     h->cd = CascadeDev{d->win_w, d->win_h, d->n_stages, tilted, stumps,
                        (const int*)(b + off[0]), (const int*)(b + off[1]), (const float*)(b + off[2]),
                        (const int*)(b + off[3]), (const int*)(b + off[4]), (const Node*)(b + off[5]),
-                       (const float*)(b + off[6]), (const Feat*)(b + off[7])};
+                       (const float*)(b + off[6]), (const Feat*)(b + off[7]),
+                       stumps ? (const StumpRec*)(b + rec_off) : nullptr, stumps ? d->n_trees : 0};
     return FM_OK;
 }
 

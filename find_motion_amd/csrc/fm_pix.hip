@@ -986,11 +986,21 @@ struct P5Raw {
 // accumulateWeighted's scalar tail (h*w % 16 != 0), so some waves take the per-pixel test.  Fixed
 // per launch, so the common kernel has a single chain path: a per-wave 3-way branch inside the
 // frame loop made the background registers a phi and cost 8 v_mov_b64 per frame.
-template <int NWB, bool KEEP, bool TAIL>
-__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+// PAIR = 2: one 1,024-thread workgroup runs two neighbouring 64 x 64 tiles (waves 0-7 and 8-15, each half
+// with its own LDS) in step, sharing the frame barrier.  With two 8-wave workgroups per CU the older
+// one's waves win issue arbitration, it finishes first and the younger runs its last frames alone
+// at half occupancy (FM_PTS, round 4: 254 of 510 workgroups end ~120 us after the median); a shared
+// barrier keeps both tiles of a CU at the same frame.
+template <int NWB>
+constexpr int p5_half_bytes() { return (P5G<NWB>::dyn_bytes + 15) & ~15; }
+template <int NWB, bool KEEP, bool TAIL, int PAIR = 1>
+__global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
     using G = P5G<NWB>;
     static_assert(FM_P5_EVENP || NWB == 8, "bands need the even-pair chain (its flag rows follow wb)");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    static_assert(PAIR == 1 || (NWB == 8 && FM_P5_SDWA == 0), "tile pairs: 64-row tiles, the table in each half's LDS");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_all[];
+    const int half = PAIR > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (64 * NWB)) : 0;
+    uint8_t* smem = smem_all + half * p5_half_bytes<NWB>();
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
@@ -1001,12 +1011,17 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     } else {
         atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);
     }
-    const int tid = threadIdx.x, ln = tid & 63;
+    const int tid = PAIR > 1 ? (int)threadIdx.x % (64 * NWB) : (int)threadIdx.x, ln = tid & 63;  // (within the tile)
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
     int ti, tx, y0, wb0;  // contour tile, its column, the band's first row, its first 8-row slice of the tile
-    if constexpr (NWB == 8) {
+    if constexpr (PAIR > 1) {
+        ti = 2 * swizzle_tile(blockIdx.x, a.ntiles / 2) + half;
+        tx = ti % a.ntx;
+        y0 = (ti / a.ntx) * TS;
+        wb0 = 0;
+    } else if constexpr (NWB == 8) {
         ti = pix_tile(blockIdx.x, a);
         tx = ti % a.ntx;
         y0 = (ti / a.ntx) * TS;
@@ -1548,6 +1563,19 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
 #ifndef FM_P5_BANDS
 #define FM_P5_BANDS 0
 #endif
+#ifndef FM_P5_PAIR
+#define FM_P5_PAIR 0  // 64 x 64 tiles two per 1,024-thread workgroup when the tile count is even (k_pix5 PAIR)
+#endif
+        if (FM_P5_PAIR && a.ntiles % 2 == 0 && a.ntiles * a.S >= 128) {
+            const dim3 pgrid(a.ntiles / 2, a.S);
+            const size_t lds = 2 * px::p5_half_bytes<8>();
+            static_assert(2 * px::p5_half_bytes<8>() <= 64 * 1024, "tile pair LDS");
+            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 2>), pgrid, dim3(1024), lds, st, a);
+            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 2>), pgrid, dim3(1024), lds, st, a);
+            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 2>), pgrid, dim3(1024), lds, st, a);
+            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 2>), pgrid, dim3(1024), lds, st, a);
+            return hipGetLastError();
+        }
         const int nwb = !FM_P5_BANDS || a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
         const int nby = a.nty * (8 / nwb);  // bands covering every 64-row contour tile whole
         const dim3 bgrid(a.ntx * nby, a.S);
