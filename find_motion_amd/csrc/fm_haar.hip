@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -64,7 +65,8 @@ struct Geo {  // per scale, copied to the device as kernel arguments
     int woff[MAXSC];           // window offset within one image
     int xtab[MAXSC], ytab[MAXSC];  // offsets into the tap table
     int toff[MAXSC], tnx[MAXSC];   // k_hdetect: first window tile of each scale, tiles per tile row
-    int P, I, NW, NT;          // per image totals (NT: window tiles)
+    int roff[MAXSC];           // k_hwalk: first window row of each scale
+    int P, I, NW, NT, NR;      // per image totals (NT: window tiles, NR: window rows)
 };
 
 __device__ __forceinline__ int find_scale(const int* off, int n, int r) {
@@ -492,6 +494,31 @@ __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict_
     }
 }
 
+// detectMultiScale's row walk on the device: one thread per window row of one scale of one image walks
+// the row as OpenCV visits it (a window stage 0 rejects skips the next one: x += result == 0 ? 2 : 1)
+// and appends the accepted windows it reaches (their index in the image's window grid) to the image's
+// candidate list; the host sorts each list, which restores OpenCV's scale / row / column order.  Only
+// these lists cross PCIe (kCandCap per image; a longer list makes the host read the whole result grid).
+constexpr int kCandCap = 1024;
+__global__ __launch_bounds__(64) void k_hwalk(const int8_t* __restrict__ res, int* __restrict__ cnt,
+                                              int* __restrict__ cand, Geo g, int nimg) {
+    const long long i = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (i >= (long long)nimg * g.NR) return;
+    const int img = (int)(i / g.NR), r = (int)(i - (long long)img * g.NR);
+    const int s = find_scale(g.roff, g.n, r);
+    const int gy = r - g.roff[s], gw = g.gw[s];
+    const int base = g.woff[s] + gy * gw;
+    const int8_t* R = res + (size_t)img * g.NW + base;
+    for (int gx = 0; gx < gw;) {
+        const int8_t v = R[gx];
+        if (v > 0) {
+            const int k = atomicAdd(&cnt[img], 1);
+            if (k < kCandCap) cand[(size_t)img * kCandCap + k] = base + gx;
+        }
+        gx += v == 0 ? 2 : 1;
+    }
+}
+
 }  // namespace haar
 }  // namespace fm
 
@@ -514,6 +541,7 @@ struct fm_haar {
     int2* d_taps = nullptr;
     uint8_t *d_raw = nullptr, *d_roi = nullptr;  // fm_haar_detect_frames: source frames, ROI frames
     const uint8_t** d_fptr = nullptr;             // fm_haar_detect_frame_list: the frames' device addresses
+    const uint8_t** h_fptr = nullptr;             // their page-locked staging copy (an asynchronous DMA)
     size_t cap_fptr = 0;
     int32_t *d_axo = nullptr, *d_axc = nullptr, *d_ayo = nullptr, *d_ayc = nullptr;
     float *d_axw = nullptr, *d_ayw = nullptr;
@@ -522,10 +550,22 @@ struct fm_haar {
     size_t cap_raw = 0, cap_roi = 0;
     size_t cap_src = 0, cap_gray = 0, cap_rimg = 0, cap_S = 0, cap_Q = 0, cap_T = 0, cap_res = 0, cap_taps = 0;
     std::vector<int8_t> h_res;
+    int *d_ccnt = nullptr, *d_cand = nullptr;  // k_hwalk: per image candidate count, candidate lists
+    int *h_ccnt = nullptr, *h_cand = nullptr;  // their page-locked host copies
+    size_t cap_cand = 0;
     std::vector<int32_t> cand;  // last call's candidates of image 0 (x, y, w, h)
     double last_ms = 0.;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    // FM_HAAR_TIMES (dev build): host seconds per phase over all calls -- resize setup, geometry + launches,
+    // result copy + wait, post-pass -- printed at destroy
+    bool times = false;
+    double tph[4] = {0, 0, 0, 0};
+    long long ncalls = 0;
 };
+
+static inline double hnow() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 static int hfail(fm_haar* h, int code, const char* fmt, ...) {
     char buf[512];
@@ -587,6 +627,7 @@ int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
     *out = nullptr;
     auto* h = new fm_haar();
     *out = h;
+    h->times = fm::dev_env("FM_HAAR_TIMES") != nullptr;  // (dev build only)
     if (!d || d->win_w < 3 || d->win_h < 3 || d->n_stages < 1 || d->n_trees < 1 || d->n_nodes < 1 ||
         d->n_features < 1 || d->n_leaves != d->n_trees + d->n_nodes)
         return hfail(h, FM_EINVAL, "bad cascade description (window >= 3x3, stages/trees/nodes/features >= 1, "
@@ -734,12 +775,20 @@ int fm_haar_create(int device, const fm_haar_desc* d, fm_haar** out) {
 
 void fm_haar_destroy(fm_haar* h) {
     if (!h) return;
+    if (h->times && h->ncalls)
+        std::fprintf(stderr, "[fm_haar] %lld calls, host ms per call: resize setup %.3f, geometry + launches %.3f, "
+                     "copy + wait %.3f, post-pass %.3f\n", h->ncalls, 1e3 * h->tph[0] / h->ncalls,
+                     1e3 * h->tph[1] / h->ncalls, 1e3 * h->tph[2] / h->ncalls, 1e3 * h->tph[3] / h->ncalls);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_blob, (void*)h->d_src, (void*)h->d_gray, (void*)h->d_rimg, (void*)h->d_S,
                     (void*)h->d_Q, (void*)h->d_T, (void*)h->d_res, (void*)h->d_taps, (void*)h->d_raw, (void*)h->d_fptr, (void*)h->d_live, (void*)h->d_nlive,
                     (void*)h->d_roi, (void*)h->d_axo, (void*)h->d_axc, (void*)h->d_ayo, (void*)h->d_ayc,
                     (void*)h->d_axw, (void*)h->d_ayw})
         if (p) (void)hipFree(p);
+    for (void* p : {(void*)h->d_ccnt, (void*)h->d_cand})
+        if (p) (void)hipFree(p);
+    for (void* p : {(void*)h->h_ccnt, (void*)h->h_cand, (void*)h->h_fptr})
+        if (p) (void)hipHostFree(p);
     if (h->e0) (void)hipEventDestroy(h->e0);
     if (h->e1) (void)hipEventDestroy(h->e1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -763,6 +812,7 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         cap < 0 || !counts || (cap > 0 && !rects))
         return hfail(h, FM_EINVAL, "bad arguments (n >= 1, 1 or 3 channels, scale_factor > 1, counts[n])");
     HH(h, hipSetDevice(h->device));
+    const double tA = h->times ? hnow() : 0.;
     for (int i = 0; i < n; ++i) counts[i] = 0;
     h->cand.clear();
     // scales (detectMultiScaleNoGrouping)
@@ -807,8 +857,10 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
         g.gh[s] = (ylim[s] + g.step[s] - 1) / g.step[s];
         if (g.gw[s] == 0) g.gh[s] = 0;
     }
-    g.P = g.I = g.NW = g.NT = 0;
+    g.P = g.I = g.NW = g.NT = g.NR = 0;
     for (int s = 0; s < g.n; ++s) {
+        g.roff[s] = g.NR;
+        g.NR += g.gw[s] > 0 ? g.gh[s] : 0;
         g.poff[s] = g.P;
         g.ioff[s] = g.I;
         g.woff[s] = g.NW;
@@ -890,9 +942,35 @@ int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int c
 swept:
     HH(h, hipGetLastError());
     HH(h, hipEventRecord(h->e1, h->stream));
-    h->h_res.resize((size_t)nw);
-    if (nw > 0) HH(h, hipMemcpyAsync(h->h_res.data(), h->d_res, (size_t)nw, hipMemcpyDeviceToHost, h->stream));
+    // candidates: the row walk on the device, then only the per-image lists cross PCIe (page-locked)
+    if ((size_t)n > h->cap_cand) {
+        for (void* p : {(void*)h->d_ccnt, (void*)h->d_cand})
+            if (p) HH(h, hipFree(p));
+        for (void* p : {(void*)h->h_ccnt, (void*)h->h_cand})
+            if (p) HH(h, hipHostFree(p));
+        h->d_ccnt = h->d_cand = h->h_ccnt = h->h_cand = nullptr;
+        h->cap_cand = 0;
+        HH(h, hipMalloc((void**)&h->d_ccnt, (size_t)n * sizeof(int)));
+        HH(h, hipMalloc((void**)&h->d_cand, (size_t)n * kCandCap * sizeof(int)));
+        HH(h, hipHostMalloc((void**)&h->h_ccnt, (size_t)n * sizeof(int), 0));
+        HH(h, hipHostMalloc((void**)&h->h_cand, (size_t)n * kCandCap * sizeof(int), 0));
+        h->cap_cand = (size_t)n;
+    }
+    HH(h, hipMemsetAsync(h->d_ccnt, 0, (size_t)n * sizeof(int), h->stream));
+    if (nw > 0 && g.NR > 0)
+        k_hwalk<<<(unsigned)(((long long)n * g.NR + 63) / 64), 64, 0, h->stream>>>(h->d_res, h->d_ccnt, h->d_cand, g, n);
+    HH(h, hipGetLastError());
+    const double tB = h->times ? hnow() : 0.;
+    HH(h, hipMemcpyAsync(h->h_ccnt, h->d_ccnt, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HH(h, hipMemcpyAsync(h->h_cand, h->d_cand, (size_t)n * kCandCap * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     HH(h, hipStreamSynchronize(h->stream));
+    bool overflow = false;
+    for (int i = 0; i < n; ++i) overflow |= h->h_ccnt[i] > kCandCap;
+    if (overflow) {  // some image has more accepted windows than a list holds: walk the whole grid here
+        h->h_res.resize((size_t)nw);
+        HH(h, hipMemcpy(h->h_res.data(), h->d_res, (size_t)nw, hipMemcpyDeviceToHost));
+    }
+    const double tC = h->times ? hnow() : 0.;
     float ms = 0.f;
     HH(h, hipEventElapsedTime(&ms, h->e0, h->e1));
     h->last_ms = ms;
@@ -902,19 +980,30 @@ swept:
     const double eps = 0.2;
     auto post = [&](int img) {
         std::vector<int32_t> c;
-        const int8_t* R = h->h_res.data() + (size_t)img * g.NW;
-        for (int s = 0; s < g.n; ++s) {
+        auto emit = [&](int s, int gy, int gx) {
             const float f = sc[s];
             const int wsw = rne_f((float)h->win_w * f), wsh = rne_f((float)h->win_h * f);
-            for (int gy = 0; gy < g.gh[s]; ++gy)
-                for (int gx = 0; gx < g.gw[s];) {
-                    const int8_t v = R[g.woff[s] + gy * g.gw[s] + gx];
-                    if (v > 0) {
-                        const int x = gx * g.step[s], y = gy * g.step[s];
-                        c.insert(c.end(), {rne_f((float)x * f), rne_f((float)y * f), wsw, wsh});
+            const int x = gx * g.step[s], y = gy * g.step[s];
+            c.insert(c.end(), {rne_f((float)x * f), rne_f((float)y * f), wsw, wsh});
+        };
+        if (!overflow) {  // the device's lists: sorted window indices are OpenCV's visiting order
+            const int nc0 = h->h_ccnt[img];
+            int* L = h->h_cand + (size_t)img * kCandCap;
+            std::sort(L, L + nc0);
+            for (int k = 0, s = 0; k < nc0; ++k) {
+                while (s + 1 < g.n && L[k] >= g.woff[s + 1]) ++s;
+                const int q = L[k] - g.woff[s], gy = q / g.gw[s];
+                emit(s, gy, q - gy * g.gw[s]);
+            }
+        } else {
+            const int8_t* R = h->h_res.data() + (size_t)img * g.NW;
+            for (int s = 0; s < g.n; ++s)
+                for (int gy = 0; gy < g.gh[s]; ++gy)
+                    for (int gx = 0; gx < g.gw[s];) {
+                        const int8_t v = R[g.woff[s] + gy * g.gw[s] + gx];
+                        if (v > 0) emit(s, gy, gx);
+                        gx += v == 0 ? 2 : 1;
                     }
-                    gx += v == 0 ? 2 : 1;
-                }
         }
         if (img == 0) h->cand = c;
         const int nc = (int)c.size() / 4;
@@ -992,8 +1081,12 @@ swept:
         const int keep = std::min(no, cap);
         if (keep > 0) std::memcpy(rects + (size_t)img * cap * 4, outr.data(), sizeof(int32_t) * 4 * keep);
     };
-    // (64 1080p ROI frames of frontalface: 12.1 ms per call single-threaded beside 3.1 ms of kernels)
-    const int nth = std::min(n, std::max(1, std::min(kPostThreads, (int)std::thread::hardware_concurrency())));
+    // (64 1080p ROI frames of frontalface: 12.1 ms per call single-threaded beside 3.1 ms of kernels, when
+    // the host walked every window; with the device's lists only grouping is left, worth threads only for
+    // many candidates)
+    long long ncand = 0;
+    for (int i = 0; i < n; ++i) ncand += overflow ? (long long)g.NW : h->h_ccnt[i];
+    const int nth = ncand < 4096 ? 1 : std::min(n, std::max(1, std::min(kPostThreads, (int)std::thread::hardware_concurrency())));
     if (nth <= 1) {
         for (int img = 0; img < n; ++img) post(img);
     } else {
@@ -1004,6 +1097,13 @@ swept:
                 for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) post(i);
             });
         for (auto& t : pool) t.join();
+    }
+    if (h->times) {
+        const double tD = hnow();
+        h->tph[1] += tB - tA;
+        h->tph[2] += tC - tB;
+        h->tph[3] += tD - tC;
+        h->ncalls++;
     }
     return FM_OK;
 }
@@ -1036,6 +1136,7 @@ static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* 
     if (!identity && !(sx >= 1 && sy >= 1))
         return hfail(h, FM_ENOTSUP, "frame width %d < ROI width %d: INTER_AREA upscaling is not supported", W, rw);
     HH(h, hipSetDevice(h->device));
+    const double t0 = h->times ? hnow() : 0.;
     const size_t fb = (size_t)H * W * 3;
     const uint8_t* src = frames;
     int rc;
@@ -1043,8 +1144,19 @@ static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* 
     // it can; otherwise the frames are gathered on the detector's stream first
     const uint8_t* const* dlist = nullptr;
     if (list) {
-        if ((rc = grow(h, &h->d_fptr, h->cap_fptr, (size_t)n))) return rc;
-        HH(h, hipMemcpyAsync(h->d_fptr, list, (size_t)n * sizeof(const uint8_t*), hipMemcpyHostToDevice, h->stream));
+        // from page-locked memory: a pageable source made this small copy cost ~0.5 ms of host time per
+        // call beside a busy pixel stream (FM_HAAR_TIMES); the previous call's copy is done (each call
+        // ends with a stream synchronize)
+        if ((size_t)n > h->cap_fptr) {
+            if (h->h_fptr) HH(h, hipHostFree((void*)h->h_fptr));
+            h->h_fptr = nullptr;
+            size_t cap = h->cap_fptr;
+            if ((rc = grow(h, &h->d_fptr, cap, (size_t)n))) return rc;
+            HH(h, hipHostMalloc((void**)&h->h_fptr, (size_t)n * sizeof(const uint8_t*), 0));
+            h->cap_fptr = cap;
+        }
+        std::memcpy((void*)h->h_fptr, list, (size_t)n * sizeof(const uint8_t*));
+        HH(h, hipMemcpyAsync(h->d_fptr, h->h_fptr, (size_t)n * sizeof(const uint8_t*), hipMemcpyHostToDevice, h->stream));
         dlist = h->d_fptr;
     }
     auto gather = [&]() -> int {
@@ -1104,6 +1216,7 @@ static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* 
     } else if (list) {
         roi = src;
     }
+    if (h->times) h->tph[0] += hnow() - t0;
     return fm_haar_detect(h, roi, n, rh, rw, 3, 1, scale_factor, min_neighbors, 0, 0, 0, 0, rects, cap, counts);
 }
 
