@@ -56,6 +56,9 @@ constexpr int RG = 512;         // k_regions threads
 #define FM_CCL_PRIO 0  // contour waves' issue priority over the pixel kernel's (round 2: +4 % at 2; round 3: 0 gives
                        // the same throughput, 368.1 vs 368.2 k, with 6 % shorter pixel launches, 436 vs 464 us)
 #endif
+#ifndef FM_CCL_REST_PRIO
+#define FM_CCL_REST_PRIO 0  // issue priority of k_regions / k_fold / k_emit / k_counts (0: the default)
+#endif
 #ifndef FM_HEAVY_PRIO
 #define FM_HEAVY_PRIO 0  // (was 3, see FM_CCL_PRIO)
 #endif
@@ -633,6 +636,7 @@ template <bool DILATE>
 // workgroup, which the contour kernels resident beside the pixel kernel often did not leave free,
 // so a batch's k_regions waited for the pixel kernel to end: 269 µs instead of 10)
 __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
+    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     extern __shared__ int uf[];  // [a.ntiles]
     __shared__ int s_nc, s_nr;
     const int f = blockIdx.x;
@@ -990,6 +994,7 @@ __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
 // one wave per candidate tile (lanes = its components) or per empty-tile region: path
 // compression with outer flags, bboxes and raster-first pixels folded into the roots
 __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
+    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
@@ -1065,6 +1070,7 @@ __device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wav
 }
 
 __global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
+    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
@@ -1257,6 +1263,7 @@ __global__ __launch_bounds__(64 * CW) void k_resolve(FusedArgs a) {
 // batch (k_pix rewrites its per-wave flag words every frame)
 constexpr int FT = 256;
 __global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
+    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const size_t f = blockIdx.x;
     const size_t F = (size_t)a.T * a.S;
     if (a.tflag_waves == 1)

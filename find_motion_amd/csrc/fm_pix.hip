@@ -1237,9 +1237,22 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
 #else
 #define P5_PH(acc) do { } while (0)
 #endif
+#ifndef FM_P5_QPRIO
+#define FM_P5_QPRIO 0  // issue priority falling with progress (levels: FM_P5_QPRIO + 1), so that the younger of a
+                       // CU's two workgroups catches up with the older one instead of finishing alone
+#endif
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
+        if constexpr (FM_P5_QPRIO > 0) {
+            if (((t - t0) & 15) == 0) {
+                const int lv = FM_P5_QPRIO - ((t - t0) * (FM_P5_QPRIO + 1)) / (t1 - t0);  // wave-uniform
+                if (lv >= 3) __builtin_amdgcn_s_setprio(3);
+                else if (lv == 2) __builtin_amdgcn_s_setprio(2);
+                else if (lv == 1) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+        }
         P5_PH(ph3);
         lds_barrier();
         P5_PH(ph0);
