@@ -1579,15 +1579,17 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
 #ifndef FM_P5_PAIR
 #define FM_P5_PAIR 0  // 64 x 64 tiles two per 1,024-thread workgroup when the tile count is even (k_pix5 PAIR)
 #endif
-        if (FM_P5_PAIR && a.ntiles % 2 == 0 && a.ntiles * a.S >= 128) {
-            const dim3 pgrid(a.ntiles / 2, a.S);
-            const size_t lds = 2 * px::p5_half_bytes<8>();
-            static_assert(2 * px::p5_half_bytes<8>() <= 64 * 1024, "tile pair LDS");
-            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 2>), pgrid, dim3(1024), lds, st, a);
-            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 2>), pgrid, dim3(1024), lds, st, a);
-            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 2>), pgrid, dim3(1024), lds, st, a);
-            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 2>), pgrid, dim3(1024), lds, st, a);
-            return hipGetLastError();
+        if constexpr (FM_P5_PAIR != 0) {
+            if (a.ntiles % 2 == 0 && a.ntiles * a.S >= 128) {
+                const dim3 pgrid(a.ntiles / 2, a.S);
+                const size_t lds = 2 * px::p5_half_bytes<8>();
+                static_assert(2 * px::p5_half_bytes<8>() <= 64 * 1024, "tile pair LDS");
+                if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 2>), pgrid, dim3(1024), lds, st, a);
+                else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 2>), pgrid, dim3(1024), lds, st, a);
+                else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 2>), pgrid, dim3(1024), lds, st, a);
+                else hipLaunchKernelGGL((px::k_pix5<8, false, false, 2>), pgrid, dim3(1024), lds, st, a);
+                return hipGetLastError();
+            }
         }
         const int nwb = !FM_P5_BANDS || a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
         const int nby = a.nty * (8 / nwb);  // bands covering every 64-row contour tile whole
