@@ -492,8 +492,34 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 
     fm_ctx* cp = c.get();
     HIP_TRY(cp, hipSetDevice(p.device));
-    {   // the pixel stream at high priority: it gets a hardware queue of its own instead of
-        // sharing one (in order) with a contour-pass stream
+    // Small work image behind a resize (mode D, -B 100: 1080p -> 100 x 56, two 64 x 64 tiles per stream):
+    // the pixel kernel is a few workgroups whose frames run one after another (latency-bound), the
+    // INTER_AREA resize of the next batch streams whole frames over every CU.  Sharing CUs, the resize
+    // doubled the pixel launch (276 -> 540 us per 256 frames, profiles/r04rs_modeD); so the pixel
+    // stream gets 8 CUs of its own (one per 32) and the input stream the others.
+#ifndef FM_CU_SPLIT
+#define FM_CU_SPLIT 1
+#endif
+    const long long work_tiles = (long long)((c->w + 63) / 64) * ((c->h + 63) / 64) * p.n_streams;
+    bool cu_split = FM_CU_SPLIT && c->rmode != ResizeMode::Identity && work_tiles <= 16;
+    if (const char* e = dev_env("FM_CU_SPLIT")) cu_split = std::atoi(e) != 0 && c->rmode != ResizeMode::Identity && work_tiles <= 16;
+    std::vector<uint32_t> pix_mask, rs_mask;
+    if (cu_split) {
+        hipDeviceProp_t prop;
+        HIP_TRY(cp, hipGetDeviceProperties(&prop, p.device));
+        const int ncu = prop.multiProcessorCount;
+        if (ncu >= 64) {
+            pix_mask.assign((ncu + 31) / 32, 0u);
+            rs_mask.assign((ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu; i++) ((i % 32 == 0) ? pix_mask : rs_mask)[i / 32] |= 1u << (i % 32);
+        } else {
+            cu_split = false;
+        }
+    }
+    if (cu_split) {
+        HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->own_stream, (uint32_t)pix_mask.size(), pix_mask.data()));
+    } else {  // the pixel stream at high priority: it gets a hardware queue of its own instead of
+              // sharing one (in order) with a contour-pass stream
         int lo = 0, hi = 0;
         HIP_TRY(cp, hipDeviceGetStreamPriorityRange(&lo, &hi));
         if (dev_env("FM_PIX_PRIO_OFF")) hi = lo;
@@ -513,7 +539,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         for (int i = 0; i < c->nccl; i++) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
-    if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
+    if (cu_split) HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()));
+    else if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
