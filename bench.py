@@ -24,9 +24,12 @@ import os
 import sys
 import time
 
-# eight hardware queues (find_motion_amd.use_hw_queues, the CLI's setting), before torch makes the first HIP
-# call; the value in effect is recorded in the JSON line
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# eight hardware queues per process (find_motion_amd.use_hw_queues, the CLI's setting), before torch makes the
+# first HIP call, whatever the environment holds (the GPU box exports HIP's default, 4): with 4 the input
+# stream shares an in-order queue with a contour stream (mode D 498 -> 591 k frames/s at 8, MJPEG-fed 74 ->
+# 84 k, the headline unchanged; profiles/r04s_hwq_ab.txt).  FM_BENCH_HW_QUEUES picks another count; the value
+# in effect is recorded in the JSON line
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("FM_BENCH_HW_QUEUES", "8")
 
 import numpy as np
 

@@ -289,7 +289,7 @@ def run(args: Namespace, print_help: typing.Callable = lambda: None) -> list:
 
 def main(argv=None) -> None:
     from . import use_hw_queues
-    use_hw_queues()  # before any HIP call in this process (and inherited by --gpus workers)
+    use_hw_queues(int(os.environ.get("FM_HW_QUEUES", "8")), force=True)  # before any HIP call (inherited by --gpus workers)
     parser = ArgumentParser(description="Find motion and objects in video (MI355X)")
     get_args(parser)
     args = parser.parse_args(argv)

@@ -139,3 +139,18 @@ def test_import_leaves_hw_queues_alone():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
     assert out.stdout.split() == ["None", "8", "8"], out.stdout + out.stderr
+
+
+def test_use_hw_queues_env_wins_unless_forced():
+    """A GPU_MAX_HW_QUEUES already in the environment stays (use_hw_queues()), unless forced, as the CLI and
+    bench.py do: machines commonly export HIP's default 4, which serialises the input stream behind a
+    contour stream."""
+    import os
+    import subprocess
+    import sys
+    code = ("import os, find_motion_amd as f; a = f.use_hw_queues(); b = f.use_hw_queues(8, force=True); "
+            "print(a, b, os.environ['GPU_MAX_HW_QUEUES'])")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="4")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["4", "8", "8"], out.stdout + out.stderr
