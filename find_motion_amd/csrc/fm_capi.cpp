@@ -511,7 +511,16 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         if (ncu >= 64) {
             pix_mask.assign((ncu + 31) / 32, 0u);
             rs_mask.assign((ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu; i++) ((i % 32 == 0) ? pix_mask : rs_mask)[i / 32] |= 1u << (i % 32);
+#ifndef FM_CU_SPLIT_EVERY
+#define FM_CU_SPLIT_EVERY 32  // the pixel stream's CUs: one in FM_CU_SPLIT_EVERY
+#endif
+#ifndef FM_CU_RS_FROM
+#define FM_CU_RS_FROM 1  // the input stream's CUs: i % 32 >= FM_CU_RS_FROM of the others (1: all of them)
+#endif
+            for (int i = 0; i < ncu; i++) {
+                if (i % FM_CU_SPLIT_EVERY == 0) pix_mask[i / 32] |= 1u << (i % 32);
+                else if (i % 32 >= FM_CU_RS_FROM) rs_mask[i / 32] |= 1u << (i % 32);
+            }
         } else {
             cu_split = false;
         }
