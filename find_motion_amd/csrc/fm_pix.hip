@@ -993,11 +993,15 @@ struct P5Raw {
 // barrier keeps both tiles of a CU at the same frame.
 template <int NWB>
 constexpr int p5_half_bytes() { return (P5G<NWB>::dyn_bytes + 15) & ~15; }
-template <int NWB, bool KEEP, bool TAIL, int PAIR = 1>
-__global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+// SPL (small work images, e.g. mode D's 100 x 56: two tiles, 256 frames in a row): 16 waves per tile,
+// waves 0-7 run the chain of their 8 rows and waves 8-15 the taps, gray and loads of the next frames, so a
+// frame's critical path is the longer of the two halves instead of their sum.
+template <int NWB, bool KEEP, bool TAIL, int PAIR = 1, bool SPL = false>
+__global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
     using G = P5G<NWB>;
     static_assert(FM_P5_EVENP || NWB == 8, "bands need the even-pair chain (its flag rows follow wb)");
     static_assert(PAIR == 1 || (NWB == 8 && FM_P5_SDWA == 0), "tile pairs: 64-row tiles, the table in each half's LDS");
+    static_assert(!SPL || (NWB == 8 && PAIR == 1), "split waves: 64-row tiles, one tile per workgroup");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_all[];
     const int half = PAIR > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (64 * NWB)) : 0;
     uint8_t* smem = smem_all + half * p5_half_bytes<NWB>();
@@ -1013,6 +1017,8 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
     }
     const int tid = PAIR > 1 ? (int)threadIdx.x % (64 * NWB) : (int)threadIdx.x, ln = tid & 63;  // (within the tile)
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool cw = !SPL || wv < 8;  // SPL: a chain wave (0-7) or a producer (8-15: pw = wv - 8)
+    const int pw = wv - 8, ptid = tid - 512;
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
     int ti, tx, y0, wb0;  // contour tile, its column, the band's first row, its first 8-row slice of the tile
@@ -1061,10 +1067,12 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
     uint32_t goff[G::GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
     uint32_t gdst[G::GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
     // this wave's gray slots (wave-uniform): the 4 / 4 deal in a 64-row workgroup, contiguous runs in a band
-    const int gjobs = NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : max(0, min(G::GFAST, G::GSLOTS - wv * G::GFAST));
+    const int gjobs = SPL ? (cw ? 0 : min(G::GJ, (G::GSLOTS - pw + 7) / 8))
+                          : NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : max(0, min(G::GFAST, G::GSLOTS - wv * G::GFAST));
 #pragma unroll
     for (int i = 0; i < G::GJ; i++) {
-        const int slot = NWB == 8 ? (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i) : wv * G::GFAST + i;
+        const int slot = SPL ? pw + 8 * i
+                             : NWB == 8 ? (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i) : wv * G::GFAST + i;
         const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / G::GQ, gq = j - gr * G::GQ;
         const int x = x0 - 4 + 4 * gq;
@@ -1074,11 +1082,11 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
         gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
     }
     uint32_t hsrc[G::HJ], hdst[G::HJ];
-    const int hjobs = G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
+    const int hjobs = SPL ? (cw ? 0 : G::HJ) : G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
     for (int i = 0; i < G::HJ; i++) {
         const int hslot = wv >= 4 ? (wv - 4) * G::HSLOW + i : 4 * G::HSLOW + wv * G::HFAST + i;
-        const int j = G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
+        const int j = SPL ? (cw ? G::NH : ptid + G::NTB * i) : G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
         hsrc[i] = (uint32_t)(G::HR * hr * G::GQ + hq);
@@ -1111,7 +1119,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int j = 0; j < RPWV; j++) {
             const int y = y0 + RPWV * wv + j;
-            const bool in = x < w && y < h;
+            const bool in = cw && x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
@@ -1162,7 +1170,8 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < G::HJ; i++) {
-            if (G::HFAST ? i >= hjobs : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
+            if (SPL ? (i >= hjobs || (i == G::HJ - 1 && pw >= G::HLASTW))
+                    : G::HFAST ? i >= hjobs : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
             if (edge_tile) {
@@ -1209,13 +1218,13 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
     // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
     // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
     // unconditional, frame indices clamped to the batch (see load).
-    load((size_t)t0 * S + s);
+    if (!SPL || !cw) load((size_t)t0 * S + s);  // (SPL: the chain waves load nothing)
     gray_stage(gray);
-    load((size_t)min(t0 + 1, t1 - 1) * S + s);
+    if (!SPL || !cw) load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
-    load((size_t)min(t0 + 2, t1 - 1) * S + s);
+    if (!SPL || !cw) load((size_t)min(t0 + 2, t1 - 1) * S + s);
 
     // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
     // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
@@ -1231,7 +1240,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
 #endif
 #if defined(FM_DEV_SWITCHES) && FM_P5_PHASES
     // profiling (FM_PTS, dev build): per-wave cycles in the frame barrier, chain, taps, gray+stores+loads
-    uint64_t* phw = a.dbg_pts ? a.dbg_pts + (size_t)a.S * a.ntiles * 4 + (((size_t)s * a.ntiles + ti) * NW + wv) * 4 : nullptr;
+    uint64_t* phw = (a.dbg_pts && wv < NW) ? a.dbg_pts + (size_t)a.S * a.ntiles * 4 + (((size_t)s * a.ntiles + ti) * NW + wv) * 4 : nullptr;
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, tA = __builtin_amdgcn_s_memtime(), tB;
 #define P5_PH(acc) do { if (phw) { tB = __builtin_amdgcn_s_memtime(); acc += tB - tA; tA = tB; } } while (0)
 #else
@@ -1241,6 +1250,38 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
 #define FM_P5_QPRIO 0  // issue priority falling with progress (levels: FM_P5_QPRIO + 1), so that the younger of a
                        // CU's two workgroups catches up with the older one instead of finishing alone
 #endif
+    if constexpr (SPL) {
+        static_assert((FM_P5_EVENP != 0) && (FM_P5_HPAIR != 0), "split waves: the even-pair chain");
+        if (cw) {  // chain waves: frame t's chain, its bits and flag word
+            for (int t = t0; t < t1; t++) {
+                const int b = (t - t0) & 1;
+                const size_t f = (size_t)t * S + s;
+                lds_barrier();
+                uint32_t colbits = 0, fl = 0;
+                ChainCtx ccf = cc;
+                ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+                int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
+                asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+                var = __builtin_amdgcn_readfirstlane(var);
+                asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+                const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
+                if (!TAIL || var == 0)
+                    chain_rows_w<KC, KEEP, false, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                else
+                    chain_rows_w<KC, KEEP, true, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+                if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            }
+        } else {  // producers: taps(t+1), gray(t+2), the load of frame t+3
+            for (int t = t0; t < t1; t++) {
+                const int b = (t - t0) & 1;
+                lds_barrier();
+                if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
+                gray_stage(gray + b * G::GBUF);
+                load((size_t)min(t + 3, t1 - 1) * S + s);
+            }
+        }
+    } else
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
@@ -1312,7 +1353,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int j = 0; j < RPWV; j++) {
         const int y = y0 + RPWV * wv + j;
-        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+        if (cw && x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
 #ifdef FM_DEV_SWITCHES
     if (pts) {
@@ -1579,6 +1620,18 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
 #ifndef FM_P5_PAIR
 #define FM_P5_PAIR 0  // 64 x 64 tiles two per 1,024-thread workgroup when the tile count is even (k_pix5 PAIR)
 #endif
+#ifndef FM_P5_SPLIT
+#define FM_P5_SPLIT 0  // small work images (<= 16 tiles): 16 waves per tile, chain and producer halves (k_pix5 SPL)
+#endif
+        if (FM_P5_SPLIT && a.ntiles * a.S <= 16) {
+            const dim3 sgrid(a.ntiles, a.S);
+            const size_t lds = px::P5G<8>::dyn_bytes;
+            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 1, true>), sgrid, dim3(1024), lds, st, a);
+            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 1, true>), sgrid, dim3(1024), lds, st, a);
+            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 1, true>), sgrid, dim3(1024), lds, st, a);
+            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 1, true>), sgrid, dim3(1024), lds, st, a);
+            return hipGetLastError();
+        }
         if constexpr (FM_P5_PAIR != 0) {
             if (a.ntiles % 2 == 0 && a.ntiles * a.S >= 128) {
                 const dim3 pgrid(a.ntiles / 2, a.S);
