@@ -996,9 +996,13 @@ constexpr int p5_half_bytes() { return (P5G<NWB>::dyn_bytes + 15) & ~15; }
 // SPL (small work images, e.g. mode D's 100 x 56: two tiles, 256 frames in a row): 16 waves per tile,
 // waves 0-7 run the chain of their 8 rows and waves 8-15 the taps, gray and loads of the next frames, so a
 // frame's critical path is the longer of the two halves instead of their sum.
-template <int NWB, bool KEEP, bool TAIL, int PAIR = 1, bool SPL = false>
-__global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
+template <int NWB, bool KEEP, bool TAIL, int PAIR = 1, bool SPL = false, int NPW = 8>
+__global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
     using G = P5G<NWB>;
+    // job rounds per wave: SPL deals the gray slots and tap jobs over the NPW producer waves only
+    constexpr int GJX = SPL ? (G::GSLOTS + NPW - 1) / NPW : G::GJ;
+    constexpr int HJX = SPL ? (G::NH + 64 * NPW - 1) / (64 * NPW) : G::HJ;
+    constexpr int HLASTX = SPL ? (G::NH - (HJX - 1) * 64 * NPW + 63) / 64 : G::HLASTW;
     static_assert(FM_P5_EVENP || NWB == 8, "bands need the even-pair chain (its flag rows follow wb)");
     static_assert(PAIR == 1 || (NWB == 8 && FM_P5_SDWA == 0), "tile pairs: 64-row tiles, the table in each half's LDS");
     static_assert(!SPL || (NWB == 8 && PAIR == 1), "split waves: 64-row tiles, one tile per workgroup");
@@ -1064,14 +1068,14 @@ __global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amd
 #endif
 
     // ---- per-thread job plans (frame invariant)
-    uint32_t goff[G::GJ];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
-    uint32_t gdst[G::GJ];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
+    uint32_t goff[GJX];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
+    uint32_t gdst[GJX];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
     // this wave's gray slots (wave-uniform): the 4 / 4 deal in a 64-row workgroup, contiguous runs in a band
-    const int gjobs = SPL ? (cw ? 0 : min(G::GJ, (G::GSLOTS - pw + 7) / 8))
+    const int gjobs = SPL ? (cw ? 0 : min(GJX, (G::GSLOTS - pw + NPW - 1) / NPW))
                           : NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : max(0, min(G::GFAST, G::GSLOTS - wv * G::GFAST));
 #pragma unroll
-    for (int i = 0; i < G::GJ; i++) {
-        const int slot = SPL ? pw + 8 * i
+    for (int i = 0; i < GJX; i++) {
+        const int slot = SPL ? pw + NPW * i
                              : NWB == 8 ? (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i) : wv * G::GFAST + i;
         const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / G::GQ, gq = j - gr * G::GQ;
@@ -1081,12 +1085,12 @@ __global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amd
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
         gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
     }
-    uint32_t hsrc[G::HJ], hdst[G::HJ];
-    const int hjobs = SPL ? (cw ? 0 : G::HJ) : G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
+    uint32_t hsrc[HJX], hdst[HJX];
+    const int hjobs = SPL ? (cw ? 0 : HJX) : G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < G::HJ; i++) {
+    for (int i = 0; i < HJX; i++) {
         const int hslot = wv >= 4 ? (wv - 4) * G::HSLOW + i : 4 * G::HSLOW + wv * G::HFAST + i;
-        const int j = SPL ? (cw ? G::NH : ptid + G::NTB * i) : G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
+        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
         hsrc[i] = (uint32_t)(G::HR * hr * G::GQ + hq);
@@ -1099,9 +1103,9 @@ __global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amd
     // gray(w-2), gray(w-3) from the quad before it); further quads feed only columns past the image
     const bool edge_tile = x0 == 0 || x0 + TS + 4 > w;  // workgroup-uniform
     const int vq = (w - x0 + 4) / 4;  // gray quad index of the quad starting at column w
-    uint32_t hfix[G::HJ];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
+    uint32_t hfix[HJX];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
 #pragma unroll
-    for (int i = 0; i < G::HJ; i++) {
+    for (int i = 0; i < HJX; i++) {
         const int hq = (int)(hsrc[i] % G::GQ);
         hfix[i] = (x0 == 0 && hq == 0 ? 1u : 0u) | (hq + 1 == vq ? 2u : 0u) | (hq + 2 == vq ? 4u : 0u);
     }
@@ -1142,7 +1146,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amd
     cpk[1] = tap4<KC>(1);
     uint32_t hcs[HS<KC>::NC];
     if (FM_HSHIFT) hs_consts<KC>(hcs);
-    P5Raw<G::GJ> rw;
+    P5Raw<GJX> rw;
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
@@ -1151,26 +1155,26 @@ __global__ __launch_bounds__(64 * NWB * PAIR * (SPL ? 2 : 1)) __attribute__((amd
         if constexpr (FM_P5_BUFLD != 0) {
             const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
-            for (int i = 0; i < G::GJ; i++) load12b(rw.v[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
+            for (int i = 0; i < GJX; i++) load12b(rw.v[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
         } else {
             const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
-            for (int i = 0; i < G::GJ; i++) {
+            for (int i = 0; i < GJX; i++) {
                 load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
             }
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < G::GJ; i++) {
+        for (int i = 0; i < GJX; i++) {
             if (i >= gjobs) break;  // wave-uniform
             gb[gdst[i]] = gray4(rw.v[i].x, rw.v[i].y, rw.v[i].z);
         }
     };
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < G::HJ; i++) {
-            if (SPL ? (i >= hjobs || (i == G::HJ - 1 && pw >= G::HLASTW))
+        for (int i = 0; i < HJX; i++) {
+            if (SPL ? (i >= hjobs || (i == HJX - 1 && pw >= HLASTX))
                     : G::HFAST ? i >= hjobs : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
@@ -1623,6 +1627,18 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
 #ifndef FM_P5_SPLIT
 #define FM_P5_SPLIT 1  // small work images (<= 16 tiles): 16 waves per tile, chain and producer halves (k_pix5 SPL; mode D +3.4 %)
 #endif
+#ifndef FM_P5_SPLIT_LARGE
+#define FM_P5_SPLIT_LARGE 0  // larger images too: 8 chain + 4 producer waves (768 threads, two workgroups per CU)
+#endif
+        if (FM_P5_SPLIT_LARGE && a.ntiles * a.S > 16) {
+            const dim3 sgrid(a.ntiles, a.S);
+            const size_t lds = px::P5G<8>::dyn_bytes;
+            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 1, true, 4>), sgrid, dim3(768), lds, st, a);
+            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 1, true, 4>), sgrid, dim3(768), lds, st, a);
+            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 1, true, 4>), sgrid, dim3(768), lds, st, a);
+            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 1, true, 4>), sgrid, dim3(768), lds, st, a);
+            return hipGetLastError();
+        }
         if (FM_P5_SPLIT && a.ntiles * a.S <= 16) {
             const dim3 sgrid(a.ntiles, a.S);
             const size_t lds = px::P5G<8>::dyn_bytes;
