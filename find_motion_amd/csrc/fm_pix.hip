@@ -1387,9 +1387,14 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
 #ifndef FM_PIXW_WPE
 #define FM_PIXW_WPE 4  // 2 workgroups per CU (<= 128 VGPRs)
 #endif
-template <int KC, int NWB, bool KEEP, bool TAIL>
-__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
+// SPL: as k_pix5's, 8 chain waves and NPW producer waves (taps, gray, loads) sharing the frame barrier
+template <int KC, int NWB, bool KEEP, bool TAIL, bool SPL = false, int NPW = 4>
+__global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
     using G = PW<KC, NWB>;
+    static_assert(!SPL || NWB == 8, "split waves: 64-row tiles");
+    constexpr int GJX = SPL ? (G::GSLOTS + NPW - 1) / NPW : G::GJ;
+    constexpr int HJX = SPL ? (G::NH + 64 * NPW - 1) / (64 * NPW) : G::HJ;
+    constexpr int HLASTX = SPL ? (G::NH - (HJX - 1) * 64 * NPW + 63) / 64 : G::HLASTW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
@@ -1403,6 +1408,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     }
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool cw = !SPL || wv < 8;  // SPL: a chain wave, or a producer (pw = wv - 8)
+    const int pw = wv - 8, ptid = tid - 512;
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
     int ti, tx, y0, wb;  // the wave's contour tile, the band's column, first row, the wave's 8-row slice of its tile
@@ -1430,11 +1437,12 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);  // (NWB >= 4)
 
     // ---- per-thread job plans (frame invariant)
-    uint32_t goff[G::GJ], gdst[G::GJ];
+    uint32_t goff[GJX], gdst[GJX];
+    const int gcnt_w = SPL ? (cw ? 0 : (G::GSLOTS - pw + NPW - 1) / NPW) : G::gcnt(wv);
 #pragma unroll
-    for (int i = 0; i < G::GJ; i++) {
-        const int slot = i * NWB + wv;
-        const int j = (i < G::gcnt(wv) && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
+    for (int i = 0; i < GJX; i++) {
+        const int slot = SPL ? i * NPW + pw : i * NWB + wv;
+        const int j = (i < gcnt_w && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
         const int gr = j / GQ, gq = j - gr * GQ;
         const int x = x0 - PC + 4 * gq;
         const bool live = j < G::NG && x >= 0 && x + 4 <= w;
@@ -1442,12 +1450,12 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
         gdst[i] = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + ln);
     }
-    const int gjobs = __builtin_amdgcn_readfirstlane(G::gcnt(wv));  // this wave's gray rounds
-    uint32_t hsrc[G::HJ], hdst[G::HJ];
-    int hqv[G::HJ];
+    const int gjobs = __builtin_amdgcn_readfirstlane(gcnt_w);  // this wave's gray rounds
+    uint32_t hsrc[HJX], hdst[HJX];
+    int hqv[HJX];
 #pragma unroll
-    for (int i = 0; i < G::HJ; i++) {
-        const int j = tid + G::NTB * i;
+    for (int i = 0; i < HJX; i++) {
+        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
         hqv[i] = hq;
@@ -1468,7 +1476,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
 #pragma unroll
         for (int j = 0; j < RPWV; j++) {
             const int y = y0 + RPWV * wv + j;
-            const bool in = x < w && y < h;
+            const bool in = cw && x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
@@ -1486,23 +1494,23 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     uint32_t cpk[G::NGR];
 #pragma unroll
     for (int gi = 0; gi < G::NGR; gi++) cpk[gi] = tapw4<KC>(gi);
-    u32x3_t rw[G::GJ];
+    u32x3_t rw[GJX];
     // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
         if constexpr (FM_PW_BUFLD != 0) {
             const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
-            for (int i = 0; i < G::GJ; i++) load12b(rw[i], rs, goff[i]);
+            for (int i = 0; i < GJX; i++) load12b(rw[i], rs, goff[i]);
         } else {
             const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
-            for (int i = 0; i < G::GJ; i++) load12(rw[i], src, goff[i]);
+            for (int i = 0; i < GJX; i++) load12(rw[i], src, goff[i]);
         }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < G::GJ; i++) {
+        for (int i = 0; i < GJX; i++) {
             if (i >= gjobs) break;  // wave-uniform
             gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z);
         }
@@ -1535,8 +1543,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
     };
     auto tap_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < G::HJ; i++) {
-            if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
+        for (int i = 0; i < HJX; i++) {
+            if (SPL ? (!cw && (i == HJX - 1 && pw >= HLASTX)) || cw : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
             const uint32_t* r0 = gb + (hsrc[i] - hqv[i]);
             uint32_t u[4], v[4];
             hrow(r0, hqv[i], u);
@@ -1546,14 +1554,45 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
         }
     };
     const int t0 = a.t_begin, t1 = a.t_end;
-    load((size_t)t0 * S + s);
+    if (!SPL || !cw) load((size_t)t0 * S + s);
     gray_stage(gray);
-    load((size_t)min(t0 + 1, t1 - 1) * S + s);
+    if (!SPL || !cw) load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
-    load((size_t)min(t0 + 2, t1 - 1) * S + s);
+    if (!SPL || !cw) load((size_t)min(t0 + 2, t1 - 1) * S + s);
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;
+    if constexpr (SPL) {
+        if (cw) {
+            for (int t = t0; t < t1; t++) {
+                const int b = (t - t0) & 1;
+                const size_t f = (size_t)t * S + s;
+                lds_barrier();
+                uint32_t colbits = 0, fl = 0;
+                ChainCtx ccf = cc;
+                ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+                int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
+                asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+                var = __builtin_amdgcn_readfirstlane(var);
+                asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+                const uint32_t* Hb = Hs + b * G::HBUF;
+                if (!TAIL || var == 0)
+                    chain_rows_w<KC, KEEP, false, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                else
+                    chain_rows_w<KC, KEEP, true, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+                if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            }
+        } else {
+            for (int t = t0; t < t1; t++) {
+                const int b = (t - t0) & 1;
+                lds_barrier();
+                if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
+                gray_stage(gray + b * G::GBUF);
+                load((size_t)min(t + 3, t1 - 1) * S + s);
+            }
+        }
+    } else
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
@@ -1585,7 +1624,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(FM_PIX
 #pragma unroll
     for (int j = 0; j < RPWV; j++) {
         const int y = y0 + RPWV * wv + j;
-        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+        if (cw && x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
 }
 
@@ -1705,6 +1744,23 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
             hipLaunchKernelGGL((px::k_pixw<21, NWB, false, false>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);           \
         }                                                                                                             \
     } while (0)
+#ifndef FM_PIXW_SPLIT
+#define FM_PIXW_SPLIT 0  // 8 chain + 4 producer waves per tile (768 threads)
+#endif
+        if constexpr (FM_PIXW_SPLIT != 0) {
+            using G = px::PW<21, 8>;
+#define FM_PIXW_SPL(K, T)                                                                                              \
+    do {                                                                                                               \
+        (void)hipFuncSetAttribute((const void*)px::k_pixw<21, 8, K, T, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+        hipLaunchKernelGGL((px::k_pixw<21, 8, K, T, true, 4>), grid, dim3(768), G::dyn_bytes, st, a);                 \
+    } while (0)
+            if (keep && tail) FM_PIXW_SPL(true, true);
+            else if (keep) FM_PIXW_SPL(true, false);
+            else if (tail) FM_PIXW_SPL(false, true);
+            else FM_PIXW_SPL(false, false);
+#undef FM_PIXW_SPL
+            return hipGetLastError();
+        }
         if (FM_PIXW_TALL && a.nty >= 4 && a.ntiles * a.S >= 2048) {
             const dim3 tgrid(a.ntx * ((a.h + 127) / 128), a.S);
             FM_PIXW_LAUNCH(16, tgrid);

@@ -20,4 +20,13 @@ for var in prod splL; do
   FM_HIP_LIB=$PWD/abvar/$var/libfm_hip.so timeout -k 10 200 python bench.py --streams 8 --batch 128 --steps 20 --warmup 5 $J > gpurun_out/ab_${TAG}_c2_${var}.log 2>&1 || { tail -20 gpurun_out/ab_${TAG}_c2_${var}.log; exit 1; }
   v gpurun_out/ab_${TAG}_c2_${var}.log "C2 $var"
 done
+FM_HIP_LIB=$PWD/abvar/pwspl/libfm_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -q -m gpu --timeout 400 --timeout-method thread -k "k21 or config5" > gpurun_out/parity_pwspl_$TAG.log 2>&1 || { tail -30 gpurun_out/parity_pwspl_$TAG.log; exit 1; }
+tail -1 gpurun_out/parity_pwspl_$TAG.log
+C5="--width 3840 --height 2160 --blur-scale 183 --streams 4 --batch 64 --ring 64 --ring-period 16 --steps 20 --warmup 10"
+for round in 1 2; do
+  for var in prod pwspl; do
+    FM_HIP_LIB=$PWD/abvar/$var/libfm_hip.so timeout -k 10 300 python bench.py $C5 $J > gpurun_out/ab_${TAG}_c5_${var}_$round.log 2>&1 || { tail -20 gpurun_out/ab_${TAG}_c5_${var}_$round.log; exit 1; }
+    v gpurun_out/ab_${TAG}_c5_${var}_$round.log "C5 $var r$round"
+  done
+done
 echo "done $TAG"
