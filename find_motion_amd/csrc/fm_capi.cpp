@@ -548,7 +548,10 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         for (int i = 0; i < c->nccl; i++) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
-    if (cu_split) HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()));
+#ifndef FM_CU_RS_ALL
+#define FM_CU_RS_ALL 0  // 1: the input stream keeps every CU (only the pixel stream is masked)
+#endif
+    if (cu_split && !FM_CU_RS_ALL) HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()));
     else if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
