@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, call z: mode D with the input stream on every CU (only the pixel stream masked to its 8) vs
-# the product (input stream on the other 248).
+# the product (input stream on the other 248); then the bounds-checked build (VARIANT=checked) through the
+# parity, configuration and JPEG suites.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,4 +14,6 @@ for round in 1 2 3; do
     v gpurun_out/ab_${TAG}_D_${var}_$round.log "D $var r$round"
   done
 done
+FM_HIP_LIB=$PWD/find_motion_amd/libfm_hip_checked.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_jpeg.py -x -q -m gpu --timeout 400 --timeout-method thread > gpurun_out/parity_checked_$TAG.log 2>&1 || { tail -30 gpurun_out/parity_checked_$TAG.log; exit 1; }
+tail -1 gpurun_out/parity_checked_$TAG.log
 echo "done $TAG"
