@@ -549,7 +549,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
 #ifndef FM_CU_RS_ALL
-#define FM_CU_RS_ALL 0  // 1: the input stream keeps every CU (only the pixel stream is masked)
+#define FM_CU_RS_ALL 1  // the input stream keeps every CU, only the pixel stream is masked (mode D 609 -> 651 k; 0: the other 248)
 #endif
     if (cu_split && !FM_CU_RS_ALL) HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()));
     else if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
