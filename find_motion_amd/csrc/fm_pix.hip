@@ -1023,6 +1023,10 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool cw = !SPL || wv < 8;  // SPL: a chain wave (0-7) or a producer (8-15: pw = wv - 8)
     const int pw = wv - 8, ptid = tid - 512;
+#ifndef FM_P5_SPL_PRIO
+#define FM_P5_SPL_PRIO 0  // SPL: issue priority of the (latency-bound) small-image waves over the resize's beside them
+#endif
+    if constexpr (SPL && FM_P5_SPL_PRIO > 0) __builtin_amdgcn_s_setprio(FM_P5_SPL_PRIO);
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
     int ti, tx, y0, wb0;  // contour tile, its column, the band's first row, its first 8-row slice of the tile
