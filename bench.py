@@ -95,17 +95,24 @@ def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | 
     return int(k["traffic_bytes"]), e.get("source"), k.get("sq")
 
 
-def config_name(S: int, W: int, H: int, mode: str, k: int, haar: bool = False) -> str:
+def config_name(S: int, W: int, H: int, mode: str, k: int, haar: bool = False, world: int = 1) -> str:
     """Which BASELINE.json config the run's shape is (configs[1] is the headline; the others are the parity
-    configurations run at their quoted perf shapes), so a line is never filed under the wrong one."""
+    configurations run at their quoted perf shapes), so a line is never filed under the wrong one.  S is
+    streams per GPU, world the number of ranks (one GPU each): 8 streams per GPU on 8 GPUs is configs[3]
+    (64 x 1080p sharded 8 per GPU, find_motion.py:1054-1122)."""
+    md = "" if mode == "F" else " (mode D)"
     if (W, H) == (1920, 1080):
         if S == 1:
-            return "configs[1]" if mode == "F" else "configs[1] (mode D)"
+            return ("configs[1]" if world == 1 else f"configs[1] x {world} GPUs") + md
         if S == 8:
-            return "configs[2]" if mode == "F" else "configs[2] (mode D)"
-        return f"{S} x 1080p streams (configs[2]/[3] family)"
+            if world == 1:
+                return "configs[2]" + md
+            if world == 8:
+                return "configs[3]" + md
+            return f"configs[3] family: 8 streams per GPU x {world} GPUs" + md
+        return f"{S} x 1080p streams per GPU x {world} GPU(s) (configs[2]/[3] family)" + md
     if (W, H) == (3840, 2160) and k == 21:
-        return "configs[4]" if haar else "configs[4] geometry (no Haar stage)"
+        return ("configs[4]" if haar else "configs[4] geometry (no Haar stage)") + ("" if world == 1 else f" x {world} GPUs")
     return "custom shape"
 
 
@@ -264,6 +271,233 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+def synthetic_ring(W: int, H: int, S: int, R: int, P: int, streams: list, local: int):
+    """Host frames [P][S][H][W][3] (the ring's distinct synthetic frames, generated on a thread pool: each
+    frame is independent of the others) and the device ring [R][S][H][W][3], slot t holding frame t % P."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from find_motion_amd.synthetic import SyntheticVideo
+    vids = [SyntheticVideo(W, H, stream=g) for g in streams]
+    host = np.empty((P, S, H, W, 3), np.uint8)
+
+    def gen(i: int) -> None:
+        host[i // S, i % S] = vids[i % S].frame(i // S)
+
+    with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:
+        list(ex.map(gen, range(P * S)))
+    uniq = torch.from_numpy(host).to(f"cuda:{local}")
+    ring = torch.empty((R, S, H, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
+    for t in range(R):
+        ring[t].copy_(uniq[t % P])
+    del uniq
+    return host, ring
+
+
+def roofline_of(ktimes: dict, cfg: dict, ms_per_step: float) -> dict | None:
+    """Roofline of the dominant kernel from the engine's per-kernel times (every pixel / resize launch
+    timed by in-kernel stamps: first workgroup's start to last wave's end).  In mode D the dominant
+    kernel is the INTER_AREA resize, the one kernel there that streams whole frames (the pixel kernel's
+    100 x 56 work image is two tiles: latency, not bandwidth)."""
+    dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+    for rk in ("resize_area", "resize_area_fast"):
+        if rk in ktimes and ktimes[rk][1] > 0:
+            dom = rk
+    if dom is None:
+        return None
+    ms, n = ktimes[dom]
+    avg_s = ms / 1e3 / max(n, 1)
+    nbytes = algorithmic_bytes(dom, cfg)
+    if nbytes is None or avg_s <= 0:
+        return None
+    ach = nbytes / avg_s / 1e9
+    traffic, tsrc, sq = pmc_traffic(dom, cfg)
+    # "bound" is the roofline the kernel is priced against (byte/integer stencils + an f64
+    # recurrence: no contraction, no MFMA).  What actually limits it is read from the SQ
+    # counters of the committed profile: "limiter" below.
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": int(n),
+            "timing": "every launch of the timed steps, in-kernel s_memrealtime stamps (first workgroup start, "
+                      "last wave end; 100 MHz)",
+            # the launches of one stream are serialised, so each is at most a step: a larger figure is a
+            # timing fault, never a kernel fraction
+            "launch_le_step": bool(avg_s * 1e3 <= ms_per_step * (1 + 1e-6))}
+    if not roof["launch_le_step"]:
+        print(f"[bench] WARNING: {dom} averages {avg_s * 1e6:.1f} us per launch, more than the "
+              f"{ms_per_step * 1e3:.1f} us step", file=sys.stderr)
+    mv = moved_bytes(dom, cfg)
+    if mv is not None:  # the same launches priced on the bytes the kernel must move as built
+        roof["moved_bytes_per_launch"] = int(mv)
+        roof["frac_moved"] = round(mv / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+    if traffic is not None:
+        roof["traffic_source"] = f"{tsrc}: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 16-B read correction)"
+    if sq:
+        roof["limiter"] = (f"issue and latency, not HBM bandwidth: of SQ_WAVE_CYCLES, {sq['wait_inst_any_frac']:.0%} "
+                           f"issue stalls (SQ_WAIT_INST_ANY), {sq['wait_any_frac']:.0%} parked on s_waitcnt / the "
+                           f"frame barrier (SQ_WAIT_ANY), {sq['active_inst_any_frac']:.0%} issuing; "
+                           f"{sq['valu_insts'] / 1e6:.1f}M VALU, {sq['salu_insts'] / 1e6:.1f}M SALU, "
+                           f"{sq['lds_insts'] / 1e6:.1f}M LDS wave-instructions per launch ({tsrc})")
+    return roof
+
+
+def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local: int, active: bool, backend: str,
+            haar: bool = False, masks: bool = False, ring_frames: int | None = None) -> dict:
+    """One workload: S streams per GPU of synthetic frames in a device-resident ring, `warmup` untimed then
+    `steps` timed steps (one step = one batch of T frames per stream submitted and one completed), the
+    barrier + synchronize on both sides, max over ranks.  Returns the line's figures and the live engine."""
+    import torch
+
+    from find_motion_amd import MotionEngine, dist, make_gaussian, work_height
+    world = pl.world
+    W, H = args.width, args.height
+    box, blur_scale = (W, W // 5) if mode == "F" else (100, 20)
+    if mode == "F" and W == 1920:
+        blur_scale = 384
+    if args.blur_scale is not None:
+        blur_scale = args.blur_scale
+    k = make_gaussian(box, blur_scale)
+    ring_frames = args.ring if ring_frames is None else ring_frames
+    R = max(ring_frames - ring_frames % T, T)
+    cfg = {"workload": f"{config_name(S, W, H, mode, k, haar, world)}: {S}x{W}x{H} stream(s) per GPU, mode {mode} "
+                       f"(-B {box} -b {blur_scale}, k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
+                       + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
+           "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
+           "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
+
+    # synthetic ring [R][S][H][W][3] on the device, distinct streams per rank (stream s -> rank s // S):
+    # ring slot t holds synthetic frame t % P; only the P distinct frames exist on the host (at 8 streams a
+    # host copy of the whole ring would be 12.7 GB per rank)
+    P = max(1, min(args.ring_period, R))
+    host, ring = synthetic_ring(W, H, S, R, P, dist.rank_streams(pl, S), local)
+    frame_bytes = S * H * W * 3
+
+    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
+                       max_batch=T, max_contours=1 << 14,
+                       profile=False if args.no_ktimes else True if args.all_ktimes else "pix", device=local)
+    footprint = dict(eng.footprint(), ring_bytes=R * frame_bytes)
+    if masks or haar:  # mask_off_areas (fm.py:611-636): rasterised once, applied in the pixel kernel
+        from find_motion_amd import rasterize_masks
+        keep = rasterize_masks(cfg["h"], cfg["w"], box / W, CONFIG5_MASKS)
+        for s in range(S):
+            eng.set_mask(s, keep)
+        cfg["masks"] = [list(map(list, m)) for m in CONFIG5_MASKS]
+    base = ring.data_ptr()
+    n_batches = R // T
+
+    # Pipelined like a live decoder feeding the engine: up to max_inflight batches are
+    # submitted before the oldest one's results are collected, so the contour passes
+    # of consecutive batches overlap each other and the next pixel kernels.  A step =
+    # one batch submitted + one batch completed; all timed batches are submitted and
+    # completed inside the timed region.
+    depth = eng.max_inflight
+
+    def submit(i: int) -> None:
+        eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
+
+    ccl = {"heavy_tiles": 0, "shared_nodes_max": 0, "fallback_frames": 0, "batches": 0}
+
+    # configs[4]'s object-ROI stage: the frames find_objects hands to the cascade, gathered from the ring
+    # (still in HBM) after each waited batch and detected in one call (INTER_AREA to 300 px + detectMultiScale)
+    det, sel = None, [RoiSelector() for _ in range(S)]
+    hs = {"calls": 0, "roi_frames": 0, "detections": 0, "wall_s": 0.0, "device_ms": 0.0}
+    if haar:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from golden_cases import load_frontalface  # the reference's cascade, as committed fixture arrays
+
+        from find_motion_amd import CascadeClassifier
+        det = CascadeClassifier(load_frontalface()[0], device=local)
+
+    def objects(i: int) -> None:
+        cnt = eng.counts()
+        base_t = (i % n_batches) * T
+        pick = [(t, s) for t in range(T) for s in range(S) if sel[s].step(int(cnt[t, s]))]
+        if not pick:
+            return
+        t0 = time.perf_counter()
+        # the ROI frames where they lie in the ring (written before the timed region): no gather copy
+        found = det.detect_frame_list([ring[base_t + t, s].data_ptr() for t, s in pick], H, W, 300, 1.1, 5)
+        hs["wall_s"] += time.perf_counter() - t0
+        hs["device_ms"] += det.last_ms()
+        hs["calls"] += 1
+        hs["roi_frames"] += len(pick)
+        hs["detections"] += sum(len(f) for f in found)
+
+    def run(first: int, n: int) -> None:
+        for i in range(min(depth, n)):
+            submit(first + i)
+        for i in range(n):
+            eng.wait()  # completes batch i and frees its slot
+            if det is not None:
+                objects(first + i)
+            st = eng.ccl_stats()  # two mapped-memory words: no device sync
+            ccl["heavy_tiles"] += st["heavy_tiles"]
+            ccl["shared_nodes_max"] = max(ccl["shared_nodes_max"], st["shared_nodes"])
+            ccl["fallback_frames"] += eng.fallbacks()
+            ccl["batches"] += 1
+            if i + depth < n:
+                submit(first + i + depth)
+
+    run(0, warmup)
+    eng.reset_kernel_times()
+    ccl.update(heavy_tiles=0, shared_nodes_max=0, fallback_frames=0, batches=0)
+
+    dist.barrier(active)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hs.update(calls=0, roi_frames=0, detections=0, wall_s=0.0, device_ms=0.0)
+    run(warmup, steps)
+    torch.cuda.synchronize()
+    dist.barrier(active)
+    wall = time.perf_counter() - t0
+    elapsed = dist.max_over_ranks(wall, active, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+    if det is not None:
+        det.close()
+
+    ktimes = eng.kernel_times()
+    total_frames = world * S * T * steps
+    ms_per_step = 1e3 * elapsed / steps
+    kernels = {name: {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3)}
+               for name, (ms, n) in ktimes.items()}
+    del ring
+    return {"cfg": cfg, "eng": eng, "host": host, "P": P, "wall": wall, "elapsed": elapsed,
+            "value": total_frames / elapsed, "ms_per_step": ms_per_step,
+            "roofline": roofline_of(ktimes, cfg, ms_per_step), "kernels": kernels, "haar": hs, "det": det,
+            "footprint": footprint, "ccl": ccl}
+
+
+def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, backend: str) -> dict:
+    """A compact figure of another configuration for the same JSON line (mode D, the reference CLI's
+    default -B 100; configs[2], 8 streams per GPU): value, step time, its own roofline."""
+    steps, warmup = max(5, min(args.steps, 20)), max(2, min(args.warmup, 5))
+    leg = run_leg(args, mode, S, T, steps, warmup, pl, local, active, backend)
+    leg["eng"].close()
+    out = {"workload": leg["cfg"]["workload"], "value": round(leg["value"], 2), "unit": "frames/s",
+           "steps": steps, "warmup": warmup, "ms_per_step": round(leg["ms_per_step"], 4), "roofline": leg["roofline"],
+           "kernels": leg["kernels"], "path_hbm_frac": round(leg["value"] / pl.world * path_bytes_per_frame(leg["cfg"])
+                                                            / 1e9 / HBM_PEAK_GBS, 4)}
+    del leg
+    import torch
+    torch.cuda.empty_cache()
+    return out
+
+
+def rank_devices(local: int, pl, active: bool) -> list:
+    """[{rank, device, pci_bus_id, name}] of every rank, gathered on rank 0 through the process group (so
+    the line records how many ranks the group really held and which device each ran on)."""
+    import torch
+
+    from find_motion_amd import dist
+    pr = torch.cuda.get_device_properties(local)
+    bus = None
+    if getattr(pr, "pci_bus_id", None) is not None:
+        bus = f"{getattr(pr, 'pci_domain_id', 0):04x}:{pr.pci_bus_id:02x}:{getattr(pr, 'pci_device_id', 0):02x}"
+    me = {"rank": pl.rank, "device": local, "pci_bus_id": bus, "name": pr.name,
+          "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+    return dist.gather_to_root(me, pl, active) or []
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -297,6 +531,8 @@ def main() -> None:
     ap.add_argument("--haar", action="store_true",
                     help="configs[4]: run the reference's frontalface_default cascade on every 15th written frame "
                          "of each stream (find_objects, fm.py:549-575, 703-731) inside the timed steps")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the mode D and configs[2] figures the default (1-GPU, configs[1]) line carries")
     ap.add_argument("--all-ktimes", action="store_true",
                     help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
@@ -320,160 +556,12 @@ def main() -> None:
     torch.cuda.set_device(local)
     active = dist.init(pl, backend, torch.device("cuda", local))
 
-    from find_motion_amd import MotionEngine, make_gaussian, work_height
-    from find_motion_amd.synthetic import SyntheticVideo
-
-    W, H = args.width, args.height
-    box, blur_scale = (W, W // 5) if args.mode == "F" else (100, 20)
-    if args.mode == "F" and W == 1920:
-        blur_scale = 384
-    if args.blur_scale is not None:
-        blur_scale = args.blur_scale
-    k = make_gaussian(box, blur_scale)
-    S, T = args.streams, args.batch
-    R = max(args.ring - args.ring % T, T)
-    cfg = {"workload": f"{config_name(S, W, H, args.mode, k, args.haar)}: {S}x{W}x{H} stream(s) per GPU, mode {args.mode} (-B {box} -b {blur_scale}, "
-                       f"k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
-                       + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
-           "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
-           "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
-
-    # synthetic ring [R][S][H][W][3] on the device, distinct streams per rank (stream s -> rank s // S):
-    # ring slot t holds synthetic frame t % P; only the P distinct frames exist on the host (at 8 streams a
-    # host copy of the whole ring would be 12.7 GB per rank)
-    P = max(1, min(args.ring_period, R))
-    vids = [SyntheticVideo(W, H, stream=g) for g in dist.rank_streams(pl, S)]
-    host = np.empty((P, S, H, W, 3), np.uint8)
-    for t in range(P):
-        for s in range(S):
-            host[t, s] = vids[s].frame(t)
-    uniq = torch.from_numpy(host).to(f"cuda:{local}")
-    ring = torch.empty((R, S, H, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
-    for t in range(R):
-        ring[t].copy_(uniq[t % P])
-    del uniq
-    frame_bytes = S * H * W * 3
-
-    eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1,
-                       max_batch=T, max_contours=1 << 14, profile=False if args.no_ktimes else True if args.all_ktimes else "pix", device=local)
-    footprint = dict(eng.footprint(), ring_bytes=R * frame_bytes)
-    if args.masks or args.haar:  # mask_off_areas (fm.py:611-636): rasterised once, applied in the pixel kernel
-        from find_motion_amd import rasterize_masks
-        keep = rasterize_masks(cfg["h"], cfg["w"], box / W, CONFIG5_MASKS)
-        for s in range(S):
-            eng.set_mask(s, keep)
-        cfg["masks"] = [list(map(list, m)) for m in CONFIG5_MASKS]
-    base = ring.data_ptr()
-    n_batches = R // T
-
-    # Pipelined like a live decoder feeding the engine: up to max_inflight batches are
-    # submitted before the oldest one's results are collected, so the contour passes
-    # of consecutive batches overlap each other and the next pixel kernels.  A step =
-    # one batch submitted + one batch completed; all timed batches are submitted and
-    # completed inside the timed region.
-    depth = eng.max_inflight
-
-    def submit(i: int) -> None:
-        eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
-
-    ccl = {"heavy_tiles": 0, "shared_nodes_max": 0, "fallback_frames": 0, "batches": 0}
-
-    # configs[4]'s object-ROI stage: the frames find_objects hands to the cascade, gathered from the ring
-    # (still in HBM) after each waited batch and detected in one call (INTER_AREA to 300 px + detectMultiScale)
-    det, sel = None, [RoiSelector() for _ in range(S)]
-    haar = {"calls": 0, "roi_frames": 0, "detections": 0, "wall_s": 0.0, "device_ms": 0.0}
-    if args.haar:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from golden_cases import load_frontalface  # the reference's cascade, as committed fixture arrays
-
-        from find_motion_amd import CascadeClassifier
-        det = CascadeClassifier(load_frontalface()[0], device=local)
-
-    def objects(i: int) -> None:
-        cnt = eng.counts()
-        base_t = (i % n_batches) * T
-        pick = [(t, s) for t in range(T) for s in range(S) if sel[s].step(int(cnt[t, s]))]
-        if not pick:
-            return
-        t0 = time.perf_counter()
-        # the ROI frames where they lie in the ring (written before the timed region): no gather copy
-        found = det.detect_frame_list([ring[base_t + t, s].data_ptr() for t, s in pick], H, W, 300, 1.1, 5)
-        haar["wall_s"] += time.perf_counter() - t0
-        haar["device_ms"] += det.last_ms()
-        haar["calls"] += 1
-        haar["roi_frames"] += len(pick)
-        haar["detections"] += sum(len(f) for f in found)
-
-    def run(first: int, n: int) -> None:
-        for i in range(min(depth, n)):
-            submit(first + i)
-        for i in range(n):
-            eng.wait()  # completes batch i and frees its slot
-            if det is not None:
-                objects(first + i)
-            st = eng.ccl_stats()  # two mapped-memory words: no device sync
-            ccl["heavy_tiles"] += st["heavy_tiles"]
-            ccl["shared_nodes_max"] = max(ccl["shared_nodes_max"], st["shared_nodes"])
-            ccl["fallback_frames"] += eng.fallbacks()
-            ccl["batches"] += 1
-            if i + depth < n:
-                submit(first + i + depth)
-
-    run(0, args.warmup)
-    eng.reset_kernel_times()
-    ccl.update(heavy_tiles=0, shared_nodes_max=0, fallback_frames=0, batches=0)
-
-    dist.barrier(active)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    haar.update(calls=0, roi_frames=0, detections=0, wall_s=0.0, device_ms=0.0)
-    run(args.warmup, args.steps)
-    torch.cuda.synchronize()
-    dist.barrier(active)
-    wall = time.perf_counter() - t0
-    elapsed = dist.max_over_ranks(wall, active, device=f"cuda:{local}" if backend == "nccl" else "cpu")
-    if det is not None:
-        det.close()
-
-    ktimes = eng.kernel_times()
-    total_frames = world * S * T * args.steps
-    value = total_frames / elapsed
-
-    # roofline of the dominant kernel; in mode D the INTER_AREA resize, the one kernel there that streams
-    # whole frames (the pixel kernel's 100 x 56 work image is two tiles: latency, not bandwidth)
-    dom = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
-    for rk in ("resize_area", "resize_area_fast"):
-        if rk in ktimes and ktimes[rk][1] > 0:
-            dom = rk
-    roof = None
-    kernels = {}
-    for name, (ms, n) in ktimes.items():
-        kernels[name] = {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3)}
-    if dom is not None:
-        ms, n = ktimes[dom]
-        avg_s = ms / 1e3 / max(n, 1)
-        nbytes = algorithmic_bytes(dom, cfg)
-        if nbytes is not None and avg_s > 0:
-            ach = nbytes / avg_s / 1e9
-            traffic, tsrc, sq = pmc_traffic(dom, cfg)
-            # "bound" is the roofline the kernel is priced against (byte/integer stencils + an f64
-            # recurrence: no contraction, no MFMA).  What actually limits it is read from the SQ
-            # counters of the committed profile: "limiter" below.
-            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3)}
-            mv = moved_bytes(dom, cfg)
-            if mv is not None:  # the same launches priced on the bytes the kernel must move as built
-                roof["moved_bytes_per_launch"] = int(mv)
-                roof["frac_moved"] = round(mv / avg_s / 1e9 / HBM_PEAK_GBS, 4)
-            if traffic is not None:
-                roof["traffic_source"] = f"{tsrc}: 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 16-B read correction)"
-            if sq:
-                roof["limiter"] = (f"issue and latency, not HBM bandwidth: of SQ_WAVE_CYCLES, {sq['wait_inst_any_frac']:.0%} "
-                                   f"issue stalls (SQ_WAIT_INST_ANY), {sq['wait_any_frac']:.0%} parked on s_waitcnt / the "
-                                   f"frame barrier (SQ_WAIT_ANY), {sq['active_inst_any_frac']:.0%} issuing; "
-                                   f"{sq['valu_insts'] / 1e6:.1f}M VALU, {sq['salu_insts'] / 1e6:.1f}M SALU, "
-                                   f"{sq['lds_insts'] / 1e6:.1f}M LDS wave-instructions per launch ({tsrc})")
+    leg = run_leg(args, args.mode, args.streams, args.batch, args.steps, args.warmup, pl, local, active, backend,
+                  haar=args.haar, masks=args.masks)
+    cfg, eng, host, P, wall, elapsed = leg["cfg"], leg["eng"], leg["host"], leg["P"], leg["wall"], leg["elapsed"]
+    S, T, W, H = cfg["streams_per_gpu"], cfg["frames_per_step"], cfg["W"], cfg["H"]
+    value, roof, kernels, haar, det = leg["value"], leg["roofline"], leg["kernels"], leg["haar"], leg["det"]
+    footprint, ccl, depth = leg["footprint"], leg["ccl"], eng.max_inflight
 
     # measured device copy peak (for reference beside the spec)
     try:
@@ -570,16 +658,29 @@ def main() -> None:
     if not args.no_mjpeg and world == 1:  # a per-GPU figure: measured in the 1-GPU run only
         mjpeg = mjpeg_fed(eng, host, T, S)
 
+    eng.close()
+    ranks = rank_devices(local, pl, active)  # (collective: every rank)
+
+    # Side configurations in the same line (per-GPU figures, the 1-GPU run only, after the headline's
+    # timed steps): mode D (-B 100 -b 20, the reference CLI's default, find_motion.py:1474) and configs[2]
+    # (8 x 1080p streams batched on one GPU), each with its own roofline
+    side = None
+    default_shape = args.mode == "F" and S == 1 and (W, H) == (1920, 1080) and not args.haar
+    if world == 1 and default_shape and not args.no_side:
+        side = {"mode_d": side_leg(args, "D", 1, args.batch, pl, local, active, backend),
+                "configs2": side_leg(args, "F", 8, 128, pl, local, active, backend)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, host.reshape(P * S, H, W, 3), min(args.cpu_frames, P * S))
 
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(leg["ms_per_step"], 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
-               "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "host_fed_per_gpu": host_fed,
+               "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "side_configs": side,
+               "ranks": {"world_size_seen": dist.world_size(active), "devices": ranks}, "host_fed_per_gpu": host_fed,
                "mjpeg_fed_per_gpu": mjpeg, "footprint_per_gpu": footprint,
                "hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                "haar_stage": None if det is None else {
@@ -596,7 +697,6 @@ def main() -> None:
                                 "shared_nodes_max": ccl["shared_nodes_max"],
                                 "fallback_frames": ccl["fallback_frames"]}}
         print(json.dumps(out), flush=True)
-    eng.close()
     dist.finalize(active)
 
 

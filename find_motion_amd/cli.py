@@ -287,9 +287,30 @@ def run(args: Namespace, print_help: typing.Callable = lambda: None) -> list:
     return results
 
 
+def hw_queues_from_env(env=None) -> tuple:
+    """(count, force) for use_hw_queues: FM_HW_QUEUES, when set, is validated (1..32, HIP's accepted range)
+    and forced over any GPU_MAX_HW_QUEUES; otherwise an exported GPU_MAX_HW_QUEUES is honoured and 8 is
+    the default (with HIP's 4 the input stream shares an in-order queue with a contour stream)."""
+    env = os.environ if env is None else env
+    v = env.get("FM_HW_QUEUES")
+    if v is None:
+        return 8, False
+    try:
+        n = int(v)
+    except ValueError:
+        raise SystemExit(f"FM_HW_QUEUES={v!r}: expected an integer in 1..32") from None
+    if not 1 <= n <= 32:
+        raise SystemExit(f"FM_HW_QUEUES={n}: expected an integer in 1..32")
+    return n, True
+
+
 def main(argv=None) -> None:
     from . import use_hw_queues
-    use_hw_queues(int(os.environ.get("FM_HW_QUEUES", "8")), force=True)  # before any HIP call (inherited by --gpus workers)
+    n, force = hw_queues_from_env()
+    use_hw_queues(n, force=force)  # before any HIP call (inherited by --gpus workers)
+    if int(os.environ["GPU_MAX_HW_QUEUES"]) < 8:
+        log.info("GPU_MAX_HW_QUEUES=%s from the environment (FM_HW_QUEUES=8 gives each pipeline stream its own "
+                 "hardware queue)", os.environ["GPU_MAX_HW_QUEUES"])
     parser = ArgumentParser(description="Find motion and objects in video (MI355X)")
     get_args(parser)
     args = parser.parse_args(argv)

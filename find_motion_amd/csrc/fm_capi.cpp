@@ -5,6 +5,7 @@
 // taps, fixed-point Gaussian taps) once at fm_create, and sequences the
 // kernels of fm_kernels.hip on one HIP stream per context.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -12,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "fm_internal.h"
@@ -66,7 +68,7 @@ struct BatchSlot {
     int32_t* h_rec = nullptr;       // mapped pinned [F][cap][5], written by the kernels
     int32_t* d_rec = nullptr;       // device alias of h_rec
     uint8_t* h_init = nullptr;      // pinned [S]
-    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr, ev_lab = nullptr, ev_mrg = nullptr;  // labelling / merge done
+    hipEvent_t ev_pix = nullptr, ev_done = nullptr, ev_rs = nullptr, ev_lab = nullptr;  // (ev_lab: labelling done)
     hipStream_t ccl_stream = nullptr;  // this slot's contour pass (slots' passes run concurrently)
     int n = 0;                      // frames in flight in this slot (0 = none)
     FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
@@ -87,9 +89,8 @@ struct fm_ctx {
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
     hipStream_t rs_stream = nullptr;  // input stream: host copies + resize, ahead of the pixel stream
     hipStream_t ccl_streams[kSlots] = {};
-    int lab_prev = -1;  // slot of the last batch whose labelling was enqueued (FM_CCL_GATE)
+    int lab_prev = -1;  // slot of the last batch whose labelling was enqueued (the labelling gate)
     int nccl = 1;
-    int ccl_next = 0;  // the next batch's contour stream
     KernelTimer timer;
 
     // device state shared by all batches
@@ -110,7 +111,8 @@ struct fm_ctx {
     int32_t* d_rec_all = nullptr;  // k_emit_all records of one frame [rec_all_cap][5] + counter
     size_t rec_all_cap = 0;
     int rec_cap = 0;          // records per frame in each slot's mapped buffer (the first fetch; more -> k_emit_all)
-    size_t dev_bytes = 0;     // fm_create's device allocations (fm_footprint)
+    size_t dev_bytes = 0;     // device bytes the context holds now (fm_footprint)
+    std::unordered_map<const void*, size_t> dev_sizes;  // (so that a freed buffer leaves dev_bytes)
     size_t pinned_bytes = 0;  // and its page-locked host allocations
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
@@ -143,6 +145,7 @@ struct fm_ctx {
     std::vector<double> ts_sum;   // summed phase deltas (cycles)
     std::vector<int64_t> ts_n;
     bool serial = false;  // FM_SERIAL: contour pass on the pixel stream (profiling: no overlap)
+    int cu_offset = -1;   // the pixel stream's CUs (small work images): i % 32 == cu_offset; -1: every CU
     int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of k_fused (results invalid)
 };
 
@@ -251,7 +254,10 @@ int dalloc(fm_ctx* c, T** p, size_t count) {
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void**)p, count * sizeof(T));
     if (e != hipSuccess) return fail(c, FM_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
-    if (c) c->dev_bytes += count * sizeof(T);
+    if (c) {
+        c->dev_bytes += count * sizeof(T);
+        c->dev_sizes[*p] = count * sizeof(T);
+    }
     return FM_OK;
 }
 
@@ -267,6 +273,18 @@ template <class T>
 void dfree(T*& p) {
     if (p) (void)hipFree(p);
     p = nullptr;
+}
+// a buffer freed while the context lives on (re-grown): its bytes leave the footprint
+template <class T>
+void dfree(fm_ctx* c, T*& p) {
+    if (p) {
+        auto it = c->dev_sizes.find(p);
+        if (it != c->dev_sizes.end()) {
+            c->dev_bytes -= it->second;
+            c->dev_sizes.erase(it);
+        }
+    }
+    dfree(p);
 }
 
 int check_idle(fm_ctx* c) {
@@ -286,7 +304,7 @@ int check_frame(fm_ctx* c, int frame, int stream, bool device_data) {
 // every record of frame f of a finished fused-path batch (count known from k_emit)
 int emit_all(fm_ctx* c, BatchSlot& B, size_t f, int count, std::vector<int32_t>& out) {
     if ((size_t)count > c->rec_all_cap) {
-        dfree(c->d_rec_all);
+        dfree(c, c->d_rec_all);
         c->rec_all_cap = 0;
         if (int rc = dalloc(c, &c->d_rec_all, (size_t)count * 5 + 1)) return rc;
         c->rec_all_cap = (size_t)count;
@@ -331,7 +349,7 @@ int relabel_frame(fm_ctx* c, BatchSlot& B, size_t f, std::vector<int32_t>& out, 
             HIP_TRY(c, hipStreamSynchronize(st));
             return FM_OK;
         }
-        dfree(c->d_rec_one);
+        dfree(c, c->d_rec_one);
         c->rec_one_cap = 0;
         if (int rc = dalloc(c, &c->d_rec_one, (size_t)n * 5)) return rc;
         c->rec_one_cap = (size_t)n;
@@ -352,7 +370,7 @@ int contour_areas(fm_ctx* c, BatchSlot& B, size_t F) {
     const size_t n = jobs.size() / 3;
     if (n == 0) return FM_OK;
     if (n > c->area_cap) {
-        dfree(c->d_area);
+        dfree(c, c->d_area);
         c->area_cap = 0;
         if (int rc = dalloc(c, &c->d_area, n * 4)) return rc;
         c->area_cap = n;
@@ -380,22 +398,22 @@ int contour_areas(fm_ctx* c, BatchSlot& B, size_t F) {
 // ---------------------------------------------------------------------------
 // KernelTimer
 namespace fm {
+int KernelTimer::id_of(const char* name) {
+    for (size_t i = 0; i < names.size(); i++)
+        if (names[i] == name || std::strcmp(names[i], name) == 0) return (int)i;
+    names.push_back(name);
+    ms.push_back(0);
+    launches.push_back(0);
+    calls.push_back(0);
+    return (int)names.size() - 1;
+}
 int KernelTimer::begin(const char* name, hipStream_t st) {
     if (!enabled) return -1;
     if (!st) st = stream;
     if (pixel_only && st != stream && st != stream2) return -1;
-    int id = -1;
-    for (size_t i = 0; i < names.size(); i++)
-        if (names[i] == name || std::strcmp(names[i], name) == 0) id = (int)i;
-    if (id < 0) {
-        names.push_back(name);
-        ms.push_back(0);
-        launches.push_back(0);
-        calls.push_back(0);
-        id = (int)names.size() - 1;
-    }
+    const int id = id_of(name);
     // events on every launch cost the pipeline ~7% (each record is a barrier packet):
-    // the pixel-only mode times a sample of the launches
+    // the pixel-only mode times a sample of the launches of the kernels it cannot stamp
     if (pixel_only && calls[id]++ % kSample != 0) return -1;
     hipEvent_t a, b;
     if (pool.size() >= 2) {
@@ -429,12 +447,58 @@ void KernelTimer::collect() {
     }
     pending.swap(keep);
 }
+// Stamped launches (pixel-only mode): the round-4 sampled events opened their window at the marker
+// ahead of the kernel, so it took in the queue's waits, and one launch in four was a biased sample
+// (a sampled mean of 709 us against a 655.5 us step).  Stamps time every launch from its first
+// workgroup's start to its last wave's end.
+uint64_t* KernelTimer::stamp(const char* name) {
+    if (!enabled || !pixel_only) return nullptr;
+    if (!d_stamps) {
+        if (hipMalloc(&d_stamps, sizeof(uint64_t) * 2 * kStampRing) != hipSuccess) {
+            d_stamps = nullptr;
+            enabled = false;
+            return nullptr;
+        }
+        std::vector<uint64_t> init(2 * kStampRing);
+        for (int i = 0; i < kStampRing; i++) init[2 * i] = ~0ull, init[2 * i + 1] = 0;
+        if (hipMemcpy(d_stamps, init.data(), init.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+            enabled = false;
+            return nullptr;
+        }
+    }
+    const int id = id_of(name);
+    if ((int)stamp_ids.size() >= kStampRing) {
+        unstamped++;
+        return nullptr;
+    }
+    stamp_ids.push_back(id);
+    return d_stamps + 2 * (stamp_ids.size() - 1);
+}
+int KernelTimer::fold_stamps() {
+    if (stamp_ids.empty()) return 0;
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (stream2) (void)hipStreamSynchronize(stream2);
+    const size_t n = stamp_ids.size();
+    std::vector<uint64_t> v(2 * n);
+    if (hipMemcpy(v.data(), d_stamps, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (size_t i = 0; i < n; i++) {
+        if (v[2 * i] == ~0ull || v[2 * i + 1] <= v[2 * i]) continue;  // (a kernel that does not stamp)
+        ms[stamp_ids[i]] += (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
+        launches[stamp_ids[i]] += 1;
+    }
+    for (size_t i = 0; i < n; i++) v[2 * i] = ~0ull, v[2 * i + 1] = 0;
+    stamp_ids.clear();
+    return hipMemcpy(d_stamps, v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
 void KernelTimer::reset() {
+    fold_stamps();  // (launches stamped before the reset are dropped with the sums below)
     std::fill(ms.begin(), ms.end(), 0.0);
     std::fill(launches.begin(), launches.end(), 0);
     std::fill(calls.begin(), calls.end(), 0);
+    unstamped = 0;
 }
 KernelTimer::~KernelTimer() {
+    if (d_stamps) (void)hipFree(d_stamps);
     for (auto& r : pending) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -496,31 +560,27 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     // the pixel kernel is a few workgroups whose frames run one after another (latency-bound), the
     // INTER_AREA resize of the next batch streams whole frames over every CU.  Sharing CUs, the resize
     // doubled the pixel launch (276 -> 540 us per 256 frames, profiles/r04rs_modeD); so the pixel
-    // stream gets 8 CUs of its own (one per 32) and the input stream the others.
-#ifndef FM_CU_SPLIT
-#define FM_CU_SPLIT 1
-#endif
+    // stream gets 8 CUs of its own, one in 32 (the input stream keeps every CU: mode D 609 -> 651 k,
+    // round 4; a masked input stream was slower whatever it left out).  Contexts sharing a device take
+    // different CUs: the set is CU i with i % 32 == k, k counting the contexts this process created on
+    // the device, offset by LOCAL_RANK (ranks rehearsed on one GPU), so two engines' pixel kernels do
+    // not queue on the same 8 CUs.
     const long long work_tiles = (long long)((c->w + 63) / 64) * ((c->h + 63) / 64) * p.n_streams;
-    bool cu_split = FM_CU_SPLIT && c->rmode != ResizeMode::Identity && work_tiles <= 16;
-    if (const char* e = dev_env("FM_CU_SPLIT")) cu_split = std::atoi(e) != 0 && c->rmode != ResizeMode::Identity && work_tiles <= 16;
-    std::vector<uint32_t> pix_mask, rs_mask;
+    bool cu_split = c->rmode != ResizeMode::Identity && work_tiles <= 16;
+    if (const char* e = dev_env("FM_CU_SPLIT")) cu_split = std::atoi(e) != 0 && cu_split;
+    std::vector<uint32_t> pix_mask;
     if (cu_split) {
         hipDeviceProp_t prop;
         HIP_TRY(cp, hipGetDeviceProperties(&prop, p.device));
         const int ncu = prop.multiProcessorCount;
         if (ncu >= 64) {
+            static std::atomic<int> split_ctx[64];
+            const char* lr = std::getenv("LOCAL_RANK");
+            const int k = (split_ctx[p.device & 63].fetch_add(1) + (lr ? std::atoi(lr) : 0)) & 31;
+            c->cu_offset = k;
             pix_mask.assign((ncu + 31) / 32, 0u);
-            rs_mask.assign((ncu + 31) / 32, 0u);
-#ifndef FM_CU_SPLIT_EVERY
-#define FM_CU_SPLIT_EVERY 32  // the pixel stream's CUs: one in FM_CU_SPLIT_EVERY
-#endif
-#ifndef FM_CU_RS_FROM
-#define FM_CU_RS_FROM 1  // the input stream's CUs: i % 32 >= FM_CU_RS_FROM of the others (1: all of them)
-#endif
-            for (int i = 0; i < ncu; i++) {
-                if (i % FM_CU_SPLIT_EVERY == 0) pix_mask[i / 32] |= 1u << (i % 32);
-                else if (i % 32 >= FM_CU_RS_FROM) rs_mask[i / 32] |= 1u << (i % 32);
-            }
+            for (int i = 0; i < ncu; i++)
+                if (i % 32 == k) pix_mask[i / 32] |= 1u << (i % 32);
         } else {
             cu_split = false;
         }
@@ -548,11 +608,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         for (int i = 0; i < c->nccl; i++) HIP_TRY(cp, hipStreamCreateWithFlags(&c->ccl_streams[i], hipStreamNonBlocking));
     HIP_TRY(cp, hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
     // input stream: host-to-device copies and the resize run here, ahead of the pixel stream
-#ifndef FM_CU_RS_ALL
-#define FM_CU_RS_ALL 1  // the input stream keeps every CU, only the pixel stream is masked (mode D 609 -> 651 k; 0: the other 248)
-#endif
-    if (cu_split && !FM_CU_RS_ALL) HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->rs_stream, (uint32_t)rs_mask.size(), rs_mask.data()));
-    else if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
+    if (!dev_env("FM_RESIZE_INLINE")) HIP_TRY(cp, hipStreamCreateWithFlags(&c->rs_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
     c->timer.enabled = (p.flags & (FM_FLAG_PROFILE | FM_FLAG_PROFILE_PIX)) != 0;
     c->timer.pixel_only = !(p.flags & FM_FLAG_PROFILE);
@@ -641,7 +697,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_rs, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_lab, hipEventDisableTiming));
-        HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_mrg, hipEventDisableTiming));
     }
     // pixel-level CCL: the whole batch on the v1 path, one frame for the fused path's overflow fallback
     const size_t ccl_px = c->use_fused ? c->work_plane : px;
@@ -733,7 +788,6 @@ void fm_destroy(fm_ctx* c) {
         if (b.ev_done) (void)hipEventDestroy(b.ev_done);
         if (b.ev_rs) (void)hipEventDestroy(b.ev_rs);
         if (b.ev_lab) (void)hipEventDestroy(b.ev_lab);
-        if (b.ev_mrg) (void)hipEventDestroy(b.ev_mrg);
     }
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_one); dfree(c->d_rec_all); dfree(c->d_area);
@@ -857,15 +911,17 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
     }
     const uint8_t* work = src;
     if (c->rmode == ResizeMode::General) {
-        int tok = c->timer.begin("resize_area", rs);
+        uint64_t* ks = c->timer.stamp("resize_area");
+        int tok = ks ? -1 : c->timer.begin("resize_area", rs);
         HIP_TRY(c, launch_resize_area(rs, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->d_xofs, c->d_xcnt,
-                                      c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt, c->d_ywt, c->ay.max_taps));
+                                      c->d_xwt, c->ax.max_taps, c->d_yofs, c->d_ycnt, c->d_ywt, c->ay.max_taps, nullptr, ks));
         c->timer.end(tok);
         work = B.d_work;
     } else if (c->rmode == ResizeMode::Fast) {
-        int tok = c->timer.begin("resize_area_fast", rs);
+        uint64_t* ks = c->timer.stamp("resize_area_fast");
+        int tok = ks ? -1 : c->timer.begin("resize_area_fast", rs);
         HIP_TRY(c, launch_resize_area_fast(rs, src, B.d_work, (int)F, c->p.src_h, c->p.src_w, c->h, c->w, c->fast_sx,
-                                           c->fast_sy));
+                                           c->fast_sy, ks));
         c->timer.end(tok);
         work = B.d_work;
     }
@@ -945,7 +1001,8 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
                 fp.bg_in = c->d_bg[c->bg_cur];
                 fp.bg_out = c->d_bg[c->bg_cur ^ 1];
                 if (!init) fp.init = nullptr;
-                int tok = c->timer.begin(name, ps);
+                fp.kstamp = c->timer.stamp(name);
+                int tok = fp.kstamp ? -1 : c->timer.begin(name, ps);
                 HIP_TRY(c, launch_pix(ps, fp, planes, init));
                 c->timer.end(tok);
                 c->bg_cur ^= 1;
@@ -966,30 +1023,17 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // consecutive batches on different contour streams: with 4 slots on 3 streams a fixed
         // slot -> stream map put every fourth pair of consecutive chains on one stream, one after
         // the other (the last batch's chain waited ≈130 µs for its predecessor's)
-#ifndef FM_CCL_GATE
-#define FM_CCL_GATE 1  // +1.5 % (388.1 vs 382.3 k, 4 alternating rounds, tools/r03_call4.sh)
-#endif
-#ifndef FM_MERGE_GATE
-#define FM_MERGE_GATE 0
-#endif
-#ifndef FM_CCL_ROTATE
-#define FM_CCL_ROTATE 0  // rotation: +2 % on one box, equal on another (369.9 vs 369.0 k, 5 rounds) with 8 % longer pixel launches: off
-#endif
-        if (FM_CCL_ROTATE) {
-            B.ccl_stream = c->ccl_streams[c->ccl_next];
-            c->ccl_next = (c->ccl_next + 1) % c->nccl;
-        }
+        // (Batches taking the contour streams in turn instead of the fixed slot map: +2 % on one box,
+        // equal on another with 8 % longer pixel launches, round 3.)
         hipStream_t cs = c->serial ? ps : B.ccl_stream;
         HIP_TRY(c, hipEventRecord(B.ev_pix, ps));
         HIP_TRY(c, hipStreamWaitEvent(cs, B.ev_pix, 0));
-        // FM_CCL_GATE: one batch's labelling kernel at a time (the previous batch's, on another contour
+        // the labelling gate: one batch's labelling kernel at a time (the previous batch's, on another contour
         // stream, is waited for), so the labelling of consecutive chains never bunches beside a pixel launch
+        // (+1.5 %, 388.1 vs 382.3 k, 4 alternating rounds, round 3)
         hipEvent_t gate_wait = nullptr;
-        if (FM_CCL_GATE && !c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
-        hipEvent_t mgate_wait = nullptr;  // FM_MERGE_GATE: the merge kernels likewise
-        if (FM_MERGE_GATE && !c->serial && c->lab_prev >= 0 && c->lab_prev != si) mgate_wait = c->slots[c->lab_prev].ev_mrg;
-        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, FM_CCL_GATE ? B.ev_lab : nullptr, mgate_wait,
-                                   FM_MERGE_GATE ? B.ev_mrg : nullptr));
+        if (!c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
+        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, B.ev_lab));
         c->lab_prev = si;  // counts land in mapped h_count / h_overflow
         B.fa = fa;
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));
@@ -1278,6 +1322,8 @@ int fm_write_background(fm_ctx* c, int stream, const double* in) {
 
 int fm_kernel_times(fm_ctx* c, const char** names, double* ms, int64_t* launches, int cap) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    if (c->timer.fold_stamps() != 0) return fail(c, FM_EHIP, "reading the launch stamps failed");
     const int n = (int)c->timer.names.size();
     for (int i = 0; i < std::min(n, cap); i++) {
         if (names) names[i] = c->timer.names[i];
@@ -1289,6 +1335,7 @@ int fm_kernel_times(fm_ctx* c, const char** names, double* ms, int64_t* launches
 
 int fm_reset_kernel_times(fm_ctx* c) {
     if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    HIP_TRY(c, hipSetDevice(c->p.device));
     c->timer.reset();
     return FM_OK;
 }

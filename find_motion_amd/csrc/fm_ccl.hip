@@ -40,31 +40,15 @@ namespace cc {
 
 constexpr int TS = 64;
 constexpr int MAXR = kTileMaxRuns;
-#ifndef FM_CCL_LIGHT
-#define FM_CCL_LIGHT 256
-#endif
-constexpr int LIGHT = FM_CCL_LIGHT;  // runs held by the light pass
+constexpr int LIGHT = 256;      // runs held by the light pass
 constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k_merge
-#ifndef FM_CCL_GW
-#define FM_CCL_GW 4  // measured: 8 > 16 > 32 > 4 (r02: 266k vs 262k vs 251k vs 257k frames/s at the bench default);
-                     // re-checked at v21 (batch 192, raised priorities), 3 alternating rounds: 8 382k, 6 381k, 16 370k;
-                     // with the labelling gate (round 3): 4 392.3k, 6 389.0k, 8 388.4k (4 alternating rounds)
-#endif
-constexpr int GW = FM_CCL_GW;          // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit
+// workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit.  Measured: with the labelling gate
+// (round 3) 4 392.3k, 6 389.0k, 8 388.4k frames/s (4 alternating rounds)
+constexpr int GW = 4;
 constexpr int RG = 512;         // k_regions threads
-#ifndef FM_CCL_PRIO
-#define FM_CCL_PRIO 0  // contour waves' issue priority over the pixel kernel's (round 2: +4 % at 2; round 3: 0 gives
-                       // the same throughput, 368.1 vs 368.2 k, with 6 % shorter pixel launches, 436 vs 464 us)
-#endif
-#ifndef FM_CCL_REST_PRIO
-#define FM_CCL_REST_PRIO 0  // issue priority of k_regions / k_fold / k_emit / k_counts (0: the default)
-#endif
-#ifndef FM_HEAVY_PRIO
-#define FM_HEAVY_PRIO 0  // (was 3, see FM_CCL_PRIO)
-#endif
-#ifndef FM_MERGE_PRIO
-#define FM_MERGE_PRIO 0  // (was 2, see FM_CCL_PRIO)
-#endif
+// The contour waves run at the pixel waves' issue priority 0.  (Raised -- labelling 2, heavy tiles 3,
+// merge 2 -- they gained 4 % in round 2; in round 3, 0 gave the same throughput, 368.1 vs 368.2 k,
+// with 6 % shorter pixel launches; every contour kernel at 3: 402.7 vs 413.3 k, round 4.)
 constexpr int MAX_REGION_TILES = 8192;
 static_assert(MAX_REGION_TILES <= 32 * RG, "k_regions keeps one candidate bit per tile of a thread in a u32");
 constexpr uint32_t REF_OUTER = 0x80000000u;
@@ -178,14 +162,11 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, int lane) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-#ifndef FM_CCL_DPP_SCAN
-#define FM_CCL_DPP_SCAN 1  // with raised contour priorities -1 % at 60 steps; at priority 0 +1.5 % (373.0 vs 367.6 k, 4 rounds)
-#endif
 // Wave-wide inclusive prefix sum by DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then
 // row_bcast 15 / 31 across rows): six VALU adds, where a __shfl_up loop is six ds_bpermute
-// round trips through the LDS unit.  Needs every lane active (callers are in wave-uniform flow).
+// round trips through the LDS unit (the DPP scans: +1.5 %, 373.0 vs 367.6 k, 4 rounds, round 3).
+// Needs every lane active (callers are in wave-uniform flow).
 __device__ __forceinline__ int wave_incl_sum(int v) {
-#if FM_CCL_DPP_SCAN
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
@@ -193,42 +174,19 @@ __device__ __forceinline__ int wave_incl_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
-#else
-    const int ln = (int)__lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(v, o, 64);
-        if (ln >= o) v += u;
-    }
-    return v;
-#endif
 }
 // __shfl_up(v, 1) / __shfl_down(v, 1) (lane 0 / 63 keep their own value) by DPP wave shifts
 __device__ __forceinline__ int lane_up1(int v) {
-#if FM_CCL_DPP_SCAN
     return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xF, 0xF, false);  // wave_shr:1
-#else
-    return __shfl_up(v, 1, 64);
-#endif
 }
 __device__ __forceinline__ int lane_down1(int v) {
-#if FM_CCL_DPP_SCAN
     return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false);  // wave_shl:1
-#else
-    return __shfl_down(v, 1, 64);
-#endif
 }
 __device__ __forceinline__ uint64_t lane_down1_64(uint64_t v) {
     return ((uint64_t)(uint32_t)lane_down1((int)(uint32_t)(v >> 32)) << 32) | (uint32_t)lane_down1((int)(uint32_t)v);
 }
-// a lane's value broadcast (v_readlane with the DPP variant, else ds_bpermute as __shfl)
-__device__ __forceinline__ int lane_at(int v, int lane) {
-#if FM_CCL_DPP_SCAN
-    return __builtin_amdgcn_readlane(v, lane);
-#else
-    return __shfl(v, lane, 64);
-#endif
-}
+// a lane's value broadcast (v_readlane)
+__device__ __forceinline__ int lane_at(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ uint64_t lane_at64(uint64_t v, int lane) {
     return ((uint64_t)(uint32_t)lane_at((int)(uint32_t)(v >> 32), lane) << 32) | (uint32_t)lane_at((int)(uint32_t)v, lane);
 }
@@ -337,9 +295,6 @@ __device__ __forceinline__ int run_at(int base, uint64_t starts, int p) {
 
 enum : int { TCCL_OK = 0, TCCL_RUNS = 1, TCCL_NODES = 2 };
 
-#ifndef FM_CCL_FULL
-#define FM_CCL_FULL 1  // fully set tiles take a closed-form record (no run labelling)
-#endif
 
 // the tile's node ids: n consecutive ids from its frame's quota (one counter per frame, so
 // the tiles of different frames never contend on one atomic), or past the quota from the
@@ -400,7 +355,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
     // full tile (every pixel set after dilation; tiles cut by the image edge never are): one
     // foreground component whose root is run 0 = row 0, columns 0..63, and no background -- what the
     // labelling below ends with after its ~7 pointer-jumping rounds over the 64-run chain
-    if (FM_CCL_FULL && __ballot(m != ~0ull) == 0) {
+    if (__ballot(m != ~0ull) == 0) {  // a fully set tile takes a closed-form record (no run labelling)
         const int nb = take_nodes(a, f, 1, ln);
         if (nb < 0) return TCCL_NODES;
         TR->edges[ln] = 0x8000u;
@@ -636,7 +591,6 @@ template <bool DILATE>
 // workgroup, which the contour kernels resident beside the pixel kernel often did not leave free,
 // so a batch's k_regions waited for the pixel kernel to end: 269 µs instead of 10)
 __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
-    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     extern __shared__ int uf[];  // [a.ntiles]
     __shared__ int s_nc, s_nr;
     const int f = blockIdx.x;
@@ -711,31 +665,14 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
 // grid (GW, F); each wave labels candidates of the frame's list with a stride, in LDS
 // (LIGHT runs); a tile with more runs (a dense texture of small blobs) goes to the
 // heavy list
-#ifndef FM_CCL_NVGPR
-#define FM_CCL_NVGPR 0  // cap on k_tile_ccl's VGPRs (0: none), so more of its waves fit beside the pixel kernel's
-#endif
-#ifndef FM_CCL_WPE
-#define FM_CCL_WPE 6  // k_tile_ccl compiled for 6 waves per SIMD: 80 VGPRs (was 96, no spills), so two of its
-                      // workgroups fit beside two k_pix5 workgroups (4 x 88 VGPRs per SIMD): +1.2 %, 4 rounds
-#endif
-#if FM_CCL_NVGPR
-#define FM_CCL_ATTR __attribute__((amdgpu_num_vgpr(FM_CCL_NVGPR)))
-#elif FM_CCL_WPE
-#define FM_CCL_ATTR __attribute__((amdgpu_waves_per_eu(FM_CCL_WPE)))
-#else
-#define FM_CCL_ATTR
-#endif
-// scratch as dynamic LDS (FM_CCL_DYN): the compiler then takes its occupancy from FM_CCL_WPE, not
-// from a static 30 KB (see k_tile_heavy)
-#ifndef FM_CCL_DYN
-#define FM_CCL_DYN 1
-#endif
+// k_tile_ccl is compiled for 6 waves per SIMD: 80 VGPRs (was 96, no spills), so two of its workgroups
+// fit beside two k_pix5 workgroups (4 x 88 VGPRs per SIMD): +1.2 %, 4 rounds.  Its scratch is dynamic
+// LDS, so the compiler takes its occupancy from that, not from a static 30 KB (see k_tile_heavy).
 constexpr size_t TC_WAVE_LDS = ((size_t)(6 * LIGHT + 66) * 4 + 2 * LIGHT + 3 * LIGHT + 15) / 16 * 16;
 constexpr size_t TC_LDS = CW * TC_WAVE_LDS;
 template <bool DILATE>
-__global__ __launch_bounds__(64 * CW) FM_CCL_ATTR void k_tile_ccl(FusedArgs a) {
+__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(6))) void k_tile_ccl(FusedArgs a) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-#if FM_CCL_DYN
     // per wave: par, amin, amax, ay, pairs (u32), rb | ord (u16) | rx0, rx1, rf (u8)
     extern __shared__ __attribute__((aligned(16))) int tc_lds[];
     int* wb = tc_lds + (size_t)wv * (TC_WAVE_LDS / 4);
@@ -743,19 +680,10 @@ __global__ __launch_bounds__(64 * CW) FM_CCL_ATTR void k_tile_ccl(FusedArgs a) {
     uint8_t* wbyte = reinterpret_cast<uint8_t*>(word + LIGHT);
     const Scratch sc{wb, wb + LIGHT, wb + 2 * LIGHT, wb + 3 * LIGHT, wbyte, wbyte + LIGHT, wbyte + 2 * LIGHT,
                      wb + 6 * LIGHT, word, reinterpret_cast<uint32_t*>(wb + 4 * LIGHT)};
-#else
-    __shared__ int par[CW][LIGHT], amin[CW][LIGHT], amax[CW][LIGHT], ay[CW][LIGHT];
-    __shared__ uint8_t rx0[CW][LIGHT], rx1[CW][LIGHT], rf[CW][LIGHT];
-    __shared__ uint16_t ord[CW][LIGHT];
-    __shared__ uint32_t pairs[CW][2 * LIGHT];
-    __shared__ int rb[CW][66];
-    const Scratch sc{par[wv], amin[wv], amax[wv], ay[wv], rx0[wv], rx1[wv], rf[wv], rb[wv], ord[wv], pairs[wv]};
-#endif
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     const int nc = a.ncr[2 * f];
     if (FM_OOB(a, nc >= 0 && nc <= a.ntiles, 1)) return;
-    if (FM_CCL_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_PRIO);
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int ti = a.clist[f * a.ntiles + k];
         if (FM_OOB(a, ti >= 0 && ti < a.ntiles, 1)) continue;
@@ -785,29 +713,14 @@ __global__ __launch_bounds__(64 * CW) FM_CCL_ATTR void k_tile_ccl(FusedArgs a) {
 // faster end to end than keeping the per-run arrays in global memory, which k_pix's ~52 KB
 // workgroups needed)
 constexpr int NHW = kHeavyWaves;
-#ifndef FM_HEAVY_WPE
-#define FM_HEAVY_WPE 1
-#endif
-#ifndef FM_HEAVY_NVGPR
-#define FM_HEAVY_NVGPR 0  // explicit VGPR budget of k_tile_heavy (0: the compiler's)
-#endif
-#if FM_HEAVY_NVGPR
-#define FM_HEAVY_ATTR __attribute__((amdgpu_num_vgpr(FM_HEAVY_NVGPR)))
-#else
-#define FM_HEAVY_ATTR
-#endif
 // The scratch is dynamic LDS: with a static 46 KB the compiler derives an occupancy of one wave per
 // SIMD from the LDS alone and then sizes the kernel's VGPR allocation for that occupancy (264
 // registers for 67 used), which no CU holding two k_pix5 workgroups (4 waves x 88 VGPRs per SIMD)
 // can fit: every batch's heavy tiles then waited for the pixel kernel to end (trace r03h: 300-370 us
 // beside it, 26 us alone).  Sized at launch, the allocation is what the code uses.
-#ifndef FM_HEAVY_DYN
-#define FM_HEAVY_DYN 1
-#endif
 constexpr int HV_INT = 4 * MAXR + 2 * MAXR + 68;   // par, amin, amax, ay | pairs (u32) | rb
 constexpr size_t HEAVY_LDS = (size_t)HV_INT * 4 + 3 * MAXR + 2 * MAXR;  // + rx0, rx1, rf (u8), ord (u16)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FM_HEAVY_WPE))) FM_HEAVY_ATTR void k_tile_heavy(FusedArgs a) {
-#if FM_HEAVY_DYN
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_tile_heavy(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) int hv_lds[];
     int* par = hv_lds;
     int* amin = par + MAXR;
@@ -819,19 +732,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FM_HEAVY_WPE
     uint8_t* rx0 = reinterpret_cast<uint8_t*>(ord + MAXR);
     uint8_t* rx1 = rx0 + MAXR;
     uint8_t* rf = rx1 + MAXR;
-#else
-    __shared__ int par[MAXR], amin[MAXR], amax[MAXR], ay[MAXR];
-    __shared__ uint8_t rx0[MAXR], rx1[MAXR], rf[MAXR];
-    __shared__ uint16_t ord[MAXR];
-    __shared__ uint32_t pairs[2 * MAXR];
-    __shared__ int rb[68];
-#endif
     const size_t F = (size_t)a.T * a.S;
     const int n = a.count[2 * F + 1];
     const int ln = threadIdx.x;
     if (FM_OOB(a, n <= (int)(F * a.ntiles), 2)) return;
     const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
-    if (FM_HEAVY_PRIO) __builtin_amdgcn_s_setprio(FM_HEAVY_PRIO);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         if (FM_OOB(a, item >= 0 && item < (int)(F * a.ntiles), 4)) continue;
@@ -847,23 +752,14 @@ __device__ __forceinline__ int efg(uint16_t e) { return e >> 15; }
 // node of the component with edge label e of candidate tile `tile`
 __device__ __forceinline__ int enode(const TileRec* TR, int tile, uint16_t e) { return TR[tile].nbase + (e & 0x7FFF); }
 
-// Union-find policies of the edge merge: over the global NodeRec parents (any frame), or over a
-// frame's nodes mirrored in LDS (k_resolve's fast path: local id = region tile, or ntiles + the
-// node's place in the frame's quota).
+// Union-find of the edge merge: over the global NodeRec parents.  (A per-frame union-find in LDS,
+// k_merge + k_fold + k_emit + k_counts of one frame in one workgroup -- k_resolve, round 4 -- measured
+// 401.6 vs 415.7 k frames/s: its long-lived per-frame workgroups held CU slots the pixel kernel needed.)
 struct GlobalUF {
     NodeRec* N;
     __device__ void uni(int x, int y) const { gunion(N, x, y); }
     __device__ bool outer(int n) const { return (N[n].flags & 2) != 0; }
     __device__ void mark_outer(int n) const { atomicOr(&N[n].flags, 2u); }
-};
-struct LocalUF {
-    int* par;
-    uint32_t* fl;
-    int rb0, qbase, nt;  // region node ids: rb0 + tile; quota node ids: qbase + i
-    __device__ int loc(int g) const { return g < qbase ? g - rb0 : g - qbase + nt; }
-    __device__ void uni(int x, int y) const { lunion(par, loc(x), loc(y)); }
-    __device__ bool outer(int n) const { return (fl[loc(n)] & 2) != 0; }
-    __device__ void mark_outer(int n) const { atomicOr(&fl[loc(n)], 2u); }
 };
 
 // Background component `nd` of a candidate touches empty region `rep`.  An outer
@@ -956,14 +852,12 @@ __device__ __forceinline__ void merge_tile(const FusedArgs& a, size_t f, int t, 
     }
 }
 
-// one wave per candidate, lane = edge position (the global-memory merge; k_resolve below replaces it
-// in the product chain)
+// one wave per candidate, lane = edge position
 __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     if (a.count[F + f]) return;
-    if (FM_MERGE_PRIO) __builtin_amdgcn_s_setprio(FM_MERGE_PRIO);
     const int nt = a.ntiles;
     const TileRec* TR = a.tiles + f * nt;
     (void)TR;  // (read by the bounds check of the checked build)
@@ -994,7 +888,6 @@ __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
 // one wave per candidate tile (lanes = its components) or per empty-tile region: path
 // compression with outer flags, bboxes and raster-first pixels folded into the roots
 __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
-    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
@@ -1070,7 +963,6 @@ __device__ __forceinline__ void emit_frame(const FusedArgs& a, size_t f, int wav
 }
 
 __global__ __launch_bounds__(64 * CW) void k_emit(FusedArgs a) {
-    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
@@ -1084,186 +976,12 @@ __global__ __launch_bounds__(64 * CW) void k_emit_all(FusedArgs a, int f, int32_
     emit_frame(a, (size_t)f, blockIdx.x * CW + wv, gridDim.x * CW, ln, recs, cnt, cap);
 }
 
-// ---------------------------------------------------------------------------
-// k_resolve: k_merge + k_fold + k_emit + k_counts of one frame in one workgroup (round 4).  The
-// frame's union-find lives in LDS -- its empty-region nodes (local id = tile) and the nodes its
-// candidate tiles took from the frame's quota (local id = ntiles + place in the quota) -- so every
-// find and link is an LDS round trip instead of a chain of agent-scope loads and atomics through L2
-// (k_merge spent 88 % of its wave cycles waiting on those), and one launch replaces four.  Foreground
-// bboxes and raster-first keys fold into the root records in HBM with atomics that return nothing;
-// the global parents and the roots' outer flags are written back, so k_emit_all and the contour-area
-// pass read the same records as after k_fold.  A frame whose tiles took nodes from the shared pool,
-// or has more nodes than RV_CAP, runs the same steps on the global union-find.
-constexpr int RV_CAP = 2048;  // LDS nodes per frame: 16 KB (parents + flags)
-__device__ __forceinline__ void agent_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
-__device__ __forceinline__ void agent_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
-
-__global__ __launch_bounds__(64 * CW) void k_resolve(FusedArgs a) {
-    __shared__ int par[RV_CAP];
-    __shared__ uint32_t fl[RV_CAP];
-    __shared__ int s_cnt;
-    const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
-    const size_t f = blockIdx.x;
-    const size_t F = (size_t)a.T * a.S;
-    const int nt = a.ntiles;
-    if (a.tflag_waves == 1)  // the k_fused path's tile flags, cleared for the slot's next batch
-        for (int t = tid; t < nt; t += 64 * CW) a.tflag[f * nt + t] = 0;
-    if (tid == 0) {
-        s_cnt = 0;
-        if (f == 0) {
-            a.h_stats[0] = a.count[2 * F];
-            a.h_stats[1] = a.count[2 * F + 1];
-        }
-    }
-    if (a.count[F + f]) {  // relabelled by the host's pixel-level fallback
-        if (tid == 0) {
-            a.h_count[f] = 0;
-            a.h_overflow[f] = 1;
-        }
-        return;
-    }
-    NodeRec* N = a.nodes;
-    const TileRec* TRf = a.tiles + f * nt;
-    const uint8_t* cf = a.candf + f * nt;
-    const int32_t* rr = a.regrep + f * nt;
-    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
-    const int rb0 = (int)(f * nt);
-    const long long q0 = (long long)F * nt;
-    const int qbase = (int)(q0 + (long long)f * a.nquota);
-    const int used = a.count[2 * F + 2 + f];  // this frame's quota fill (past nquota: the pool was used)
-    const int nl = nt + used;
-    int32_t* recs = a.rec + f * a.cap * 5;
-    const int cap = a.cap;
-    if (used > a.nquota || nl > RV_CAP) {
-        // ---- slow path: the same steps over the global union-find
-        const GlobalUF G{N};
-        for (int k = wv; k < nc; k += CW) {
-            const int t = a.clist[f * nt + k];
-            if (FM_OOB(a, t >= 0 && t < nt && TRf[t].nbase >= 0 && TRf[t].nbase + TRf[t].nroots <= a.nnodes, 5)) continue;
-            merge_tile(a, f, t, ln, G);
-        }
-        agent_release();
-        __syncthreads();
-        agent_acquire();
-        for (int k = wv; k < nc + nr; k += CW) {
-            if (k < nc) {
-                const int t = a.clist[f * nt + k];
-                if (FM_OOB(a, t >= 0 && t < nt, 1)) continue;
-                const int k1 = TRf[t].nroots, nb = TRf[t].nbase;
-                if (FM_OOB(a, nb >= 0 && (long long)nb + k1 <= a.nnodes, 5)) continue;
-                for (int i = ln; i < k1; i += 64) fold_node(N, nb + i);
-            } else if (ln == 0) {
-                const int r = a.rlist[f * nt + (k - nc)];
-                if (FM_OOB(a, r >= 0 && r < nt, 6)) continue;
-                fold_node(N, rb0 + r);
-            }
-        }
-        agent_release();
-        __syncthreads();
-        agent_acquire();
-        emit_frame(a, f, wv, CW, ln, recs, &s_cnt, cap);
-        __syncthreads();
-        if (tid == 0) {
-            a.count[f] = s_cnt;
-            a.h_count[f] = s_cnt;
-            a.h_overflow[f] = 0;
-        }
-        return;
-    }
-    // ---- fast path: the frame's nodes in LDS
-    const LocalUF U{par, fl, rb0, qbase, nt};
-    for (int i = tid; i < nl; i += 64 * CW) {
-        par[i] = i;
-        // region nodes: only the representatives' records are this batch's (the rest are never referenced)
-        fl[i] = i < nt ? (cf[i] == 0 && rr[i] == i ? N[rb0 + i].flags : 0u) : N[qbase + i - nt].flags;
-    }
-    __syncthreads();
-    for (int k = wv; k < nc; k += CW) {
-        const int t = a.clist[f * nt + k];
-        if (FM_OOB(a, t >= 0 && t < nt && TRf[t].nbase >= qbase && TRf[t].nbase + TRf[t].nroots <= qbase + used, 5))
-            continue;
-        merge_tile(a, f, t, ln, U);
-    }
-    __syncthreads();
-    // fold: every node to its root (par flattened), outer flags into the roots' LDS flags, foreground
-    // extents into the roots' records in HBM; global parents written back
-    for (int i = tid; i < nl; i += 64 * CW) {
-        if (i < nt && !(cf[i] == 0 && rr[i] == i)) continue;
-        const int rt = lfind(par, i);
-        par[i] = rt;
-        const int gi = i < nt ? rb0 + i : qbase + i - nt;
-        const int grt = rt < nt ? rb0 + rt : qbase + rt - nt;
-        if (rt == i) continue;
-        N[gi].parent = grt;
-        const uint32_t fi = fl[i];
-        if (fi & 1) {
-            const NodeRec nd = N[gi];
-            atomicMin((unsigned long long*)&N[grt].key, (unsigned long long)nd.key);
-            atomicMin(&N[grt].minx, nd.minx);
-            atomicMax(&N[grt].maxx, nd.maxx);
-            atomicMax(&N[grt].maxy, nd.maxy);
-        } else if (fi & 2) {
-            atomicOr(&fl[rt], 2u);
-        }
-    }
-    agent_release();
-    __syncthreads();
-    agent_acquire();  // the folded root records, as other CUs' atomics left them in L2
-    // emit: the external test at every foreground root, its record into mapped host memory; the roots'
-    // outer flags back into their records (k_emit_all / the area pass read them there)
-    for (int i = tid; i < nl; i += 64 * CW) {
-        if (i < nt && !(cf[i] == 0 && rr[i] == i)) continue;
-        if (par[i] != i) continue;
-        const int gi = i < nt ? rb0 + i : qbase + i - nt;
-        const uint32_t fi = fl[i];
-        if (!(fi & 1)) {
-            if (fi & 2) N[gi].flags = fi;
-            continue;
-        }
-        const uint64_t key = N[gi].key;
-        const uint32_t first = (uint32_t)(key >> 32), ref = (uint32_t)key;
-        const int fx = (int)(first % (uint32_t)a.w), fy = (int)(first / (uint32_t)a.w);
-        bool ext;
-        if (ref & REF_OUTER) {
-            ext = true;
-        } else {
-            const int tf = (fy / TS) * a.ntx + fx / TS;  // tile of the raster-first pixel (a candidate)
-            if (FM_OOB(a, tf >= 0 && tf < nt && (!(ref & REF_EDGE) || tf % a.ntx > 0), 7)) continue;
-            int bn;
-            if (ref & REF_EDGE) {
-                const int lt = tf - 1;
-                bn = cf[lt] ? U.loc(enode(TRf, lt, TRf[lt].edges[64 + (ref & 63)])) : rr[lt];
-            } else {
-                bn = U.loc(TRf[tf].nbase + (int)ref);
-            }
-            if (FM_OOB(a, bn >= 0 && bn < nl, 5)) continue;
-            ext = (fl[par[bn]] & 2) != 0;
-        }
-        if (!ext) continue;
-        const int id = atomicAdd(&s_cnt, 1);
-        if (id < cap) {
-            int32_t* rec = recs + (size_t)id * 5;
-            rec[0] = (int32_t)first;
-            rec[1] = N[gi].minx;
-            rec[2] = fy;
-            rec[3] = N[gi].maxx;
-            rec[4] = N[gi].maxy;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        a.count[f] = s_cnt;
-        a.h_count[f] = s_cnt;
-        a.h_overflow[f] = 0;
-    }
-}
 
 // one workgroup per frame: counts and overflow flags straight into mapped host memory
 // (no copy after the kernel); the k_fused path's tile flags cleared for the slot's next
 // batch (k_pix rewrites its per-wave flag words every frame)
 constexpr int FT = 256;
 __global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
-    if (FM_CCL_REST_PRIO) __builtin_amdgcn_s_setprio(FM_CCL_REST_PRIO);
     const size_t f = blockIdx.x;
     const size_t F = (size_t)a.T * a.S;
     if (a.tflag_waves == 1)
@@ -1379,7 +1097,7 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
 }
 
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* tm, hipEvent_t gate_wait,
-                           hipEvent_t gate_done, hipEvent_t mgate_wait, hipEvent_t mgate_done) {
+                           hipEvent_t gate_done) {
     if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;
     const unsigned F = (unsigned)(a.T * a.S);
     const dim3 gf(cc::GW, F);
@@ -1393,41 +1111,17 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
         if (e != hipSuccess) return e;
     }
     tok = tm ? tm->begin("tile_ccl", st) : -1;
-    if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
-    else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), FM_CCL_DYN ? cc::TC_LDS : 0, st, a);
+    if (dilate) hipLaunchKernelGGL(cc::k_tile_ccl<true>, gf, dim3(64 * cc::CW), cc::TC_LDS, st, a);
+    else hipLaunchKernelGGL(cc::k_tile_ccl<false>, gf, dim3(64 * cc::CW), cc::TC_LDS, st, a);
     if (gate_done) {
         const hipError_t e = hipEventRecord(gate_done, st);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), FM_HEAVY_DYN ? cc::HEAVY_LDS : 0, st, a);
+    hipLaunchKernelGGL(cc::k_tile_heavy, dim3(cc::NHW), dim3(64), cc::HEAVY_LDS, st, a);
     if (tm) tm->end(tok);
-    if (mgate_wait) {
-        const hipError_t e = hipStreamWaitEvent(st, mgate_wait, 0);
-        if (e != hipSuccess) return e;
-    }
-#ifndef FM_CCL_RESOLVE
-#define FM_CCL_RESOLVE 0  // k_resolve (one workgroup per frame, LDS union-find) instead of merge / fold / emit / counts.
-                          // Measured (round 4, 2 alternating rounds): 401.6 vs 415.7 k frames/s, pixel launches
-                          // 619-773 vs 557-597 us beside the chains: the per-frame workgroups hold their CU slots
-                          // far longer than k_merge's short waves; off
-#endif
-    if (FM_CCL_RESOLVE) {
-        tok = tm ? tm->begin("resolve", st) : -1;
-        hipLaunchKernelGGL(cc::k_resolve, dim3(F), dim3(64 * cc::CW), 0, st, a);
-        if (tm) tm->end(tok);
-        if (mgate_done) {
-            const hipError_t e = hipEventRecord(mgate_done, st);
-            if (e != hipSuccess) return e;
-        }
-        return hipGetLastError();
-    }
     tok = tm ? tm->begin("merge", st) : -1;
     hipLaunchKernelGGL(cc::k_merge, gf, dim3(64 * cc::CW), 0, st, a);
     if (tm) tm->end(tok);
-    if (mgate_done) {
-        const hipError_t e = hipEventRecord(mgate_done, st);
-        if (e != hipSuccess) return e;
-    }
     tok = tm ? tm->begin("fold_emit", st) : -1;
     hipLaunchKernelGGL(cc::k_fold, gf, dim3(64 * cc::CW), 0, st, a);
     hipLaunchKernelGGL(cc::k_emit, gf, dim3(64 * cc::CW), 0, st, a);

@@ -148,8 +148,30 @@ struct FusedArgs {
     double alpha, beta;
     long long acc_vec_end;
     int any_keep;                // some stream of the context has a keep-mask (k_pix5 variant choice)
+    uint64_t* kstamp;            // this launch's [first start, last end] stamp pair (KernelTimer::stamp) or nullptr
     int32_t coef[kMaxK];
 };
+
+// In-kernel launch stamps (KernelTimer::stamp): thread 0 of every workgroup takes the 100 MHz
+// s_memrealtime counter at its start into ks[0] (atomic min), lane 0 of every wave at its end into
+// ks[1] (atomic max), so ks[1] - ks[0] is the launch from its first workgroup's start to its last
+// wave's end.  Plain (vector) global atomics that return nothing.
+__device__ __forceinline__ void kstamp_begin(uint64_t* ks) {
+    if (ks && threadIdx.x == 0)
+        atomicMin(reinterpret_cast<unsigned long long*>(ks), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void kstamp_end(uint64_t* ks) {
+    if (ks && (threadIdx.x & 63) == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(ks) + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+// Kernels of thousands of short workgroups (the INTER_AREA resize): the start from the first 8
+// workgroups dispatched, the end from wave 0 of every workgroup (one atomic per workgroup).
+__device__ __forceinline__ void kstamp_begin_grid(uint64_t* ks) {
+    if (blockIdx.x + blockIdx.y * gridDim.x < 8) kstamp_begin(ks);
+}
+__device__ __forceinline__ void kstamp_end_wg(uint64_t* ks) {
+    if (threadIdx.x < 64) kstamp_end(ks);
+}
 
 // computeResizeAreaTab restated (fm_capi.cpp); false if a destination's taps are not consecutive
 bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A);
@@ -158,9 +180,9 @@ bool build_area_axis(int ssize, int dsize, double scale, AreaAxis& A);
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
                               int h, int w, const int32_t* xofs, const int32_t* xcnt, const float* xwt,
                               int xtaps, const int32_t* yofs, const int32_t* ycnt, const float* ywt,
-                              int ytaps, const uint8_t* const* srcs = nullptr);
+                              int ytaps, const uint8_t* const* srcs = nullptr, uint64_t* kstamp = nullptr);
 hipError_t launch_resize_area_fast(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W,
-                                   int h, int w, int sx, int sy);
+                                   int h, int w, int sx, int sy, uint64_t* kstamp = nullptr);
 hipError_t launch_pixel(hipStream_t st, const PixelArgs& a);
 struct KernelTimer;
 hipError_t launch_ccl(hipStream_t st, const CclArgs& a, KernelTimer* timer);
@@ -176,8 +198,7 @@ bool pix_supported(int ksize);
 // gate_wait / gate_done (optional): the labelling kernel waits for gate_wait (the previous batch's
 // labelling) and gate_done is recorded after it, so that one batch's labelling runs at a time
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer,
-                           hipEvent_t gate_wait = nullptr, hipEvent_t gate_done = nullptr,
-                           hipEvent_t mgate_wait = nullptr, hipEvent_t mgate_done = nullptr);
+                           hipEvent_t gate_wait = nullptr, hipEvent_t gate_done = nullptr);
 // every external-contour record of frame f of a finished batch (all of them, unlike the
 // capped k_emit), into rec [cap][5]; *cnt must be 0 before
 hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap);
@@ -189,24 +210,33 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
 hipError_t launch_expand_bits(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, uint8_t* out, int h, int w,
                               int ntx);
 
-// Optional per-kernel event timing (FM_FLAG_PROFILE): events are recorded on
-// the launch stream around each kernel and read back after the stream syncs.
+// Optional per-kernel timing.  FM_FLAG_PROFILE: events recorded on the launch stream around each
+// kernel, read back after the stream syncs.  FM_FLAG_PROFILE_PIX: the pixel kernel and the INTER_AREA
+// resize only, EVERY launch timed by in-kernel stamps (stamp(): no event packet enters the streams);
+// other kernels on the pixel / input stream by events on one launch in kSample.
 struct KernelTimer {
     bool enabled = false;
-    bool pixel_only = false;  // time only launches on `stream` (the pixel stream), one in kSample: FM_FLAG_PROFILE_PIX
+    bool pixel_only = false;
     static constexpr int kSample = 4;
+    static constexpr int kStampRing = 4096;  // stamped launches held between two folds (more go untimed)
     std::vector<int64_t> calls;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // also sampled in the pixel-only mode: the input stream's resize
+    hipStream_t stream2 = nullptr;  // also timed in the pixel-only mode: the input stream's resize
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
     std::vector<const char*> names;
     std::vector<double> ms;
     std::vector<int64_t> launches;
+    uint64_t* d_stamps = nullptr;   // device [kStampRing][2]: (first start, last end), ticks of 10 ns
+    std::vector<int> stamp_ids;     // name id of ring entries [0, stamp_ids.size()) not yet folded
+    int64_t unstamped = 0;          // launches that found the ring full
+    int id_of(const char* name);
     int begin(const char* name, hipStream_t st = nullptr);  // token for end(), -1 when disabled
     void end(int token);
     void collect();                // folds in every pair whose end event has completed
+    uint64_t* stamp(const char* name);  // this launch's stamp pair, nullptr when not stamping
+    int fold_stamps();             // waits for the stamped streams, folds and re-arms the entries
     void reset();
     ~KernelTimer();
 };

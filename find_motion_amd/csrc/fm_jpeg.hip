@@ -1463,11 +1463,15 @@ int fm_mjpeg_enqueue(fm_mjpeg* d, const uint8_t* const* jpegs, const size_t* siz
     std::vector<TabSet> fsets(n);
     for (int i = 0; i < n; i++) {
         const ParsedJpeg& J = P[i];
-        if (J.W != g.W || J.H != g.H || J.nc != g.nc) return jfail(d, FM_EINVAL, "frame %d: geometry differs", i);
+        if (J.W != g.W || J.H != g.H) return jfail(d, FM_EINVAL, "frame %d: geometry differs", i);
+        // a later frame coded with other components or sampling than the decoder's layout: FM_ENOTSUP, the
+        // status on which the decode-ahead feeder decodes the batch on the host (a stream may switch)
+        if (J.nc != g.nc) return jfail(d, FM_ENOTSUP, "frame %d: %d components, the decoder's layout has %d", i, J.nc, g.nc);
         TabSet& ts_ = fsets[i];
         int ids[2][2] = {{-1, -1}, {-1, -1}};
         for (int c = 0; c < g.nc; c++) {
-            if (J.ch[c] != g.comp[c].h || J.cv[c] != g.comp[c].v) return jfail(d, FM_EINVAL, "frame %d: sampling differs", i);
+            if (J.ch[c] != g.comp[c].h || J.cv[c] != g.comp[c].v)
+                return jfail(d, FM_ENOTSUP, "frame %d: sampling differs from the decoder's layout", i);
             if (!J.qt_present[J.ctq[c]]) return jfail(d, FM_EINVAL, "frame %d: missing DQT %d", i, J.ctq[c]);
             int k = 0;
             while (k < J.ns && J.sid[k] != J.cid[c]) k++;

@@ -44,7 +44,8 @@ __global__ __launch_bounds__(256) void k_resize_area(const uint8_t* __restrict__
                                                       const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
                                                       int xtaps, const int32_t* __restrict__ yofs,
                                                       const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
-                                                      int ytaps) {
+                                                      int ytaps, uint64_t* kstamp) {
+    kstamp_begin_grid(kstamp);
     const int dy = blockIdx.x;
     const size_t f = blockIdx.y;
     const uint8_t* S0 = src + f * (size_t)H * W * 3;
@@ -65,6 +66,7 @@ __global__ __launch_bounds__(256) void k_resize_area(const uint8_t* __restrict__
         }
         D[e] = sat_u8(__float2int_rn(sum));
     }
+    kstamp_end_wg(kstamp);
 }
 
 // INTER_AREA, general path, staged: one workgroup per (destination row, frame) walks
@@ -83,7 +85,8 @@ __global__ __launch_bounds__(RS_T) void k_resize_area_rows(const uint8_t* __rest
                                                            const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
                                                            int xtaps, const int32_t* __restrict__ yofs,
                                                            const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
-                                                           int ytaps) {
+                                                           int ytaps, uint64_t* kstamp) {
+    kstamp_begin_grid(kstamp);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int rowb = 3 * W;                        // multiple of 16
     uint8_t* rows = lds;                           // [2][rowb]
@@ -154,6 +157,7 @@ __global__ __launch_bounds__(RS_T) void k_resize_area_rows(const uint8_t* __rest
         const int e = tid + RS_T * k;
         if (e < ne) D[e] = sat_u8(__float2int_rn(sum[k]));
     }
+    kstamp_end_wg(kstamp);
 #undef RS_LOAD_ROW
 #undef RS_STORE_ROW
 }
@@ -176,7 +180,9 @@ __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restri
                                                          const int32_t* __restrict__ xcnt, const float* __restrict__ xwt,
                                                          int xtaps, const int32_t* __restrict__ yofs,
                                                          const int32_t* __restrict__ ycnt, const float* __restrict__ ywt,
-                                                         int ytaps, const uint8_t* const* __restrict__ srcs) {
+                                                         int ytaps, const uint8_t* const* __restrict__ srcs,
+                                                         uint64_t* kstamp) {
+    kstamp_begin_grid(kstamp);
     constexpr int NB = 3 * NT;          // tap bytes of one row
     constexpr int NA = (NB + 3) / 4;    // aligned dwords holding them
     constexpr int ND = NA + 1;          // dwords loaded (a 0..3-byte misalignment)
@@ -260,29 +266,34 @@ __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restri
 #pragma unroll
         for (int c = 0; c < 3; c++) D[c] = sat_u8(__float2int_rn(sum[c]));
     }
+    kstamp_end_wg(kstamp);
 }
 
 // INTER_AREA integer-scale path (resizeAreaFast): 2x2 => (sum+2)>>2,
 // otherwise cvRound(sum * (1.f/area)).
 __global__ __launch_bounds__(256) void k_resize_area_fast(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                           int H, int W, int h, int w, int sx, int sy, float inv_area) {
+                                                           int H, int W, int h, int w, int sx, int sy, float inv_area,
+                                                           uint64_t* kstamp) {
+    kstamp_begin_grid(kstamp);
     const size_t f = blockIdx.y;
     const int n = h * w * 3;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const int c = e % 3, dx = (e / 3) % w, dy = e / (3 * w);
-    const uint8_t* S = src + f * (size_t)H * W * 3;
-    int sum = 0;
-    for (int yy = 0; yy < sy; yy++)
-        for (int xx = 0; xx < sx; xx++) sum += S[((size_t)(dy * sy + yy) * W + (dx * sx + xx)) * 3 + c];
-    const int v = (sx == 2 && sy == 2) ? ((sum + 2) >> 2) : __float2int_rn(__fmul_rn((float)sum, inv_area));
-    dst[f * (size_t)n + e] = sat_u8(v);
+    if (e < n) {
+        const int c = e % 3, dx = (e / 3) % w, dy = e / (3 * w);
+        const uint8_t* S = src + f * (size_t)H * W * 3;
+        int sum = 0;
+        for (int yy = 0; yy < sy; yy++)
+            for (int xx = 0; xx < sx; xx++) sum += S[((size_t)(dy * sy + yy) * W + (dx * sx + xx)) * 3 + c];
+        const int v = (sx == 2 && sy == 2) ? ((sum + 2) >> 2) : __float2int_rn(__fmul_rn((float)sum, inv_area));
+        dst[f * (size_t)n + e] = sat_u8(v);
+    }
+    kstamp_end_wg(kstamp);
 }
 
 hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W, int h, int w,
                               const int32_t* xofs, const int32_t* xcnt, const float* xwt, int xtaps,
                               const int32_t* yofs, const int32_t* ycnt, const float* ywt, int ytaps,
-                              const uint8_t* const* srcs) {
+                              const uint8_t* const* srcs, uint64_t* kstamp) {
     const int nt = (xtaps + 1) & ~1;
     if (nt <= 32 && (size_t)3 * W * H < (1u << 31)) {
         const dim3 g((h * w + RN_T - 1) / RN_T, F);
@@ -290,7 +301,7 @@ hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, 
 #define RN_CASE(N)                                                                                                      \
     case N:                                                                                                            \
         hipLaunchKernelGGL(k_resize_area_nt<N>, g, dim3(RN_T), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs, \
-                           ycnt, ywt, ytaps, srcs);                                                                    \
+                           ycnt, ywt, ytaps, srcs, kstamp);                                                            \
         break;
             RN_CASE(2) RN_CASE(4) RN_CASE(6) RN_CASE(8) RN_CASE(10) RN_CASE(12) RN_CASE(14) RN_CASE(16)
             RN_CASE(18) RN_CASE(20) RN_CASE(22) RN_CASE(24) RN_CASE(26) RN_CASE(28) RN_CASE(30) RN_CASE(32)
@@ -306,20 +317,20 @@ hipError_t launch_resize_area(hipStream_t st, const uint8_t* src, uint8_t* dst, 
         const int bytes = 2 * rowb + w * xtaps * 4;
         (void)hipFuncSetAttribute((const void*)k_resize_area_rows, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         hipLaunchKernelGGL(k_resize_area_rows, grid, dim3(RS_T), bytes, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps,
-                           yofs, ycnt, ywt, ytaps);
+                           yofs, ycnt, ywt, ytaps, kstamp);
     } else {
         hipLaunchKernelGGL(k_resize_area, grid, dim3(256), 0, st, src, dst, H, W, h, w, xofs, xcnt, xwt, xtaps, yofs,
-                           ycnt, ywt, ytaps);
+                           ycnt, ywt, ytaps, kstamp);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_resize_area_fast(hipStream_t st, const uint8_t* src, uint8_t* dst, int F, int H, int W, int h,
-                                   int w, int sx, int sy) {
+                                   int w, int sx, int sy, uint64_t* kstamp) {
     const int n = h * w * 3;
     dim3 grid((n + 255) / 256, F);
     const float inv_area = 1.f / (float)(sx * sy);
-    hipLaunchKernelGGL(k_resize_area_fast, grid, dim3(256), 0, st, src, dst, H, W, h, w, sx, sy, inv_area);
+    hipLaunchKernelGGL(k_resize_area_fast, grid, dim3(256), 0, st, src, dst, H, W, h, w, sx, sy, inv_area, kstamp);
     return hipGetLastError();
 }
 

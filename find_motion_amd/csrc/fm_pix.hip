@@ -28,24 +28,11 @@ namespace fm {
 namespace px {
 
 constexpr int TS = 64;          // tile edge
-// minimum waves per SIMD the steady-state variants are compiled for (2 workgroups of
-// 8 waves per CU = 4 per SIMD: <= 128 VGPRs)
-#ifndef FM_PIX_WPE
-#define FM_PIX_WPE 4
-#endif
-#ifndef FM_PIX_WPE_LARGE
-#define FM_PIX_WPE_LARGE 1  // k = 21: no register cap (178 VGPRs, one workgroup per CU)
-#endif
-#ifndef FM_PIX_NT
-#define FM_PIX_NT 512
-#endif
-#ifndef FM_PIX_PRIO
-#define FM_PIX_PRIO 0
-#endif
-#ifndef FM_PIX_ABL
-#define FM_PIX_ABL 0  // timing ablations of the chain (results invalid): 1 f64 update, 2 absdiff, 4 ballot
-#endif
-constexpr int NT = FM_PIX_NT;   // threads
+// minimum waves per SIMD the steady-state kernels are compiled for: 2 workgroups of 8 waves per CU =
+// 4 per SIMD (<= 128 VGPRs).  (6 per SIMD, three k_pix5 workgroups per CU: 366 vs 401 k frames/s,
+// round 4.)  k_pix<21> has no cap (178 VGPRs, one workgroup per CU).
+constexpr int kPixWPE = 4;
+constexpr int NT = 512;         // threads
 constexpr int NW = NT / 64;     // waves; wave w owns tile rows [8w, 8w + 8)
 constexpr int RPWV = TS / NW;   // rows per wave in the chain stage
 static_assert(NW == 8, "tflag holds 8 words per tile (FusedArgs::tflag_waves)");
@@ -213,29 +200,8 @@ __device__ __forceinline__ int swizzle_tile(int b, int n) {
     return (b & 7) * (full >> 3) + (b >> 3);
 }
 
-// XCD-aware 2-D order (round 4): as swizzle_tile, XCD x takes the x-th eighth of the tiles, but in
-// super-tile order -- 8 x 8 tile blocks, row-major over the blocks, row-major inside them (clipped at
-// the grid's right and bottom edges) -- so the 64 workgroups an XCD holds at once (2 per CU) form one
-// 8 x 8 block: their vertical halos are each other's rows too, read through that XCD's L2, where a
-// row-major run of 64 tiles shares only the horizontal ones.  A bijection on [0, ntx * nty).
-__device__ __forceinline__ int block_tile(int b, int ntx, int nty) {
-    const int full = (ntx * nty) & ~7;
-    const int j = b >= full ? b : (b & 7) * (full >> 3) + (b >> 3);  // place in super-tile order
-    const int sr = j / (8 * ntx), R = min(8, nty - 8 * sr);           // super-row, its tile rows
-    const int i = j - sr * 8 * ntx;
-    const int c8 = i / (8 * R), rem = i - 8 * R * c8;                 // column block (the last may be narrower)
-    const int wb = min(8, ntx - 8 * c8);
-    const int r = rem / wb, cc = rem - r * wb;
-    return (8 * sr + r) * ntx + 8 * c8 + cc;
-}
-#ifndef FM_PIX_ORDER
-#define FM_PIX_ORDER 0  // tile order of k_pix5 / k_pixw: 1 = block_tile (2-D), 0 = swizzle_tile (row-major runs).
-                        // Measured (round 4, 2 alternating rounds): k_pixw at config 5 3.19 / 3.33 ms per launch
-                        // (row-major / 2-D), the driver's line 406.6 / 401.6 k frames/s: row-major stays
-#endif
-__device__ __forceinline__ int pix_tile(int b, const FusedArgs& a) {
-    return FM_PIX_ORDER ? block_tile(b, a.ntx, a.nty) : swizzle_tile(b, a.ntiles);
-}
+// (A 2-D order -- each XCD's 64 resident workgroups as an 8 x 8 tile block, so that vertical halos
+// also come through its L2 -- measured slower, round 4: config 5 3.33 vs 3.19 ms per launch.)
 
 // OpenCV's 8-bit fixed-point Gaussian taps (getGaussianKernelBitExact +
 // error-diffusion rounding, restated in fm_capi.cpp gaussian_taps); fixed at
@@ -258,23 +224,13 @@ template <int K> constexpr uint32_t tap2(int t) {
     return (uint32_t)Taps<K>::c[2 * t] | (2 * t + 1 < K ? (uint32_t)Taps<K>::c[2 * t + 1] << 16 : 0u);
 }
 
-#ifndef FM_PIX_FMA_INPLACE
-#define FM_PIX_FMA_INPLACE 1
-#endif
-#ifndef FM_PIX_SADDR
-#define FM_PIX_SADDR 1
-#endif
 // accumulateWeighted's bg = fma(bg, beta, blur * alpha) updating the background register in place.
 // As __fma_rn the compiler picks v_fmac_f64 accumulating into the register of the table read, so
 // every loop-carried background value went through a v_mov_b64 at the top of the frame loop
 // (8 of the chain's ~95 VALU instructions per wave-frame).
 __device__ __forceinline__ double bg_fma(double b, double beta, double bl) {
-#if FM_PIX_FMA_INPLACE
     asm("v_fma_f64 %0, %0, %1, %2" : "+v"(b) : "s"(beta), "v"(bl));
     return b;
-#else
-    return __fma_rn(b, beta, bl);
-#endif
 }
 
 // A frame's base address in SGPRs, so the quad loads take the saddr form (SGPR base + the lane's
@@ -289,27 +245,14 @@ __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) 
     typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
     d = *(const __attribute__((address_space(1))) u3a*)(base + off);
 }
-// FM_P5_BUFLD / FM_PW_BUFLD: the quad loads of k_pix5 / k_pixw as buffer loads through a per-frame
-// descriptor built from wave-uniform values (frame base and size in SGPRs): the lane's 32-bit offset is
-// the whole per-lane address, so the 64-bit add per load (v_lshl_add_u64) is gone.
-// FM_P5_SDWA / FM_PW_SDWA: the blur x alpha table as static LDS at address 0, its byte offset from the
-// accumulator by ONE SDWA shift (byte 2 of acc times 8) instead of v_bfe_u32 + v_lshl_add_u32 (the
-// dynamic LDS array's base is a link-time symbol the compiler adds to every index).
-// Measured (round 4, 3 alternating rounds of the driver's command and 2 of config 5): both on in
-// k_pix5 cost 3.4 % (396.0 vs 410.1 k frames/s, pixel launches 612-653 vs 556-629 us); both on in
-// k_pixw gain 1.9 % (80.9 vs 79.5 k frames/s, 3.07-3.12 vs 3.16-3.17 ms per launch).
-#ifndef FM_P5_BUFLD
-#define FM_P5_BUFLD 0
-#endif
-#ifndef FM_P5_SDWA
-#define FM_P5_SDWA 0
-#endif
-#ifndef FM_PW_BUFLD
-#define FM_PW_BUFLD 1
-#endif
-#ifndef FM_PW_SDWA
-#define FM_PW_SDWA 1
-#endif
+// k_pixw's quad loads are buffer loads through a per-frame descriptor built from wave-uniform values
+// (frame base and size in SGPRs): the lane's 32-bit offset is the whole per-lane address, so the 64-bit
+// add per load (v_lshl_add_u64) is gone; and its blur x alpha table is static LDS at address 0, its byte
+// offset from the accumulator by ONE SDWA shift (byte 2 of acc times 8) instead of v_bfe_u32 +
+// v_lshl_add_u32 (the dynamic LDS array's base is a link-time symbol the compiler adds to every index).
+// Measured (round 4, 3 alternating rounds of the driver's command and 2 of config 5): both in k_pixw
+// gain 1.9 % (80.9 vs 79.5 k frames/s, 3.07-3.12 vs 3.16-3.17 ms per launch); both in k_pix5 cost 3.4 %
+// (396.0 vs 410.1 k frames/s), which keeps global loads and the dynamic table.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* p, uint32_t bytes) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
@@ -320,14 +263,10 @@ __device__ __forceinline__ void load12b(u32x3_t& d, __amdgpu_buffer_rsrc_t r, ui
     d = __builtin_bit_cast(u32x3_t, __builtin_amdgcn_raw_buffer_load_b96(r, (int)off, 0, 0));
 }
 __device__ __forceinline__ gbytes_t frame_base(const uint8_t* p) {
-#if FM_PIX_SADDR
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
     uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
     asm volatile("" : "+s"(lo), "+s"(hi));
     return (gbytes_t)(((uint64_t)hi << 32) | lo);
-#else
-    return (gbytes_t)reinterpret_cast<uintptr_t>(p);
-#endif
 }
 
 // Per-frame, per-wave constants of the chain stage (computed once per tile).
@@ -345,8 +284,7 @@ struct ChainCtx {
 // fm.py:651-652); `init` says whether this frame is one.  KEEP: apply the
 // keep-mask bytes (off when the stream has no mask).  TAIL: the wave's rows reach
 // accumulateWeighted's scalar tail (per-pixel test of the product order).
-// HPAIR: H is stored as row pairs (k_pix5): u32 [pair][64 columns] = H[2p][c] | H[2p+1][c] << 16
-template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL, bool HPAIR = false>
+template <int KC, bool PLANES, bool INIT, bool KEEP, bool TAIL>
 __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* Hs, const double* atab, const Geo& g,
                                            double (&bg)[RPWV],
                                            int wv, int ln, int x0, int y0, size_t f, const ChainCtx& cc,
@@ -357,12 +295,7 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
     const int w = a.w;
     // column ln of H, rows 8*wv .. 8*wv + NV - 1, as u16 pairs (ds_read_u16_d16 / _d16_hi)
     uint32_t P[NP + 1];
-    if (HPAIR) {  // one ds_read_b32 per row pair
-        const uint32_t* col = reinterpret_cast<const uint32_t*>(Hs) + (RPWV / 2 * wv) * TS + ln;
-#pragma unroll
-        for (int i = 0; i < NP; i++) P[i] = col[i * TS];
-        P[NP] = 0;
-    } else {
+    {
         const uint16_t* col = Hs + (RPWV * wv) * g.RSH + ln;
 #pragma unroll
         for (int i = 0; i < NP; i++) {
@@ -399,25 +332,13 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
         if (INIT && init) b = (double)blur;
         // convertScaleAbs: f64 -> f32 (rne), |.|, rne, saturate to u8 -- into byte 2 of a copy
         // of acc, so that the byte-wise absdiff of the two words is |blur - q|
-#if FM_PIX_ABL & 2  // timing ablation only (results invalid): no convertScaleAbs / absdiff
-        const uint32_t r = (acc >> 16) + bias;
-#else
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
         const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);  // absdiff + bias
-#endif
-#if !(FM_PIX_ABL & 4)  // timing ablation only: no threshold bits
         tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
-#endif
-#if FM_PIX_ABL & 1  // timing ablation only: no f64 background update
-        double nb = b + 0.0;
-        const double bl = 0.0;
-        (void)beta;
-#else
         // (double)blur * alpha from a 256-entry LDS table (the same correctly rounded product):
         // an LDS read instead of two f64-rate VALU ops per pixel
         const double bl = atab[blur];
         double nb = bg_fma(b, beta, bl);
-#endif
         if (TAIL) {  // accumulateWeighted's scalar tail: two products, one add there
             const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
             if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
@@ -447,7 +368,7 @@ __device__ __forceinline__ void chain_rows(const FusedArgs& a, const uint16_t* H
 }
 
 template <int KC, bool PLANES, bool INIT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && !INIT) ? (KC <= 7 ? FM_PIX_WPE : FM_PIX_WPE_LARGE) : 1))) void k_pix(FusedArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && !INIT && KC <= 7) ? kPixWPE : 1))) void k_pix(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = KC >> 1;
     const Geo g(R);
@@ -461,6 +382,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
     const int ti = swizzle_tile(blockIdx.x, a.ntiles);
+    kstamp_begin(a.kstamp);
     // profiling only (FM_PTS): [hw_id | xcc_id << 32, realtime start, realtime end, memtime cycles]
     uint64_t* pts = (a.dbg_pts && tid == 0) ? a.dbg_pts + ((size_t)s * a.ntiles + ti) * 4 : nullptr;
     uint64_t rt0 = 0, mt0 = 0;
@@ -668,18 +590,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
         for (int t = t0; t < t1; t++) {
             const int b = (t - t0) & 1;
             const size_t f = (size_t)t * S + s;
-#if FM_PIX_PRIO
-            // two workgroups share each CU; by age the first-dispatched one wins issue and the
-            // second finishes alone at one wave per SIMD.  Priority falling with progress keeps
-            // the pair within a quarter batch of each other.
-            {
-                const int q4 = ((t - t0) * 4) / (t1 - t0);
-                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
-                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
-                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-#endif
             if (t + 1 < t1) {
                 if (!(skip & 8)) stage_raw(Rw, b ^ 1);
                 if (t + 2 < t1 && !(skip & 4)) load_raw(Rw, a.src + (f + 2 * S) * fbytes, fb32, plan, span);
@@ -722,6 +632,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu((!PLANES && 
         const int y = y0 + RPWV * wv + j;
         if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
+    kstamp_end(a.kstamp);
     if (pts) {
         const uint64_t rt = __builtin_amdgcn_s_memrealtime(), mt = __builtin_amdgcn_s_memtime();
         pts[1] = rt0;
@@ -745,10 +656,11 @@ template <int K> constexpr int tap_hi() {
     return i;
 }
 
-// NWB: waves of the workgroup, each over 8 rows: NWB = 8 the 64 x 64 tile, NWB = 16 a 64-wide, 128-row
-// band (two contour tiles: the 2R-row vertical halo is read once per 128 rows instead of per 64)
-template <int KC, int NWB = 8>
+// One 64 x 64 tile per workgroup of 8 waves, each over 8 rows.  (A 64-wide, 128-row band of 16 waves, its
+// 2R-row vertical halo read once per 128 rows: 3.61 vs 3.33 ms per config-5 launch, round 4.)
+template <int KC>
 struct PW {
+    static constexpr int NWB = 8;
     static constexpr int R = KC / 2;
     static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
     static constexpr int NTB = 64 * NWB;           // threads
@@ -780,7 +692,7 @@ struct PW {
     }
     static constexpr int NP = np_max();            // pairs a wave's chain reads
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 4 + 256 * 8;
-    static constexpr int dyn_bytes = bytes - (FM_PW_SDWA ? 256 * 8 : 0);  // (FM_PW_SDWA: the table is static LDS)
+    static constexpr int dyn_bytes = bytes - 256 * 8;  // (k_pixw: the table is static LDS)
 };
 template <int KC> constexpr uint32_t tapw4(int g) {  // dot4 group g of the non-zero taps
     uint32_t v = 0;
@@ -798,12 +710,12 @@ template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of o
 // chain_rows over H row pairs with even-aligned pair windows: output row j's window starts on an
 // even H row, absorbing a zero tap (outside the kernel, or one of OpenCV's zero end taps) on the
 // side the row parity needs, so no pair is rebuilt with v_alignbit
-// wv: the wave within its workgroup (H rows, image rows); wb: its 8-row slice of the 64-row contour
-// tile (flag rows: FLAG_T* from slice 0, FLAG_B* from slice 7) -- the same as wv for a 64-row workgroup
+// wv: the wave within its workgroup = its 8-row slice of the 64-row tile (flag rows: FLAG_T* from slice 0,
+// FLAG_B* from slice 7)
 template <int KC, bool KEEP, bool TAIL, bool SDWA>
 __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
                                              int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
-                                             uint32_t& flags, int wb) {
+                                             uint32_t& flags) {
     using G = PW<KC>;
     uint32_t P[G::NP];
     const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
@@ -847,15 +759,14 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     tb &= cc.tbmask;
     colbits = tb;
     const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
-    const uint64_t top = wb == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
-    const uint64_t bot = wb == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
+    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
     uint32_t fl = 0;
     if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
-    if (wb == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
-    if (wb == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
     flags = fl;
 }
-
 
 // Horizontal taps with the byte window folded into the constants: output k of a quad sums its
 // taps over window bytes [B0 + k, B0 + k + NTAPS) of the row's gray dwords; instead of shifting
@@ -925,57 +836,34 @@ __device__ __forceinline__ uint32_t hs_tap(const uint32_t (&q)[N], const uint32_
 // quad just outside the image from the mirrored quad beside it (REFLECT_101).
 // Needs w % 4 == 0 and w >= 8 (4-B aligned quads, one real quad each side);
 // one barrier per frame as in k_pix.
-#ifndef FM_P5_EVENP
-#define FM_P5_EVENP 1  // k_pix5's chain on even-aligned pair windows (chain_rows_w)
-#endif
-#ifndef FM_P5_GFAST
-#define FM_P5_GFAST 4  // (A/B: 4 >= 3 > 5)
-#endif
-// Tap jobs cover 2 H rows x 4 columns and store them as row pairs (one ds_write_b128), which the chain
-// reads back as six dwords instead of twelve u16 reads and their merges (FM_P5_HPAIR 0: 1 x 4 jobs,
-// row-major H, as k_pix)
-#ifndef FM_P5_HPAIR
-#define FM_P5_HPAIR 1
-#endif
-// tap jobs likewise (FM_P5_HFAST slots to each of waves 0..3); 0 keeps the round-robin deal
-#ifndef FM_P5_HFAST
-#define FM_P5_HFAST 0
-#endif
-// k_pix5 geometry for a workgroup of NWB waves over a band of 8 * NWB tile rows (NWB = 8: the 64 x 64
-// tile; small work images -- mode D's 100 x 56 is two tiles -- take bands of 8 or 16 rows so that more
-// workgroups share the per-frame critical path)
-template <int NWB>
+// The chain runs on even-aligned pair windows (chain_rows_w); tap jobs cover 2 H rows x 4 columns and store
+// them as row pairs (one ds_write_b128), which the chain reads back as six dwords instead of twelve u16
+// reads and their merges; the horizontal taps take shifted constants (HS).
 struct P5G {
+    static constexpr int NWB = 8;                        // waves of a tile
     static constexpr int NTB = 64 * NWB;                 // threads
-    static constexpr int TH = RPWV * NWB;                // band rows
+    static constexpr int TH = RPWV * NWB;                // tile rows
     static constexpr int GH = TH + 4;                    // gray rows y0-2 .. y0+TH+1
     static constexpr int GQ = 18;                        // gray quads per row: columns x0-4 .. x0+67
     static constexpr int NG = GH * GQ;                   // gray jobs per frame
-    // Gray jobs go to waves in whole wave-slots of 64 jobs.  In a 64-row workgroup waves 4..7 lose issue
-    // arbitration to waves 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves
-    // 0..3 spent ~30 % of their cycles in the barrier), so waves 0..3 take GFAST slots each and waves
-    // 4..7 the rest; the partial last slot goes to wave 3.  Narrower bands deal them round robin.
+    // Gray jobs go to waves in whole wave-slots of 64 jobs.  Waves 4..7 lose issue arbitration to waves
+    // 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves 0..3 spent ~30 % of
+    // their cycles in the barrier), so waves 0..3 take GFAST slots each and waves 4..7 the rest; the
+    // partial last slot goes to wave 3.  (GFAST A/B: 4 >= 3 > 5.)
     static constexpr int GSLOTS = (NG + 63) / 64;
-    static constexpr int GFAST = NWB == 8 ? FM_P5_GFAST : (GSLOTS + NWB - 1) / NWB;
-    static constexpr int GSLOW = NWB == 8 ? (GSLOTS - 4 * GFAST + 3) / 4 : GFAST;
+    static constexpr int GFAST = 4;
+    static constexpr int GSLOW = (GSLOTS - 4 * GFAST + 3) / 4;
     static constexpr int GJ = GFAST > GSLOW ? GFAST : GSLOW;  // load rounds per wave
-    static constexpr int HR = FM_P5_HPAIR ? 2 : 1;       // H rows per tap job
-    static constexpr int NH = (GH / HR) * (TS / 4);      // tap jobs per frame
-    static constexpr int HFAST = NWB == 8 ? FM_P5_HFAST : 0;
-    static constexpr int HSLOTS = (NH + 63) / 64;
-    static constexpr int HSLOW = HFAST ? (HSLOTS - 4 * HFAST + 3) / 4 : 0;
-    static constexpr int HJ = HFAST ? (HFAST > HSLOW ? HFAST : HSLOW) : (NH + NTB - 1) / NTB;
+    static constexpr int NH = (GH / 2) * (TS / 4);       // tap jobs per frame
+    static constexpr int HJ = (NH + NTB - 1) / NTB;
     // the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
     static constexpr int HLASTW = (NH - (HJ - 1) * NTB + 63) / 64;
     static constexpr int GBUF = NG + 64;                 // + a pad slot per lane for the idle jobs' stores (branch-free)
-    static constexpr int HROW = TS;                      // u16 per H row
-    static constexpr int HBUF = (GH + HR) * HROW;        // + the pad row (pair) idle tap jobs store to
+    static constexpr int HBUF = (GH + 2) * TS;           // u16; + the pad pair row idle tap jobs store to
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
-    static constexpr int dyn_bytes = bytes - (FM_P5_SDWA ? 256 * 8 : 0);  // (FM_P5_SDWA: the table is static LDS)
+    static constexpr int dyn_bytes = bytes;
 };
-static_assert(P5G<8>::GSLOW >= 0 && 4 * (P5G<8>::GFAST + P5G<8>::GSLOW) >= P5G<8>::GSLOTS, "gray slots");
-static_assert(!P5G<8>::HFAST || (P5G<8>::HSLOW >= 0 && 4 * (P5G<8>::HFAST + P5G<8>::HSLOW) >= P5G<8>::HSLOTS), "tap slots");
-template <int NWB> constexpr int p5_lds_bytes() { return P5G<NWB>::bytes; }
+static_assert(P5G::GSLOW >= 0 && 4 * (P5G::GFAST + P5G::GSLOW) >= P5G::GSLOTS, "gray slots");
 
 template <int GJ>
 struct P5Raw {
@@ -986,80 +874,41 @@ struct P5Raw {
 // accumulateWeighted's scalar tail (h*w % 16 != 0), so some waves take the per-pixel test.  Fixed
 // per launch, so the common kernel has a single chain path: a per-wave 3-way branch inside the
 // frame loop made the background registers a phi and cost 8 v_mov_b64 per frame.
-// PAIR = 2: one 1,024-thread workgroup runs two neighbouring 64 x 64 tiles (waves 0-7 and 8-15, each half
-// with its own LDS) in step, sharing the frame barrier.  With two 8-wave workgroups per CU the older
-// one's waves win issue arbitration, it finishes first and the younger runs its last frames alone
-// at half occupancy (FM_PTS, round 4: 254 of 510 workgroups end ~120 us after the median); a shared
-// barrier keeps both tiles of a CU at the same frame.
-template <int NWB>
-constexpr int p5_half_bytes() { return (P5G<NWB>::dyn_bytes + 15) & ~15; }
 // SPL (small work images, e.g. mode D's 100 x 56: two tiles, 256 frames in a row): 16 waves per tile,
 // waves 0-7 run the chain of their 8 rows and waves 8-15 the taps, gray and loads of the next frames, so a
-// frame's critical path is the longer of the two halves instead of their sum.
-template <int NWB, bool KEEP, bool TAIL, int PAIR = 1, bool SPL = false, int NPW = 8>
-__global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute__((amdgpu_waves_per_eu(FM_PIX_WPE))) void k_pix5(FusedArgs a) {
-    using G = P5G<NWB>;
+// frame's critical path is the longer of the two halves instead of their sum.  (The same split on full
+// grids, 8 chain + 4 producer waves: 375 vs 407 k frames/s, round 4 -- there the CU is issue-bound.)
+// Measured and withdrawn (round 4): 8- / 16-row bands for small images, two tiles per 1,024-thread
+// workgroup sharing the frame barrier, issue priority falling with progress.
+template <bool KEEP, bool TAIL, bool SPL = false>
+__global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
+    using G = P5G;
+    constexpr int NPW = 8;  // SPL: producer waves
     // job rounds per wave: SPL deals the gray slots and tap jobs over the NPW producer waves only
     constexpr int GJX = SPL ? (G::GSLOTS + NPW - 1) / NPW : G::GJ;
     constexpr int HJX = SPL ? (G::NH + 64 * NPW - 1) / (64 * NPW) : G::HJ;
     constexpr int HLASTX = SPL ? (G::NH - (HJX - 1) * 64 * NPW + 63) / 64 : G::HLASTW;
-    static_assert(FM_P5_EVENP || NWB == 8, "bands need the even-pair chain (its flag rows follow wb)");
-    static_assert(PAIR == 1 || (NWB == 8 && FM_P5_SDWA == 0), "tile pairs: 64-row tiles, the table in each half's LDS");
-    static_assert(!SPL || (NWB == 8 && PAIR == 1), "split waves: 64-row tiles, one tile per workgroup");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_all[];
-    const int half = PAIR > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (64 * NWB)) : 0;
-    uint8_t* smem = smem_all + half * p5_half_bytes<NWB>();
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
-    double* atab;  // blur x alpha (f64): static LDS at address 0 with FM_P5_SDWA, else behind H
-    if constexpr (FM_P5_SDWA != 0) {
-        __shared__ double atab_s[256];
-        atab = atab_s;
-    } else {
-        atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);
-    }
-    const int tid = PAIR > 1 ? (int)threadIdx.x % (64 * NWB) : (int)threadIdx.x, ln = tid & 63;  // (within the tile)
+    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);  // blur x alpha (f64)
+    const int tid = (int)threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool cw = !SPL || wv < 8;  // SPL: a chain wave (0-7) or a producer (8-15: pw = wv - 8)
     const int pw = wv - 8, ptid = tid - 512;
-#ifndef FM_P5_SPL_PRIO
-#define FM_P5_SPL_PRIO 0  // SPL: issue priority of the (latency-bound) small-image waves over the resize's beside them
-#endif
-    if constexpr (SPL && FM_P5_SPL_PRIO > 0) __builtin_amdgcn_s_setprio(FM_P5_SPL_PRIO);
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
-    int ti, tx, y0, wb0;  // contour tile, its column, the band's first row, its first 8-row slice of the tile
-    if constexpr (PAIR > 1) {
-        ti = 2 * swizzle_tile(blockIdx.x, a.ntiles / 2) + half;
-        tx = ti % a.ntx;
-        y0 = (ti / a.ntx) * TS;
-        wb0 = 0;
-    } else if constexpr (NWB == 8) {
-        ti = pix_tile(blockIdx.x, a);
-        tx = ti % a.ntx;
-        y0 = (ti / a.ntx) * TS;
-        wb0 = 0;
-    } else {
-        // the bands tile every contour tile whole: the slices of the last tile below the image are
-        // written as zeros (no bits, no flags) as the 64-row kernel writes them, not left stale
-        const int nby = a.nty * (TS / G::TH);
-        const int bt = FM_PIX_ORDER ? block_tile(blockIdx.x, a.ntx, nby) : swizzle_tile(blockIdx.x, a.ntx * nby);
-        tx = bt % a.ntx;
-        y0 = (bt / a.ntx) * G::TH;
-        ti = (y0 / TS) * a.ntx + tx;
-        wb0 = (y0 % TS) / RPWV;
-    }
+    const int ti = swizzle_tile(blockIdx.x, a.ntiles);  // contour tile
+    const int tx = ti % a.ntx;
+    const int y0 = (ti / a.ntx) * TS;
     const int x0 = tx * TS;
     const size_t plane = (size_t)h * w;
     const size_t fbytes = plane * 3;
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
-    if constexpr (NWB >= 4) {
-        if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
-    } else {
-        for (int i = tid; i < 256; i += G::NTB) atab[i] = __dmul_rn((double)i, a.alpha);
-    }
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+    kstamp_begin(a.kstamp);
 #ifdef FM_DEV_SWITCHES
     // profiling only (FM_PTS, dev build): [hw_id | xcc_id << 32, realtime start, realtime end, memtime cycles]
     uint64_t* pts = (a.dbg_pts && tid == 0) ? a.dbg_pts + ((size_t)s * a.ntiles + ti) * 4 : nullptr;
@@ -1074,13 +923,11 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
     // ---- per-thread job plans (frame invariant)
     uint32_t goff[GJX];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
     uint32_t gdst[GJX];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
-    // this wave's gray slots (wave-uniform): the 4 / 4 deal in a 64-row workgroup, contiguous runs in a band
-    const int gjobs = SPL ? (cw ? 0 : min(GJX, (G::GSLOTS - pw + NPW - 1) / NPW))
-                          : NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : max(0, min(G::GFAST, G::GSLOTS - wv * G::GFAST));
+    // this wave's gray slots (wave-uniform): the 4 / 4 deal, or SPL's producer waves in turn
+    const int gjobs = SPL ? (cw ? 0 : min(GJX, (G::GSLOTS - pw + NPW - 1) / NPW)) : (wv < 4 ? G::GFAST : G::GSLOW);
 #pragma unroll
     for (int i = 0; i < GJX; i++) {
-        const int slot = SPL ? pw + NPW * i
-                             : NWB == 8 ? (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i) : wv * G::GFAST + i;
+        const int slot = SPL ? pw + NPW * i : (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i);
         const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / G::GQ, gq = j - gr * G::GQ;
         const int x = x0 - 4 + 4 * gq;
@@ -1090,17 +937,14 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
         gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
     }
     uint32_t hsrc[HJX], hdst[HJX];
-    const int hjobs = SPL ? (cw ? 0 : HJX) : G::HFAST ? (wv < 4 ? G::HFAST : G::HSLOW) : G::HJ;  // this wave's tap rounds (wave-uniform)
+    const int hjobs = SPL ? (cw ? 0 : HJX) : G::HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
     for (int i = 0; i < HJX; i++) {
-        const int hslot = wv >= 4 ? (wv - 4) * G::HSLOW + i : 4 * G::HSLOW + wv * G::HFAST + i;
-        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : G::HFAST ? (i < hjobs ? hslot * 64 + ln : G::NH) : tid + G::NTB * i;
+        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
-        hsrc[i] = (uint32_t)(G::HR * hr * G::GQ + hq);
-        // FM_P5_HPAIR: u32 index of the pair's 4 columns, else u16 index of the row's
-        hdst[i] = FM_P5_HPAIR ? (uint32_t)((live ? hr : G::GH / 2) * TS + 4 * hq)
-                              : (uint32_t)((live ? hr : G::GH) * G::HROW + 4 * hq);
+        hsrc[i] = (uint32_t)(2 * hr * G::GQ + hq);
+        hdst[i] = (uint32_t)((live ? hr : G::GH / 2) * TS + 4 * hq);  // u32 index of the pair's 4 columns
     }
     // REFLECT_101 quads: left of column 0 (tile x0 = 0, tap quad 0 reads gray quad 0 = columns -4..-1:
     // bytes 2, 3 = gray(2), gray(1) from quad 1) and the quad starting at column w (bytes 0, 1 =
@@ -1142,31 +986,17 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
     for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
     asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
 
-#ifndef FM_HSHIFT
-#define FM_HSHIFT 1  // horizontal taps with shifted constants (HS) instead of v_alignbyte windows
-#endif
-    uint32_t cpk[2];
-    cpk[0] = tap4<KC>(0);
-    cpk[1] = tap4<KC>(1);
     uint32_t hcs[HS<KC>::NC];
-    if (FM_HSHIFT) hs_consts<KC>(hcs);
+    hs_consts<KC>(hcs);
     P5Raw<GJX> rw;
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        if constexpr (FM_P5_BUFLD != 0) {
-            const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
+        const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
-            for (int i = 0; i < GJX; i++) load12b(rw.v[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
-        } else {
-            const gbytes_t src = frame_base(a.src + f * fbytes);
-#pragma unroll
-            for (int i = 0; i < GJX; i++) {
-                load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
-            }
-        }
+        for (int i = 0; i < GJX; i++) load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
@@ -1178,8 +1008,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < HJX; i++) {
-            if (SPL ? (i >= hjobs || (i == HJX - 1 && pw >= HLASTX))
-                    : G::HFAST ? i >= hjobs : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
+            if (SPL ? (i >= hjobs || (i == HJX - 1 && pw >= HLASTX)) : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
             if (edge_tile) {
@@ -1188,41 +1017,26 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
                 if (hfix[i] & 4) qv[2] = __builtin_amdgcn_perm(qv[1], qv[1], 0x00000102u);
             }
             // outputs x0+4q+k, k = 0..3: taps over gray columns x0+4q+k-2 .. +2 = bytes k+2 .. k+6 of qv
-            const uint32_t h0 = FM_HSHIFT ? hs_tap<KC, 0>(qv, hcs) : htap<0, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h1 = FM_HSHIFT ? hs_tap<KC, 1>(qv, hcs) : htap<1, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h2 = FM_HSHIFT ? hs_tap<KC, 2>(qv, hcs) : htap<2, 2, 2, 0, 4>(qv, cpk, 0u);
-            const uint32_t h3 = FM_HSHIFT ? hs_tap<KC, 3>(qv, hcs) : htap<3, 2, 2, 0, 4>(qv, cpk, 0u);
-            if (FM_P5_HPAIR) {  // the next gray row, then both rows' sums as row pairs
-                uint32_t qw[4] = {gb[hsrc[i] + G::GQ], gb[hsrc[i] + G::GQ + 1], gb[hsrc[i] + G::GQ + 2], 0u};
-                if (edge_tile) {
-                    if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
-                    if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
-                    if (hfix[i] & 4) qw[2] = __builtin_amdgcn_perm(qw[1], qw[1], 0x00000102u);
-                }
-                const uint32_t k0 = FM_HSHIFT ? hs_tap<KC, 0>(qw, hcs) : htap<0, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k1 = FM_HSHIFT ? hs_tap<KC, 1>(qw, hcs) : htap<1, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k2 = FM_HSHIFT ? hs_tap<KC, 2>(qw, hcs) : htap<2, 2, 2, 0, 4>(qw, cpk, 0u);
-                const uint32_t k3 = FM_HSHIFT ? hs_tap<KC, 3>(qw, hcs) : htap<3, 2, 2, 0, 4>(qw, cpk, 0u);
-                *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
-                    make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
-            } else {
-                *reinterpret_cast<uint2*>(Hb + hdst[i]) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+            const uint32_t h0 = hs_tap<KC, 0>(qv, hcs);
+            const uint32_t h1 = hs_tap<KC, 1>(qv, hcs);
+            const uint32_t h2 = hs_tap<KC, 2>(qv, hcs);
+            const uint32_t h3 = hs_tap<KC, 3>(qv, hcs);
+            // the next gray row, then both rows' sums as row pairs
+            uint32_t qw[4] = {gb[hsrc[i] + G::GQ], gb[hsrc[i] + G::GQ + 1], gb[hsrc[i] + G::GQ + 2], 0u};
+            if (edge_tile) {
+                if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
+                if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
+                if (hfix[i] & 4) qw[2] = __builtin_amdgcn_perm(qw[1], qw[1], 0x00000102u);
             }
+            const uint32_t k0 = hs_tap<KC, 0>(qw, hcs);
+            const uint32_t k1 = hs_tap<KC, 1>(qw, hcs);
+            const uint32_t k2 = hs_tap<KC, 2>(qw, hcs);
+            const uint32_t k3 = hs_tap<KC, 3>(qw, hcs);
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
+                make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
         }
     };
-    const Geo g(R);
     const int t0 = a.t_begin, t1 = a.t_end;
-    // profiling-only stage ablation (dev build, FM_DEBUG_SKIP; results invalid): 1 gray, 2 chain,
-    // 4 loads, 8 taps.  A constant 0 in the product build: a runtime skip path around the loads or
-    // gray leaves loads unwaited on it, and the wait pass then stalls every frame on the stores
-#ifndef FM_P5_SKIP
-#define FM_P5_SKIP 0  // compile-time stage ablation (tools/ablate_p5c.sh)
-#endif
-#ifdef FM_DEV_SKIP  // runtime FM_DEBUG_SKIP (changes the code shape; tools/ablate_p5c.sh does it at compile time)
-    const int skip = __builtin_amdgcn_readfirstlane(a.dbg_skip);
-#else
-    constexpr int skip = FM_P5_SKIP;
-#endif
     // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
     // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
     // unconditional, frame indices clamped to the batch (see load).
@@ -1239,27 +1053,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
-#ifndef FM_P5_PRIO
-#define FM_P5_PRIO 0  // issue priority of the pixel waves against the contour pass's (fm_ccl.hip FM_*_PRIO)
-#endif
-    if (FM_P5_PRIO) __builtin_amdgcn_s_setprio(FM_P5_PRIO);
-#ifndef FM_P5_PHASES
-#define FM_P5_PHASES 1  // dev build: FM_PTS also takes the per-wave phase cycles (0: workgroup stamps only)
-#endif
-#if defined(FM_DEV_SWITCHES) && FM_P5_PHASES
-    // profiling (FM_PTS, dev build): per-wave cycles in the frame barrier, chain, taps, gray+stores+loads
-    uint64_t* phw = (a.dbg_pts && wv < NW) ? a.dbg_pts + (size_t)a.S * a.ntiles * 4 + (((size_t)s * a.ntiles + ti) * NW + wv) * 4 : nullptr;
-    uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, tA = __builtin_amdgcn_s_memtime(), tB;
-#define P5_PH(acc) do { if (phw) { tB = __builtin_amdgcn_s_memtime(); acc += tB - tA; tA = tB; } } while (0)
-#else
-#define P5_PH(acc) do { } while (0)
-#endif
-#ifndef FM_P5_QPRIO
-#define FM_P5_QPRIO 0  // issue priority falling with progress (levels: FM_P5_QPRIO + 1), so that the younger of a
-                       // CU's two workgroups catches up with the older one instead of finishing alone
-#endif
     if constexpr (SPL) {
-        static_assert((FM_P5_EVENP != 0) && (FM_P5_HPAIR != 0), "split waves: the even-pair chain");
         if (cw) {  // chain waves: frame t's chain, its bits and flag word
             for (int t = t0; t < t1; t++) {
                 const int b = (t - t0) & 1;
@@ -1274,9 +1068,9 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
                 asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
                 const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
                 if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                    chain_rows_w<KC, KEEP, false, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
                 else
-                    chain_rows_w<KC, KEEP, true, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
+                    chain_rows_w<KC, KEEP, true, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
                 reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
                 if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
             }
@@ -1289,72 +1083,37 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
                 load((size_t)min(t + 3, t1 - 1) * S + s);
             }
         }
-    } else
-    for (int t = t0; t < t1; t++) {
-        const int b = (t - t0) & 1;
-        const size_t f = (size_t)t * S + s;
-        if constexpr (FM_P5_QPRIO > 0) {
-            if (((t - t0) & 15) == 0) {
-                const int lv = FM_P5_QPRIO - ((t - t0) * (FM_P5_QPRIO + 1)) / (t1 - t0);  // wave-uniform
-                if (lv >= 3) __builtin_amdgcn_s_setprio(3);
-                else if (lv == 2) __builtin_amdgcn_s_setprio(2);
-                else if (lv == 1) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
+    } else {
+        for (int t = t0; t < t1; t++) {
+            const int b = (t - t0) & 1;
+            const size_t f = (size_t)t * S + s;
+            lds_barrier();
+            uint32_t colbits = 0, fl = 0;
+            ChainCtx ccf = cc;
+            ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
+            int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
+            asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
+            var = __builtin_amdgcn_readfirstlane(var);
+            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+            const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
+            if (!TAIL || var == 0)
+                chain_rows_w<KC, KEEP, false, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            else
+                chain_rows_w<KC, KEEP, true, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
+            // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
+            // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
+            // makes every frame wait for the stores below before the next loads
+            gray_stage(gray + b * G::GBUF);
+            // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
+            // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
+            // the prefetch would be waited for with it
+            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            // unconditional (see load): past the batch's last frame it re-reads that frame
+            load((size_t)min(t + 3, t1 - 1) * S + s);
         }
-        P5_PH(ph3);
-        lds_barrier();
-        P5_PH(ph0);
-        uint32_t colbits = 0, fl = 0;
-        ChainCtx ccf = cc;
-        ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
-        int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
-        asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-        var = __builtin_amdgcn_readfirstlane(var);
-        asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-        // chain_rows reads H as row pairs (FM_P5_HPAIR) or as [row][RSH = 64] u16
-        const uint16_t* Hb = Hs + b * G::HBUF;
-        if (!(skip & 2)) {
-            if constexpr ((FM_P5_EVENP != 0) && (FM_P5_HPAIR != 0)) {
-                const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hb);
-                const int wbf = NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb0 + wv);
-                if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
-                else
-                    chain_rows_w<KC, KEEP, true, FM_P5_SDWA != 0>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wbf);
-            } else if (!TAIL || var == 0) {
-                chain_rows<KC, false, false, KEEP, false, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
-                                                                         colbits, fl);
-            } else {
-                chain_rows<KC, false, false, KEEP, true, FM_P5_HPAIR>(a, Hb, atab, g, bg, wvf, ln, x0f, y0f, f, ccf, false,
-                                                                        colbits, fl);
-            }
-        }
-        P5_PH(ph1);
-        if (t + 1 < t1 && !(skip & 8)) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
-        P5_PH(ph2);
-        // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
-        // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
-        // makes every frame wait for the stores below before the next loads
-        if (!(skip & 1)) gray_stage(gray + b * G::GBUF);
-        // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
-        // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
-        // the prefetch would be waited for with it
-        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wb0 + wv] = (uint8_t)colbits;
-        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wb0 + wv] = fl;
-        // unconditional (see load): past the batch's last frame it re-reads that frame
-        if (!(skip & 4)) load((size_t)min(t + 3, t1 - 1) * S + s);
     }
-#if defined(FM_DEV_SWITCHES) && FM_P5_PHASES
-    P5_PH(ph3);
-    if (phw && ln == 0) {
-        phw[0] = ph0;
-        phw[1] = ph1;
-        phw[2] = ph2;
-        phw[3] = ph3;
-    }
-#endif
-#undef P5_PH
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
@@ -1363,6 +1122,7 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
         const int y = y0 + RPWV * wv + j;
         if (cw && x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
+    kstamp_end(a.kstamp);
 #ifdef FM_DEV_SWITCHES
     if (pts) {
         const uint64_t rt = __builtin_amdgcn_s_memrealtime(), mt = __builtin_amdgcn_s_memtime();
@@ -1388,64 +1148,39 @@ __global__ __launch_bounds__(64 * NWB * PAIR + (SPL ? 64 * NPW : 0)) __attribute
 // two edge tiles of a tile row the tap jobs rebuild them from the mirrored inside quads (one
 // v_perm of two gray dwords: quad at column c < 0 holds gray(-c .. -c-3), at c >= w gray(2w-2-c ..)).
 // Rows: reflect101 source rows, as k_pix5.  Needs w % 4 == 0 and w >= 2 * PC + 8.
-#ifndef FM_PIXW_WPE
-#define FM_PIXW_WPE 4  // 2 workgroups per CU (<= 128 VGPRs)
-#endif
-// SPL: as k_pix5's, 8 chain waves and NPW producer waves (taps, gray, loads) sharing the frame barrier
-template <int KC, int NWB, bool KEEP, bool TAIL, bool SPL = false, int NPW = 4>
-__global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amdgpu_waves_per_eu(FM_PIXW_WPE))) void k_pixw(FusedArgs a) {
-    using G = PW<KC, NWB>;
-    static_assert(!SPL || NWB == 8, "split waves: 64-row tiles");
-    constexpr int GJX = SPL ? (G::GSLOTS + NPW - 1) / NPW : G::GJ;
-    constexpr int HJX = SPL ? (G::NH + 64 * NPW - 1) / (64 * NPW) : G::HJ;
-    constexpr int HLASTX = SPL ? (G::NH - (HJX - 1) * 64 * NPW + 63) / 64 : G::HLASTW;
+// 2 workgroups per CU (<= 128 VGPRs).  (8 chain + 4 producer waves per tile, as k_pix5's SPL: 57.8 vs
+// 79.0 k frames/s at config 5, round 4.)
+template <int KC, bool KEEP, bool TAIL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pixw(FusedArgs a) {
+    using G = PW<KC>;
+    constexpr int GJX = G::GJ, HJX = G::HJ;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][GBUF]
     uint32_t* Hs = reinterpret_cast<uint32_t*>(smem + 2 * G::GBUF * 4);          // [2][HBUF]
-    double* atab;  // blur x alpha (f64): static LDS at address 0 with FM_PW_SDWA, else behind H
-    if constexpr (FM_PW_SDWA != 0) {
-        __shared__ double atab_s[256];
-        atab = atab_s;
-    } else {
-        atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 4);
-    }
+    __shared__ double atab_s[256];  // blur x alpha (f64), static LDS at address 0 (the SDWA table offset)
+    double* atab = atab_s;
     const int tid = threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool cw = !SPL || wv < 8;  // SPL: a chain wave, or a producer (pw = wv - 8)
-    const int pw = wv - 8, ptid = tid - 512;
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
-    int ti, tx, y0, wb;  // the wave's contour tile, the band's column, first row, the wave's 8-row slice of its tile
-    bool tile_ok = true;  // (a 128-row band's second tile may lie past the grid)
-    if constexpr (NWB == 8) {
-        ti = pix_tile(blockIdx.x, a);
-        tx = ti % a.ntx;
-        y0 = (ti / a.ntx) * TS;
-        wb = wv;
-    } else {
-        const int nby = (h + G::TH - 1) / G::TH;
-        const int bt = FM_PIX_ORDER ? block_tile(blockIdx.x, a.ntx, nby) : swizzle_tile(blockIdx.x, a.ntx * nby);
-        tx = bt % a.ntx;
-        y0 = (bt / a.ntx) * G::TH;
-        const int tyw = (y0 + RPWV * wv) / TS;
-        tile_ok = tyw < a.nty;
-        ti = tyw * a.ntx + tx;
-        wb = (RPWV * wv % TS) / RPWV;
-    }
+    const int ti = swizzle_tile(blockIdx.x, a.ntiles);  // contour tile
+    const int tx = ti % a.ntx;
+    const int y0 = (ti / a.ntx) * TS;
     const int x0 = tx * TS;
     const size_t plane = (size_t)h * w;
     const size_t fbytes = plane * 3;
     const bool hk = a.has_keep[s] != 0;
     const uint8_t* keep = a.keep + (size_t)s * plane;
-    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);  // (NWB >= 4)
+    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
+    kstamp_begin(a.kstamp);
 
     // ---- per-thread job plans (frame invariant)
     uint32_t goff[GJX], gdst[GJX];
-    const int gcnt_w = SPL ? (cw ? 0 : (G::GSLOTS - pw + NPW - 1) / NPW) : G::gcnt(wv);
+    const int gcnt_w = G::gcnt(wv);
 #pragma unroll
     for (int i = 0; i < GJX; i++) {
-        const int slot = SPL ? i * NPW + pw : i * NWB + wv;
+        const int slot = i * G::NWB + wv;
         const int j = (i < gcnt_w && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
         const int gr = j / GQ, gq = j - gr * GQ;
         const int x = x0 - PC + 4 * gq;
@@ -1459,7 +1194,7 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
     int hqv[HJX];
 #pragma unroll
     for (int i = 0; i < HJX; i++) {
-        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : tid + G::NTB * i;
+        const int j = tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
         hqv[i] = hq;
@@ -1480,7 +1215,7 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
 #pragma unroll
         for (int j = 0; j < RPWV; j++) {
             const int y = y0 + RPWV * wv + j;
-            const bool in = cw && x < w && y < h;
+            const bool in = x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
@@ -1502,15 +1237,9 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
     // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5: a load under a
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
-        if constexpr (FM_PW_BUFLD != 0) {
-            const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
+        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
 #pragma unroll
-            for (int i = 0; i < GJX; i++) load12b(rw[i], rs, goff[i]);
-        } else {
-            const gbytes_t src = frame_base(a.src + f * fbytes);
-#pragma unroll
-            for (int i = 0; i < GJX; i++) load12(rw[i], src, goff[i]);
-        }
+        for (int i = 0; i < GJX; i++) load12b(rw[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
@@ -1548,7 +1277,7 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
     auto tap_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < HJX; i++) {
-            if (SPL ? (!cw && (i == HJX - 1 && pw >= HLASTX)) || cw : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
+            if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
             const uint32_t* r0 = gb + (hsrc[i] - hqv[i]);
             uint32_t u[4], v[4];
             hrow(r0, hqv[i], u);
@@ -1558,45 +1287,14 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
         }
     };
     const int t0 = a.t_begin, t1 = a.t_end;
-    if (!SPL || !cw) load((size_t)t0 * S + s);
+    load((size_t)t0 * S + s);
     gray_stage(gray);
-    if (!SPL || !cw) load((size_t)min(t0 + 1, t1 - 1) * S + s);
+    load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
-    if (!SPL || !cw) load((size_t)min(t0 + 2, t1 - 1) * S + s);
+    load((size_t)min(t0 + 2, t1 - 1) * S + s);
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;
-    if constexpr (SPL) {
-        if (cw) {
-            for (int t = t0; t < t1; t++) {
-                const int b = (t - t0) & 1;
-                const size_t f = (size_t)t * S + s;
-                lds_barrier();
-                uint32_t colbits = 0, fl = 0;
-                ChainCtx ccf = cc;
-                ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
-                int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
-                asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-                var = __builtin_amdgcn_readfirstlane(var);
-                asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-                const uint32_t* Hb = Hs + b * G::HBUF;
-                if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
-                else
-                    chain_rows_w<KC, KEEP, true, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl, wvf);
-                reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-                if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
-            }
-        } else {
-            for (int t = t0; t < t1; t++) {
-                const int b = (t - t0) & 1;
-                lds_barrier();
-                if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
-                gray_stage(gray + b * G::GBUF);
-                load((size_t)min(t + 3, t1 - 1) * S + s);
-            }
-        }
-    } else
     for (int t = t0; t < t1; t++) {
         const int b = (t - t0) & 1;
         const size_t f = (size_t)t * S + s;
@@ -1610,17 +1308,13 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
         const uint32_t* Hb = Hs + b * G::HBUF;
         if (!TAIL || var == 0)
-            chain_rows_w<KC, KEEP, false, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
-                                          NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
+            chain_rows_w<KC, KEEP, false, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
         else
-            chain_rows_w<KC, KEEP, true, FM_PW_SDWA != 0>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl,
-                                         NWB == 8 ? wvf : __builtin_amdgcn_readfirstlane(wb));
+            chain_rows_w<KC, KEEP, true, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
         if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         gray_stage(gray + b * G::GBUF);
-        if (NWB == 8 || tile_ok) {
-            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wb] = (uint8_t)colbits;
-            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wb] = fl;
-        }
+        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
         load((size_t)min(t + 3, t1 - 1) * S + s);
     }
     double* bgo = a.bg_out + (size_t)s * plane;
@@ -1628,8 +1322,9 @@ __global__ __launch_bounds__(64 * NWB + (SPL ? 64 * NPW : 0)) __attribute__((amd
 #pragma unroll
     for (int j = 0; j < RPWV; j++) {
         const int y = y0 + RPWV * wv + j;
-        if (cw && x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
+    kstamp_end(a.kstamp);
 }
 
 }  // namespace px
@@ -1646,131 +1341,45 @@ static bool taps_match(const FusedArgs& a) {
 }
 
 hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init) {
-#ifndef FM_PIX_LDS_PAD
-#define FM_PIX_LDS_PAD 0  // diagnostics only: extra LDS per workgroup (limits workgroups per CU)
-#endif
-    const int bytes = px::Geo(a.ksize >> 1).bytes + FM_PIX_LDS_PAD;
+    const int bytes = px::Geo(a.ksize >> 1).bytes;
     const bool ok = a.ksize == 3 ? taps_match<3>(a) : a.ksize == 5 ? taps_match<5>(a) : a.ksize == 7 ? taps_match<7>(a)
                   : a.ksize == 21 ? taps_match<21>(a) : false;
     if (!ok) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
     if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
-        px::p5_lds_bytes<8>() <= 64 * 1024) {
+        px::P5G::bytes <= 64 * 1024) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        // FM_P5_BANDS: small work images (mode D's 100 x 56 is two tiles, 256 frames in a row on two CUs)
-        // on bands of 8 or 16 rows.  Measured (round 4): mode D 470 k -> 479 k frames/s, the pixel kernel
-        // 417 vs 320-466 us per 256 frames -- a frame's critical path is per wave (its 8-row chain and its
-        // share of gray and taps), which a band does not shorten; off
-#ifndef FM_P5_BANDS
-#define FM_P5_BANDS 0
-#endif
-#ifndef FM_P5_PAIR
-#define FM_P5_PAIR 0  // 64 x 64 tiles two per 1,024-thread workgroup when the tile count is even (k_pix5 PAIR)
-#endif
-#ifndef FM_P5_SPLIT
-#define FM_P5_SPLIT 1  // small work images (<= 16 tiles): 16 waves per tile, chain and producer halves (k_pix5 SPL; mode D +3.4 %)
-#endif
-#ifndef FM_P5_SPLIT_LARGE
-#define FM_P5_SPLIT_LARGE 0  // larger images too: 8 chain + 4 producer waves (768 threads, two workgroups per CU)
-#endif
-        if (FM_P5_SPLIT_LARGE && a.ntiles * a.S > 16) {
-            const dim3 sgrid(a.ntiles, a.S);
-            const size_t lds = px::P5G<8>::dyn_bytes;
-            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 1, true, 4>), sgrid, dim3(768), lds, st, a);
-            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 1, true, 4>), sgrid, dim3(768), lds, st, a);
-            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 1, true, 4>), sgrid, dim3(768), lds, st, a);
-            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 1, true, 4>), sgrid, dim3(768), lds, st, a);
-            return hipGetLastError();
-        }
-        if (FM_P5_SPLIT && a.ntiles * a.S <= 16) {
-            const dim3 sgrid(a.ntiles, a.S);
-            const size_t lds = px::P5G<8>::dyn_bytes;
-            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 1, true>), sgrid, dim3(1024), lds, st, a);
-            else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 1, true>), sgrid, dim3(1024), lds, st, a);
-            else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 1, true>), sgrid, dim3(1024), lds, st, a);
-            else hipLaunchKernelGGL((px::k_pix5<8, false, false, 1, true>), sgrid, dim3(1024), lds, st, a);
-            return hipGetLastError();
-        }
-        if constexpr (FM_P5_PAIR != 0) {
-            if (a.ntiles % 2 == 0 && a.ntiles * a.S >= 128) {
-                const dim3 pgrid(a.ntiles / 2, a.S);
-                const size_t lds = 2 * px::p5_half_bytes<8>();
-                static_assert(2 * px::p5_half_bytes<8>() <= 64 * 1024, "tile pair LDS");
-                if (keep && tail) hipLaunchKernelGGL((px::k_pix5<8, true, true, 2>), pgrid, dim3(1024), lds, st, a);
-                else if (keep) hipLaunchKernelGGL((px::k_pix5<8, true, false, 2>), pgrid, dim3(1024), lds, st, a);
-                else if (tail) hipLaunchKernelGGL((px::k_pix5<8, false, true, 2>), pgrid, dim3(1024), lds, st, a);
-                else hipLaunchKernelGGL((px::k_pix5<8, false, false, 2>), pgrid, dim3(1024), lds, st, a);
-                return hipGetLastError();
-            }
-        }
-        const int nwb = !FM_P5_BANDS || a.ntiles * a.S >= 128 ? 8 : a.ntiles * a.S >= 32 ? 2 : 1;
-        const int nby = a.nty * (8 / nwb);  // bands covering every 64-row contour tile whole
-        const dim3 bgrid(a.ntx * nby, a.S);
-#define FM_P5_LAUNCH(NWB)                                                                                          \
-    do {                                                                                                           \
-        const size_t lds = px::P5G<NWB>::dyn_bytes;                                                                \
-        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<NWB, true, true>), bgrid, dim3(64 * NWB), lds, st, a);    \
-        else if (keep) hipLaunchKernelGGL((px::k_pix5<NWB, true, false>), bgrid, dim3(64 * NWB), lds, st, a);      \
-        else if (tail) hipLaunchKernelGGL((px::k_pix5<NWB, false, true>), bgrid, dim3(64 * NWB), lds, st, a);      \
-        else hipLaunchKernelGGL((px::k_pix5<NWB, false, false>), bgrid, dim3(64 * NWB), lds, st, a);               \
+        const size_t lds = px::P5G::dyn_bytes;
+        // small work images (<= 16 tiles, e.g. mode D's two): 16 waves per tile, chain and producer halves
+        // (k_pix5 SPL; mode D +3.4 %, round 4)
+        const bool spl = a.ntiles * a.S <= 16;
+#define FM_P5_LAUNCH(SP)                                                                                       \
+    do {                                                                                                       \
+        const dim3 blk(SP ? 1024 : 512);                                                                       \
+        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, SP>), grid, blk, lds, st, a);              \
+        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, SP>), grid, blk, lds, st, a);                \
+        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, SP>), grid, blk, lds, st, a);                \
+        else hipLaunchKernelGGL((px::k_pix5<false, false, SP>), grid, blk, lds, st, a);                         \
     } while (0)
-        if (nwb == 8) FM_P5_LAUNCH(8);
-        else if (nwb == 2) FM_P5_LAUNCH(2);
-        else FM_P5_LAUNCH(1);
+        if (spl) FM_P5_LAUNCH(true);
+        else FM_P5_LAUNCH(false);
 #undef FM_P5_LAUNCH
         return hipGetLastError();
     }
-#ifndef FM_PIXW
-#define FM_PIXW 1  // k = 21 steady state on k_pixw (0: k_pix<21>, the round-2 kernel)
-#endif
-#ifndef FM_PIXW_TALL
-#define FM_PIXW_TALL 0  // large grids on 128-row bands of 16 waves (one workgroup per CU) instead of 64 x 64 tiles.
-                        // Measured (round 4, 2 alternating rounds, config 5): 3.61 vs 3.33 ms per launch: off
-#endif
-    if (FM_PIXW && a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 &&
-        ((uintptr_t)a.src & 3) == 0) {
+    // k = 21 steady state (config 5) on k_pixw
+    if (a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 && ((uintptr_t)a.src & 3) == 0) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-#define FM_PIXW_LAUNCH(NWB, GRID)                                                                                     \
-    do {                                                                                                              \
-        using G = px::PW<21, NWB>;                                                                                    \
-        static_assert(G::bytes <= 160 * 1024, "k_pixw LDS");                                                          \
-        if (keep && tail) {                                                                                           \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, true>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);             \
-        } else if (keep) {                                                                                            \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, true, false>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);            \
-        } else if (tail) {                                                                                            \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, true>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);            \
-        } else {                                                                                                      \
-            (void)hipFuncSetAttribute((const void*)px::k_pixw<21, NWB, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-            hipLaunchKernelGGL((px::k_pixw<21, NWB, false, false>), GRID, dim3(64 * NWB), G::dyn_bytes, st, a);           \
-        }                                                                                                             \
+        using G = px::PW<21>;
+        static_assert(G::bytes <= 160 * 1024, "k_pixw LDS");
+#define FM_PIXW_LAUNCH(K, T)                                                                                            \
+    do {                                                                                                                \
+        (void)hipFuncSetAttribute((const void*)px::k_pixw<21, K, T>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+        hipLaunchKernelGGL((px::k_pixw<21, K, T>), grid, dim3(512), G::dyn_bytes, st, a);                                \
     } while (0)
-#ifndef FM_PIXW_SPLIT
-#define FM_PIXW_SPLIT 0  // 8 chain + 4 producer waves per tile (768 threads)
-#endif
-        if constexpr (FM_PIXW_SPLIT != 0) {
-            using G = px::PW<21, 8>;
-#define FM_PIXW_SPL(K, T)                                                                                              \
-    do {                                                                                                               \
-        (void)hipFuncSetAttribute((const void*)px::k_pixw<21, 8, K, T, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-        hipLaunchKernelGGL((px::k_pixw<21, 8, K, T, true, 4>), grid, dim3(768), G::dyn_bytes, st, a);                 \
-    } while (0)
-            if (keep && tail) FM_PIXW_SPL(true, true);
-            else if (keep) FM_PIXW_SPL(true, false);
-            else if (tail) FM_PIXW_SPL(false, true);
-            else FM_PIXW_SPL(false, false);
-#undef FM_PIXW_SPL
-            return hipGetLastError();
-        }
-        if (FM_PIXW_TALL && a.nty >= 4 && a.ntiles * a.S >= 2048) {
-            const dim3 tgrid(a.ntx * ((a.h + 127) / 128), a.S);
-            FM_PIXW_LAUNCH(16, tgrid);
-        } else {
-            FM_PIXW_LAUNCH(8, grid);
-        }
+        if (keep && tail) FM_PIXW_LAUNCH(true, true);
+        else if (keep) FM_PIXW_LAUNCH(true, false);
+        else if (tail) FM_PIXW_LAUNCH(false, true);
+        else FM_PIXW_LAUNCH(false, false);
 #undef FM_PIXW_LAUNCH
         return hipGetLastError();
     }

@@ -45,6 +45,15 @@ def init(p: Placement, backend: str, device=None) -> bool:
     return True
 
 
+def world_size(active: bool) -> int:
+    """Ranks in the process group as the group itself reports them (1 without one)."""
+    if not active:
+        return 1
+    import torch.distributed as dist
+
+    return dist.get_world_size()
+
+
 def barrier(active: bool) -> None:
     if active:
         import torch.distributed as dist

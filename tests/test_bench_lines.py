@@ -1,0 +1,73 @@
+"""bench.py's labelling and roofline arithmetic (CPU): which BASELINE config a run is filed under at world
+size 1 / 2 / 8 (configs[3] = 64 x 1080p, 8 streams per GPU on 8 GPUs, find_motion.py:1054-1122), and the
+launch-time consistency check of the roofline (a launch of one stream's serialised pixel kernels can never
+average more than a step)."""
+import importlib
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    saved = os.environ.get("GPU_MAX_HW_QUEUES")  # bench.py sets it at import (for its own process)
+    sys.path.insert(0, ROOT)
+    try:
+        yield importlib.import_module("bench")
+    finally:
+        if saved is None:
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = saved
+
+
+@pytest.mark.parametrize("S,world,mode,want", [
+    (1, 1, "F", "configs[1]"),
+    (1, 1, "D", "configs[1] (mode D)"),
+    (1, 8, "F", "configs[1] x 8 GPUs"),
+    (8, 1, "F", "configs[2]"),
+    (8, 1, "D", "configs[2] (mode D)"),
+    (8, 8, "F", "configs[3]"),
+    (8, 2, "F", "configs[3] family: 8 streams per GPU x 2 GPUs"),
+    (8, 4, "F", "configs[3] family: 8 streams per GPU x 4 GPUs"),
+])
+def test_config_name_is_world_aware(bench, S, world, mode, want):
+    assert bench.config_name(S, 1920, 1080, mode, 5, world=world) == want
+
+
+def test_config_name_other_shapes(bench):
+    assert bench.config_name(4, 3840, 2160, "F", 21, haar=True) == "configs[4]"
+    assert bench.config_name(4, 3840, 2160, "F", 21) == "configs[4] geometry (no Haar stage)"
+    assert bench.config_name(3, 1920, 1080, "F", 5, world=2).startswith("3 x 1080p streams per GPU x 2 GPU(s)")
+    assert bench.config_name(1, 640, 480, "F", 5) == "custom shape"
+
+
+def _cfg(S=1, T=256, mode="F"):
+    h, w = (1080, 1920) if mode == "F" else (56, 100)
+    return {"streams_per_gpu": S, "frames_per_step": T, "H": 1080, "W": 1920, "h": h, "w": w,
+            "workload": "test"}
+
+
+def test_roofline_frac_and_launch_check(bench):
+    cfg = _cfg()
+    # 20 stamped launches of 450 us each inside 500 us steps
+    roof = bench.roofline_of({"pix": (20 * 0.450, 20)}, cfg, ms_per_step=0.5)
+    assert roof["kernel"] == "pix" and roof["launches_timed"] == 20
+    assert roof["avg_launch_us"] == pytest.approx(450.0)
+    assert roof["bytes_per_launch"] == 2_073_600 * (4 * 256 + 16)
+    assert roof["frac"] == pytest.approx(roof["bytes_per_launch"] / 450e-6 / 1e9 / 8000.0, abs=1e-4)
+    assert roof["launch_le_step"] is True
+    # a launch longer than the step is a timing fault, flagged in the line
+    bad = bench.roofline_of({"pix": (20 * 0.709, 20)}, cfg, ms_per_step=0.6555)
+    assert bad["launch_le_step"] is False
+
+
+def test_roofline_mode_d_prices_the_resize(bench):
+    cfg = _cfg(mode="D")
+    roof = bench.roofline_of({"pix": (10 * 0.3, 10), "resize_area": (10 * 0.29, 10)}, cfg, ms_per_step=0.4)
+    assert roof["kernel"] == "resize_area"
+    assert roof["bytes_per_launch"] == 256 * (1920 * 1080 * 3 + 56 * 100 * 3)
+    assert roof["launch_le_step"] is True

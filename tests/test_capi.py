@@ -154,3 +154,15 @@ def test_use_hw_queues_env_wins_unless_forced():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, check=True)
     assert out.stdout.split() == ["4", "8", "8"], out.stdout + out.stderr
+
+
+def test_cli_hw_queues_honours_env_and_validates():
+    """The CLI forces FM_HW_QUEUES when it is set (validated to HIP's 1..32); otherwise an exported
+    GPU_MAX_HW_QUEUES is honoured and 8 is only the default."""
+    from find_motion_amd.cli import hw_queues_from_env
+    assert hw_queues_from_env({}) == (8, False)
+    assert hw_queues_from_env({"GPU_MAX_HW_QUEUES": "4"}) == (8, False)  # use_hw_queues keeps the 4
+    assert hw_queues_from_env({"FM_HW_QUEUES": "16", "GPU_MAX_HW_QUEUES": "4"}) == (16, True)
+    for bad in ("abc", "0", "33", "-1"):
+        with pytest.raises(SystemExit, match="FM_HW_QUEUES"):
+            hw_queues_from_env({"FM_HW_QUEUES": bad})

@@ -75,12 +75,14 @@ def test_lazy_raw_frames_written_uncompressed(tmp_path):
 
 def test_unsupported_frames_mid_stream_decode_on_the_host(tmp_path):
     """A stream whose first frame the GPU decoder takes but whose later frames it refuses (progressive
-    JPEGs from frame 10 on): the batches holding them are decoded on the host and submitted as frames
-    (feeder), cached frames of overwritten batches too (one-frame decoder) -- decisions and every written
-    raw frame equal the oracle's on the libjpeg-turbo-decoded frames, nothing raises."""
+    JPEGs at frames 10-29, then 4:4:4 instead of the first frame's 4:2:0 sampling at frames 30-35): the
+    batches holding them are decoded on the host and submitted as frames (feeder), cached frames of
+    overwritten batches too (one-frame decoder) -- decisions and every written raw frame equal the
+    oracle's on the libjpeg-turbo-decoded frames, nothing raises."""
     W, H, n = 320, 240, 40
     vid = SyntheticVideo(W, H, 3)
-    jp = [encode(vid.frame(i), quality=85, progressive=10 <= i < 30) for i in range(n)]
+    jp = [encode(vid.frame(i), quality=85, progressive=10 <= i < 30, subsampling=0 if 30 <= i < 36 else 2)
+          for i in range(n)]
     src = tmp_path / "v.avi"
     w = videoio.MjpegAviWriter(str(src), 30, (W, H))
     for j in jp:
@@ -97,10 +99,10 @@ def test_unsupported_frames_mid_stream_decode_on_the_host(tmp_path):
     assert len(got) == len(want)
     for g, i in zip(got, want):
         assert np.array_equal(g, reference_decode(jp[i])), i
-    cap = videoio.JpegListCapture(jp[8:12])
-    for k in range(4):  # the one-frame GPU decoder: baseline frames on the GPU, progressive ones on the host
+    cap = videoio.JpegListCapture(jp[8:12] + jp[28:32])
+    for k in range(8):  # the one-frame GPU decoder: baseline frames on the GPU, progressive / 4:4:4 ones on the host
         ok, f = cap.read()
-        assert ok and np.array_equal(f, reference_decode(jp[8 + k])), k
+        assert ok and np.array_equal(f, reference_decode((jp[8:12] + jp[28:32])[k])), k
     cap.release()
 
 

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE (round 5): this archived A/B predates bench.py reading FM_BENCH_HW_QUEUES; bench.py now overwrites
+# GPU_MAX_HW_QUEUES, so re-running it as written measures 8 queues in both arms (use FM_BENCH_HW_QUEUES=$q).
 # Round 4, call s: hardware queues per process (the box exports GPU_MAX_HW_QUEUES=4, which bench.py's
 # use_hw_queues() left in place): mode D, the driver's command and the MJPEG-fed leg at 4 vs 8, alternating;
 # first the parity suite and mode D with the pixel / input streams on disjoint CUs (FM_CU_SPLIT) vs shared.
