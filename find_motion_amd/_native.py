@@ -31,7 +31,8 @@ EXPORTED = (
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
     "fm_mjpeg_create", "fm_mjpeg_destroy", "fm_mjpeg_last_error", "fm_mjpeg_decode", "fm_mjpeg_last_ms",
     "fm_submit_jpeg", "fm_read_frame", "fm_mjpeg_tune", "fm_frame_device", "fm_mjpeg_geometry",
-    "fm_submit_streams", "fm_footprint", "fm_haar_detect_frame_list",
+    "fm_submit_streams", "fm_footprint", "fm_haar_detect_frame_list", "fm_haar_detect_frame_list_async",
+    "fm_haar_collect",
 )
 
 
@@ -117,6 +118,8 @@ def load() -> C.CDLL:
     L.fm_haar_candidates.argtypes = [vp, vp, i32]
     L.fm_haar_detect_frames.argtypes = [vp, vp, i32, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
     L.fm_haar_detect_frame_list.argtypes = [vp, vp, i32, i32, i32, i32, C.c_double, i32, vp, i32, vp, vp]
+    L.fm_haar_detect_frame_list_async.argtypes = [vp, vp, i32, i32, i32, i32, C.c_double, i32, vp]
+    L.fm_haar_collect.argtypes = [vp, vp, i32, vp, i32]
     L.fm_haar_last_ms.argtypes = [vp]
     L.fm_haar_last_ms.restype = C.c_double
     L.fm_mjpeg_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -514,6 +517,33 @@ class CascadeClassifier:
                                              C.byref(rh))
             if rc != FM_OK:
                 raise FMError(rc, f"fm_haar_detect_frame_list: {L.fm_haar_last_error(self._h).decode()}")
+            if counts.max(initial=0) <= cap:
+                return [rects[i, :counts[i]].copy() for i in range(n)]
+            cap = int(counts.max())
+
+    def detect_frame_list_async(self, ptrs, H: int, W: int, roi_w: int = 300, scaleFactor=1.1, minNeighbors=5) -> int:
+        """detect_frame_list queued on the detector's own stream without waiting (fm_haar_detect_frame_list_async);
+        `collect` returns its results.  One detection in flight per detector; the frames must stay in place
+        until it is collected.  Returns the number of frames queued."""
+        L = load()
+        n = len(ptrs)
+        arr = (C.c_void_p * n)(*[int(p) for p in ptrs])
+        rh = C.c_int32()
+        rc = L.fm_haar_detect_frame_list_async(self._h, C.cast(arr, C.c_void_p), n, int(H), int(W), int(roi_w),
+                                               float(scaleFactor), int(minNeighbors), C.byref(rh))
+        if rc != FM_OK:
+            raise FMError(rc, f"fm_haar_detect_frame_list_async: {L.fm_haar_last_error(self._h).decode()}")
+        return n
+
+    def collect(self, n: int, cap: int = 256):
+        """The queued detection's results (waits for it): a list of [k, 4] rect arrays, one per frame."""
+        L = load()
+        while True:
+            rects = np.zeros((n, cap, 4), np.int32)
+            counts = np.zeros(n, np.int32)
+            rc = L.fm_haar_collect(self._h, _ptr(rects), cap, _ptr(counts), int(n))
+            if rc != FM_OK:
+                raise FMError(rc, f"fm_haar_collect: {L.fm_haar_last_error(self._h).decode()}")
             if counts.max(initial=0) <= cap:
                 return [rects[i, :counts[i]].copy() for i in range(n)]
             cap = int(counts.max())

@@ -48,6 +48,7 @@ struct BatchSlot {
     uint8_t* d_work = nullptr;      // resized BGR [T][S][h][w][3] (mode D)
     uint8_t* d_planes = nullptr;    // [3][T][S][h*w] gray, blur, frame_delta (FM_FLAG_KEEP_PLANES)
     uint64_t* d_bits = nullptr;     // threshold bit rows (k_pix output)
+    uint8_t* d_sblur = nullptr;     // small work images: blur bytes [T*S][w][nty * 64] (k_small_blur -> k_small_scan)
     uint64_t* d_dbits = nullptr;    // dilated bit rows = VideoFrame.thresh
     TileRec* d_tiles = nullptr;
     NodeRec* d_nodes = nullptr;
@@ -116,6 +117,7 @@ struct fm_ctx {
     size_t pinned_bytes = 0;  // and its page-locked host allocations
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
+    bool use_small = false;        // the pixel stage as k_small_blur + k_small_scan (small work images)
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;  // nnodes: per batch slot
     int nquota = 0;                                             // nodes of each frame's quota
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
@@ -556,6 +558,17 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 
     fm_ctx* cp = c.get();
     HIP_TRY(cp, hipSetDevice(p.device));
+    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
+                   ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
+    c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
+                 dev_env("FM_NO_PIX") == nullptr;
+    // small work images (mode D): frame-parallel blur + per-pixel scan (fm_small.hip), unless the caller
+    // keeps the gray / blur / delta planes (k_pix writes them)
+#ifndef FM_SMALL_DEFAULT
+#define FM_SMALL_DEFAULT 0  // (round 5 A/B: abvar builds with 1 until the GPU suite is green on it)
+#endif
+    c->use_small = FM_SMALL_DEFAULT && c->use_pix && !(p.flags & FM_FLAG_KEEP_PLANES) && small_supported(c->h, c->w, p.ksize);
+    if (const char* e = dev_env("FM_SMALL")) c->use_small = c->use_small && std::atoi(e) != 0;
     // Small work image behind a resize (mode D, -B 100: 1080p -> 100 x 56, two 64 x 64 tiles per stream):
     // the pixel kernel is a few workgroups whose frames run one after another (latency-bound), the
     // INTER_AREA resize of the next batch streams whole frames over every CU.  Sharing CUs, the resize
@@ -566,7 +579,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     // the device, offset by LOCAL_RANK (ranks rehearsed on one GPU), so two engines' pixel kernels do
     // not queue on the same 8 CUs.
     const long long work_tiles = (long long)((c->w + 63) / 64) * ((c->h + 63) / 64) * p.n_streams;
-    bool cu_split = c->rmode != ResizeMode::Identity && work_tiles <= 16;
+    bool cu_split = c->rmode != ResizeMode::Identity && work_tiles <= 16 && !c->use_small;
     if (const char* e = dev_env("FM_CU_SPLIT")) cu_split = std::atoi(e) != 0 && cu_split;
     std::vector<uint32_t> pix_mask;
     if (cu_split) {
@@ -620,10 +633,6 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     c->src_frame_bytes = (size_t)p.src_h * p.src_w * 3;
     const size_t frames = S * T, px = frames * c->work_plane;
     int rc;
-    c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
-                   ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
-    c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
-                 dev_env("FM_NO_PIX") == nullptr;
     c->nslots = c->use_fused ? kSlots : 1;
     // contour-pass streams shared round-robin by the slots: few streams, because the
     // runtime multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order,
@@ -668,6 +677,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
                 (rc = dalloc(cp, &b.d_regrep, frames * c->ntiles)) || (rc = dalloc(cp, &b.d_ncr, frames * 2)) ||
                 (rc = dalloc(cp, &b.d_dbits, frames * c->ntiles * 64)) ||
                 (c->use_pix && (rc = dalloc(cp, &b.d_bits, frames * c->ntiles * 64))) ||
+                (c->use_small && (rc = dalloc(cp, &b.d_sblur, small_scratch_bytes(c->h, c->w, c->nty, frames)))) ||
                 (rc = dalloc(cp, &b.d_nodes, (size_t)c->nnodes)))
                 return rc;
         }
@@ -779,7 +789,7 @@ void fm_destroy(fm_ctx* c) {
             st = nullptr;
         }
     for (auto& b : c->slots) {
-        dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles);
+        dfree(b.d_in); dfree(b.d_work); dfree(b.d_planes); dfree(b.d_bits); dfree(b.d_dbits); dfree(b.d_tiles); dfree(b.d_sblur);
         dfree(b.d_nodes); dfree(b.d_heavy); dfree(b.d_count); dfree(b.d_tflag); dfree(b.d_candf);
         dfree(b.d_clist); dfree(b.d_rlist); dfree(b.d_regrep); dfree(b.d_ncr);
         for (auto* hp : {(void*)b.h_count, (void*)b.h_overflow, (void*)b.h_rec, (void*)b.h_init, (void*)b.h_stats})
@@ -1001,10 +1011,16 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
                 fp.bg_in = c->d_bg[c->bg_cur];
                 fp.bg_out = c->d_bg[c->bg_cur ^ 1];
                 if (!init) fp.init = nullptr;
-                fp.kstamp = c->timer.stamp(name);
-                int tok = fp.kstamp ? -1 : c->timer.begin(name, ps);
-                HIP_TRY(c, launch_pix(ps, fp, planes, init));
-                c->timer.end(tok);
+                if (c->use_small) {
+                    uint64_t* k1 = c->timer.stamp(init ? "small_blur_init" : "small_blur");
+                    uint64_t* k2 = c->timer.stamp(init ? "small_scan_init" : "small_scan");
+                    HIP_TRY(c, launch_small(ps, fp, B.d_sblur, k1, k2));
+                } else {
+                    fp.kstamp = c->timer.stamp(name);
+                    int tok = fp.kstamp ? -1 : c->timer.begin(name, ps);
+                    HIP_TRY(c, launch_pix(ps, fp, planes, init));
+                    c->timer.end(tok);
+                }
                 c->bg_cur ^= 1;
                 return FM_OK;
             };

@@ -608,6 +608,13 @@ struct fm_haar {
     bool times = false;
     double tph[4] = {0, 0, 0, 0};
     long long ncalls = 0;
+    // a queued detection (detect_enqueue) and, after detect_finish, its results per image
+    bool pending = false;
+    int pend_n = 0, pend_min_neighbors = 0;
+    std::vector<float> pend_sc;
+    std::vector<std::vector<int32_t>> out;  // grouped rects (x, y, w, h) of each image of the last detection
+    Geo pend_g{};
+    double pend_tA = 0., pend_tB = 0.;
 };
 
 static inline double hnow() {
@@ -851,22 +858,29 @@ int fm_haar_window(const fm_haar* h, int* w, int* hh) {
     return FM_OK;
 }
 
-int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int channels, int on_device,
-                   double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h,
-                   int32_t* rects, int cap, int32_t* counts) {
+// The detection of n images queued on the detector's stream (nothing waits): scales, pyramid, integrals,
+// window sweep, the device row walk and the copies of the candidate lists; detect_finish waits for them and
+// runs the host post-pass.  One detection in flight per detector.
+static int detect_enqueue_impl(fm_haar* h, const uint8_t* images, int n, int H, int W, int channels, int on_device,
+                               double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h) {
     if (!h || !h->d_blob) return FM_EINVAL;
-    if (!images || n < 1 || H < 1 || W < 1 || (channels != 1 && channels != 3) || !(scale_factor > 1.0) ||
-        cap < 0 || !counts || (cap > 0 && !rects))
-        return hfail(h, FM_EINVAL, "bad arguments (n >= 1, 1 or 3 channels, scale_factor > 1, counts[n])");
+    if (!images || n < 1 || H < 1 || W < 1 || (channels != 1 && channels != 3) || !(scale_factor > 1.0))
+        return hfail(h, FM_EINVAL, "bad arguments (n >= 1, 1 or 3 channels, scale_factor > 1)");
+    if (h->pending) return hfail(h, FM_ESTATE, "a detection is already queued: collect it first");
     HH(h, hipSetDevice(h->device));
     const double tA = h->times ? hnow() : 0.;
-    for (int i = 0; i < n; ++i) counts[i] = 0;
+    h->out.assign(n, {});
+    h->pend_n = n;
+    h->pend_min_neighbors = min_neighbors;
+    h->pend_sc.clear();
+    h->pend_g = Geo{};
     h->cand.clear();
     // scales (detectMultiScaleNoGrouping)
     if (max_w == 0 || max_h == 0) {
         max_w = W;
         max_h = H;
     }
+    h->pending = true;  // (a detection with no window finishes with empty results)
     if (H < h->win_h || W < h->win_w) return FM_OK;
     std::vector<float> all, sc;
     for (double f = 1;; f *= scale_factor) {
@@ -1010,6 +1024,35 @@ swept:
     const double tB = h->times ? hnow() : 0.;
     HH(h, hipMemcpyAsync(h->h_ccnt, h->d_ccnt, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     HH(h, hipMemcpyAsync(h->h_cand, h->d_cand, (size_t)n * kCandCap * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    h->pend_sc = sc;
+    h->pend_g = g;
+    h->pend_tA = tA;
+    h->pend_tB = tB;
+    return FM_OK;
+}
+
+static int detect_enqueue(fm_haar* h, const uint8_t* images, int n, int H, int W, int channels, int on_device,
+                          double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h) {
+    const int rc = detect_enqueue_impl(h, images, n, H, W, channels, on_device, scale_factor, min_neighbors, min_w,
+                                       min_h, max_w, max_h);
+    if (rc != FM_OK && h && rc != FM_ESTATE) {  // (a failed call leaves nothing to collect)
+        h->pending = false;
+        h->out.clear();
+    }
+    return rc;
+}
+
+// Waits for the queued detection and runs the host post-pass: OpenCV's row walk order from the device's
+// sorted candidate lists (or the whole result grid when a list overflowed), then groupRectangles.
+static int detect_finish(fm_haar* h) {
+    if (!h->pending) return FM_OK;
+    h->pending = false;
+    const int n = h->pend_n, min_neighbors = h->pend_min_neighbors;
+    const std::vector<float>& sc = h->pend_sc;
+    const Geo& g = h->pend_g;
+    if (sc.empty()) return FM_OK;  // no scale (or an image smaller than the window): no detections
+    const double tA = h->pend_tA, tB = h->pend_tB;
+    const long long nw = (long long)n * g.NW;
     HH(h, hipStreamSynchronize(h->stream));
     bool overflow = false;
     for (int i = 0; i < n; ++i) overflow |= h->h_ccnt[i] > kCandCap;
@@ -1123,10 +1166,7 @@ swept:
                 if (j == ncls) outr.insert(outr.end(), r1, r1 + 4);
             }
         }
-        const int no = (int)outr.size() / 4;
-        counts[img] = no;
-        const int keep = std::min(no, cap);
-        if (keep > 0) std::memcpy(rects + (size_t)img * cap * 4, outr.data(), sizeof(int32_t) * 4 * keep);
+        h->out[img] = std::move(outr);
     };
     // (64 1080p ROI frames of frontalface: 12.1 ms per call single-threaded beside 3.1 ms of kernels, when
     // the host walked every window; with the device's lists only grouping is left, worth threads only for
@@ -1155,6 +1195,30 @@ swept:
     return FM_OK;
 }
 
+// the last detection's results: counts[i] (all of them) and up to cap rects per image
+static void detect_copy(const fm_haar* h, int32_t* rects, int cap, int32_t* counts) {
+    for (int img = 0; img < (int)h->out.size(); ++img) {
+        const int no = (int)h->out[img].size() / 4;
+        counts[img] = no;
+        const int keep = std::min(no, cap);
+        if (keep > 0) std::memcpy(rects + (size_t)img * cap * 4, h->out[img].data(), sizeof(int32_t) * 4 * keep);
+    }
+}
+
+int fm_haar_detect(fm_haar* h, const uint8_t* images, int n, int H, int W, int channels, int on_device,
+                   double scale_factor, int min_neighbors, int min_w, int min_h, int max_w, int max_h,
+                   int32_t* rects, int cap, int32_t* counts) {
+    if (!h || !h->d_blob) return FM_EINVAL;
+    if (cap < 0 || !counts || (cap > 0 && !rects)) return hfail(h, FM_EINVAL, "bad arguments (counts[n], rects[n][cap])");
+    if (int rc = detect_finish(h)) return rc;  // (a queued detection the caller never collected)
+    if (int rc = detect_enqueue(h, images, n, H, W, channels, on_device, scale_factor, min_neighbors, min_w, min_h,
+                                max_w, max_h))
+        return rc;
+    if (int rc = detect_finish(h)) return rc;
+    detect_copy(h, rects, cap, counts);
+    return FM_OK;
+}
+
 int fm_haar_candidates(const fm_haar* h, int32_t* rects, int cap) {
     if (!h || cap < 0 || (cap > 0 && !rects)) return FM_EINVAL;
     const int nc = (int)h->cand.size() / 4;
@@ -1169,10 +1233,15 @@ double fm_haar_last_ms(const fm_haar* h) { return h ? h->last_ms : 0.; }
 
 // find_objects' resize + detect over n frames: consecutive [n][H][W][3] frames at `frames` (host memory,
 // or device memory when on_device), or -- list != nullptr -- the n device frames at list[i]
+// async: queue the detection (fm_haar_collect takes its results), else detect and return the results
 static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* const* list, int n, int H, int W,
                               int on_device, int roi_w, double scale_factor, int min_neighbors, int32_t* rects,
-                              int cap, int32_t* counts, int* roi_h_out) {
+                              int cap, int32_t* counts, int* roi_h_out, bool async = false) {
     if (!h || !h->d_blob) return FM_EINVAL;
+    if (h->pending) {
+        if (async) return hfail(h, FM_ESTATE, "a detection is already queued: collect it first");
+        if (int rc = detect_finish(h)) return rc;  // (queued and never collected)
+    }
     if ((!frames && !list) || n < 1 || H < 1 || W < 1 || roi_w < 1)
         return hfail(h, FM_EINVAL, "bad arguments (n >= 1, frame and ROI sizes >= 1)");
     const int rw = roi_w, rh = (int)(H * ((double)roi_w / (double)W));  // imutils.resize(raw, width=roi_w)
@@ -1264,6 +1333,7 @@ static int detect_frames_impl(fm_haar* h, const uint8_t* frames, const uint8_t* 
         roi = src;
     }
     if (h->times) h->tph[0] += hnow() - t0;
+    if (async) return detect_enqueue(h, roi, n, rh, rw, 3, 1, scale_factor, min_neighbors, 0, 0, 0, 0);
     return fm_haar_detect(h, roi, n, rh, rw, 3, 1, scale_factor, min_neighbors, 0, 0, 0, 0, rects, cap, counts);
 }
 
@@ -1283,6 +1353,24 @@ int fm_haar_detect_frame_list(fm_haar* h, const uint8_t* const* frames, int n, i
         if (!frames[i]) return hfail(h, FM_EINVAL, "frame %d: null address", i);
     return detect_frames_impl(h, nullptr, frames, n, H, W, 1, roi_w, scale_factor, min_neighbors, rects, cap, counts,
                               roi_h_out);
+}
+
+int fm_haar_detect_frame_list_async(fm_haar* h, const uint8_t* const* frames, int n, int H, int W, int roi_w,
+                                    double scale_factor, int min_neighbors, int* roi_h_out) {
+    if (!frames) return h ? hfail(h, FM_EINVAL, "null frame list") : FM_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (!frames[i]) return hfail(h, FM_EINVAL, "frame %d: null address", i);
+    return detect_frames_impl(h, nullptr, frames, n, H, W, 1, roi_w, scale_factor, min_neighbors, nullptr, 0, nullptr,
+                              roi_h_out, true);
+}
+
+int fm_haar_collect(fm_haar* h, int32_t* rects, int cap, int32_t* counts, int n) {
+    if (!h) return FM_EINVAL;
+    if (cap < 0 || !counts || (cap > 0 && !rects)) return hfail(h, FM_EINVAL, "bad arguments (counts[n], rects[n][cap])");
+    if (int rc = detect_finish(h)) return rc;
+    if (n != (int)h->out.size()) return hfail(h, FM_ESTATE, "%d images asked for, the last detection had %zu", n, h->out.size());
+    detect_copy(h, rects, cap, counts);
+    return FM_OK;
 }
 
 }  // extern "C"

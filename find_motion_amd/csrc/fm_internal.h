@@ -194,6 +194,11 @@ int fused_max_ksize();
 hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init);
 int pix_lds_bytes(int ksize);
 bool pix_supported(int ksize);
+// small work images (fm_small.hip): k_small_blur (every frame of the launch in parallel) + k_small_scan
+// (one wave per column and tile row, lane = row); sblur: small_scratch_bytes of the batch's frames
+bool small_supported(int h, int w, int ksize);
+size_t small_scratch_bytes(int h, int w, int nty, size_t frames);
+hipError_t launch_small(hipStream_t st, const FusedArgs& a, uint8_t* sblur, uint64_t* ks_blur, uint64_t* ks_scan);
 // CCL over tile summaries; dilate = true: a.bits are threshold rows to dilate into a.dbits
 // gate_wait / gate_done (optional): the labelling kernel waits for gate_wait (the previous batch's
 // labelling) and gate_done is recorded after it, so that one batch's labelling runs at a time

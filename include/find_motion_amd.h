@@ -240,6 +240,16 @@ int fm_haar_detect_frames(fm_haar* det, const uint8_t* frames, int n, int H, int
 int fm_haar_detect_frame_list(fm_haar* det, const uint8_t* const* frames, int n, int H, int W, int roi_w,
                               double scale_factor, int min_neighbors, int32_t* rects, int cap, int32_t* counts,
                               int* roi_h_out);
+/* fm_haar_detect_frame_list without waiting for it: the detection is queued on the detector's own
+ * stream and the call returns; fm_haar_collect waits and returns its results (find_objects' detections
+ * feed only the seen-objects set and the display, never the written-frame decision, fm.py:549-575, 703-731,
+ * so they may be collected a batch later).  One detection in flight per detector (FM_ESTATE otherwise);
+ * the frames must stay where they are until it is collected. */
+int fm_haar_detect_frame_list_async(fm_haar* det, const uint8_t* const* frames, int n, int H, int W, int roi_w,
+                                    double scale_factor, int min_neighbors, int* roi_h_out);
+/* The results of the last detection (waits for a queued one): counts[n] (every rect) and up to cap rects
+ * per image in rects[n][cap][4], as fm_haar_detect_frame_list; may be called again with a larger cap. */
+int fm_haar_collect(fm_haar* det, int32_t* rects, int cap, int32_t* counts, int n);
 /* The ungrouped candidates of image 0 of the last fm_haar_detect (parity
  * tests); returns their number. */
 int fm_haar_candidates(const fm_haar* det, int32_t* rects, int cap);

@@ -124,6 +124,40 @@ def test_detect_frame_list_reads_frames_in_place(W, H, roi_w):
     det.close()
 
 
+def test_detect_frame_list_async_collect():
+    """fm_haar_detect_frame_list_async + fm_haar_collect (the configs[4] bench's overlapped Haar stage):
+    the same detections as the synchronous call and the restatement; a second queue before collecting is
+    refused (FM_ESTATE); collect can be repeated with a larger cap; the synchronous call after an
+    uncollected queue still returns its own results."""
+    import torch
+
+    from find_motion_amd import FMError
+    cs = make_cascade(1, tight=0.38, depth=2, tilted=True)
+    W, H = 1920, 1080
+    raws = np.stack([_raw_frame(s, W, H) for s in range(4)])
+    det = CascadeClassifier(cs)
+    ring = torch.from_numpy(raws).to("cuda:0")
+    torch.cuda.synchronize()
+    ptrs = [ring[k].data_ptr() for k in (3, 1, 0, 2)]
+    sync = det.detect_frame_list(ptrs, H, W, 300, 1.1, 3)
+    assert det.detect_frame_list_async(ptrs, H, W, 300, 1.1, 3) == 4
+    with pytest.raises(FMError):
+        det.detect_frame_list_async(ptrs, H, W, 300, 1.1, 3)
+    got = det.collect(4, cap=1)  # grows the cap and collects again
+    again = det.collect(4)
+    for i, k in enumerate((3, 1, 0, 2)):
+        ref = haar.detect_multiscale(cs, oracle.resize_area_bgr(raws[k], 300), 1.1, 3)
+        assert [tuple(r) for r in got[i].tolist()] == ref, i
+        assert [tuple(r) for r in again[i].tolist()] == ref, i
+        assert [tuple(r) for r in sync[i].tolist()] == ref, i
+    det.detect_frame_list_async(ptrs[:2], H, W, 300, 1.1, 3)
+    later = det.detect_frame_list(ptrs[2:], H, W, 300, 1.1, 3)  # finishes the queued call first
+    for i, k in enumerate((0, 2)):
+        assert [tuple(r) for r in later[i].tolist()] == haar.detect_multiscale(
+            cs, oracle.resize_area_bgr(raws[k], 300), 1.1, 3), i
+    det.close()
+
+
 def test_detect_frames_device_input():
     # frames already resident in HBM (on_device = 1: no H2D copy) give the host path's and the
     # restatement's detections
