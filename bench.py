@@ -40,6 +40,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters
 PCIE_GBS = 63.0  # PCIe Gen5 x16, one direction
 CONFIG5_MASKS = [((0, 0), (639, 359)), ((3839, 2159), (3200, 2159), (3839, 1600))]
 METRIC = "frames/sec on 1080p synthetic video at 1/2/4/8 MI355X; achieved HBM GB/s %peak"
+# kernels the engine times by in-kernel stamps on every launch (fm_capi.cpp KernelTimer::stamp)
+STAMPED = ("pix", "pix_init", "resize_area", "resize_area_fast", "small_blur", "small_scan")
 
 
 def algorithmic_bytes(kernel: str, cfg: dict) -> float | None:
@@ -322,8 +324,8 @@ def roofline_of(ktimes: dict, cfg: dict, ms_per_step: float) -> dict | None:
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": int(n),
-            "timing": "every launch of the timed steps, in-kernel s_memrealtime stamps (first workgroup start, "
-                      "last wave end; 100 MHz)",
+            "timing": ("every launch of the timed steps, in-kernel s_memrealtime stamps (first workgroup start, "
+                       "last wave end; 100 MHz)") if dom in STAMPED else "HIP events around one launch in four",
             # the launches of one stream are serialised, so each is at most a step: a larger figure is a
             # timing fault, never a kernel fraction
             "launch_le_step": bool(avg_s * 1e3 <= ms_per_step * (1 + 1e-6))}

@@ -560,8 +560,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     HIP_TRY(cp, hipSetDevice(p.device));
     c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
                    ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
-    c->use_pix = c->use_fused && pix_supported(p.ksize) && c->work_plane >= 16 && pix_lds_bytes(p.ksize) <= 160 * 1024 &&
-                 dev_env("FM_NO_PIX") == nullptr;
+    c->use_pix = c->use_fused && pix_supported(p.ksize) && (size_t)c->h * c->w >= 16 &&
+                 pix_lds_bytes(p.ksize) <= 160 * 1024 && dev_env("FM_NO_PIX") == nullptr;
     // small work images (mode D): frame-parallel blur + per-pixel scan (fm_small.hip), unless the caller
     // keeps the gray / blur / delta planes (k_pix writes them)
 #ifndef FM_SMALL_DEFAULT

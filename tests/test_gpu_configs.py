@@ -396,3 +396,27 @@ def test_video_motion_live_area_filter_on_gpu(tmp_path):
         counts.append(len(keep))
     assert skipped > 0
     assert vm.written_indices == written_indices(counts, min_time=0.1, cache_time=0.3)
+
+
+@pytest.mark.parametrize("W,H,box,bs,want", [
+    (1920, 1080, 1920, 384, {"pix"}),                   # configs[1] mode F, k 5: the pixel kernel (not k_fused)
+    (3840, 2160, 3840, 183, {"pix"}),                   # configs[4] geometry, k 21
+    (1920, 1080, 100, 20, {"pix", "small_scan"}),       # mode D, k 5 (the small-image path when it is on)
+    (640, 480, 640, 58, {"fused"}),                     # k 11: k_fused
+])
+def test_product_kernel_selection(W, H, box, bs, want):
+    """Which kernel the product runs for each configuration, read from the engine's own launch timing (the
+    round-5 bench ran k_fused at 1080p k = 5 for one build because the pixel-kernel test saw an unset
+    work-plane size: every parity test stayed green on the slower generic path)."""
+    k = make_gaussian(box, bs)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=4,
+                       profile="pix")
+    fr = batch(W, H, 1, 0, 4)
+    for _ in range(2):  # the second batch has no first-frame launch
+        eng.submit(fr)
+        eng.wait()
+    names = {n for n, (ms, cnt) in eng.kernel_times().items() if cnt > 0}
+    eng.close()
+    assert names & want, (names, want)
+    if "fused" not in want:
+        assert "fused" not in names, names
