@@ -5,7 +5,6 @@
 // taps, fixed-point Gaussian taps) once at fm_create, and sequences the
 // kernels of fm_kernels.hip on one HIP stream per context.
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -147,7 +146,6 @@ struct fm_ctx {
     std::vector<double> ts_sum;   // summed phase deltas (cycles)
     std::vector<int64_t> ts_n;
     bool serial = false;  // FM_SERIAL: contour pass on the pixel stream (profiling: no overlap)
-    int cu_offset = -1;   // the pixel stream's CUs (small work images): i % 32 == cu_offset; -1: every CU
     int dbg_skip = 0;  // FM_DEBUG_SKIP: profiling-only stage ablation of k_fused (results invalid)
 };
 
@@ -560,48 +558,19 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     HIP_TRY(cp, hipSetDevice(p.device));
     c->use_fused = p.ksize <= fused_max_ksize() && fused_lds_bytes(p.ksize) <= 160 * 1024 &&
                    ((c->w + 63) / 64) * ((c->h + 63) / 64) <= 8192;  // region labelling holds the tile grid in LDS
-    c->use_pix = c->use_fused && pix_supported(p.ksize) && (size_t)c->h * c->w >= 16 &&
-                 pix_lds_bytes(p.ksize) <= 160 * 1024 && dev_env("FM_NO_PIX") == nullptr;
-    // small work images (mode D): frame-parallel blur + per-pixel scan (fm_small.hip), unless the caller
-    // keeps the gray / blur / delta planes (k_pix writes them)
-#ifndef FM_SMALL_DEFAULT
-#define FM_SMALL_DEFAULT 0  // (round 5 A/B: abvar builds with 1 until the GPU suite is green on it)
-#endif
-    c->use_small = FM_SMALL_DEFAULT && c->use_pix && !(p.flags & FM_FLAG_KEEP_PLANES) && small_supported(c->h, c->w, p.ksize);
+    // small work images (mode D: 1080p -> 100 x 56), any k: frame-parallel blur + per-pixel scan
+    // (fm_small.hip; mode D 634 -> 746 k frames/s, round 5), unless the caller keeps the gray / blur /
+    // delta planes (k_pix writes them).  Both it and k_pix write threshold bits for the dilating contour pass.
+    c->use_small = c->use_fused && (size_t)c->h * c->w >= 16 && !(p.flags & FM_FLAG_KEEP_PLANES) &&
+                   small_supported(c->h, c->w, p.ksize) && dev_env("FM_NO_PIX") == nullptr;
     if (const char* e = dev_env("FM_SMALL")) c->use_small = c->use_small && std::atoi(e) != 0;
-    // Small work image behind a resize (mode D, -B 100: 1080p -> 100 x 56, two 64 x 64 tiles per stream):
-    // the pixel kernel is a few workgroups whose frames run one after another (latency-bound), the
-    // INTER_AREA resize of the next batch streams whole frames over every CU.  Sharing CUs, the resize
-    // doubled the pixel launch (276 -> 540 us per 256 frames, profiles/r04rs_modeD); so the pixel
-    // stream gets 8 CUs of its own, one in 32 (the input stream keeps every CU: mode D 609 -> 651 k,
-    // round 4; a masked input stream was slower whatever it left out).  Contexts sharing a device take
-    // different CUs: the set is CU i with i % 32 == k, k counting the contexts this process created on
-    // the device, offset by LOCAL_RANK (ranks rehearsed on one GPU), so two engines' pixel kernels do
-    // not queue on the same 8 CUs.
-    const long long work_tiles = (long long)((c->w + 63) / 64) * ((c->h + 63) / 64) * p.n_streams;
-    bool cu_split = c->rmode != ResizeMode::Identity && work_tiles <= 16 && !c->use_small;
-    if (const char* e = dev_env("FM_CU_SPLIT")) cu_split = std::atoi(e) != 0 && cu_split;
-    std::vector<uint32_t> pix_mask;
-    if (cu_split) {
-        hipDeviceProp_t prop;
-        HIP_TRY(cp, hipGetDeviceProperties(&prop, p.device));
-        const int ncu = prop.multiProcessorCount;
-        if (ncu >= 64) {
-            static std::atomic<int> split_ctx[64];
-            const char* lr = std::getenv("LOCAL_RANK");
-            const int k = (split_ctx[p.device & 63].fetch_add(1) + (lr ? std::atoi(lr) : 0)) & 31;
-            c->cu_offset = k;
-            pix_mask.assign((ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu; i++)
-                if (i % 32 == k) pix_mask[i / 32] |= 1u << (i % 32);
-        } else {
-            cu_split = false;
-        }
-    }
-    if (cu_split) {
-        HIP_TRY(cp, hipExtStreamCreateWithCUMask(&c->own_stream, (uint32_t)pix_mask.size(), pix_mask.data()));
-    } else {  // the pixel stream at high priority: it gets a hardware queue of its own instead of
-              // sharing one (in order) with a contour-pass stream
+    c->use_pix = c->use_small || (c->use_fused && pix_supported(p.ksize) && (size_t)c->h * c->w >= 16 &&
+                                  pix_lds_bytes(p.ksize) <= 160 * 1024 && dev_env("FM_NO_PIX") == nullptr);
+    // The pixel stream at high priority: it gets a hardware queue of its own instead of sharing one (in
+    // order) with a contour-pass stream.  (Round 4 gave small work images' pixel stream 8 CUs of its own
+    // -- k_pix5's chain / producer waves on two tiles were a latency chain the next resize starved; the
+    // small-image path of round 5 runs a batch's frames in parallel over every CU instead.)
+    {
         int lo = 0, hi = 0;
         HIP_TRY(cp, hipDeviceGetStreamPriorityRange(&lo, &hi));
         if (dev_env("FM_PIX_PRIO_OFF")) hi = lo;

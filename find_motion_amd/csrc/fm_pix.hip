@@ -712,14 +712,13 @@ template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of o
 // side the row parity needs, so no pair is rebuilt with v_alignbit
 // wv: the wave within its workgroup = its 8-row slice of the 64-row tile (flag rows: FLAG_T* from slice 0,
 // FLAG_B* from slice 7)
-// OWNH: Hp is the wave's own H buffer (its first pair row is the wave's), else the tile's shared one
-template <int KC, bool KEEP, bool TAIL, bool SDWA, bool OWNH = false>
+template <int KC, bool KEEP, bool TAIL, bool SDWA>
 __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
                                              int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
                                              uint32_t& flags) {
     using G = PW<KC>;
     uint32_t P[G::NP];
-    const uint32_t* col = Hp + (OWNH ? 0 : (RPWV / 2 * wv) * TS) + ln;
+    const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
 #pragma unroll
     for (int i = 0; i < G::NP; i++) P[i] = col[i * TS];
     const int w = a.w;
@@ -759,6 +758,20 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     });
     tb &= cc.tbmask;
     colbits = tb;
+#ifndef FM_P5_LEAN
+#define FM_P5_LEAN 0  // round-5 A/B: branch-free flag word (one edge ballot), frame pointers by increment
+#endif
+#if FM_P5_LEAN
+    // one edge ballot: the tile's rows 0-1 in wave 0, rows 62-63 in wave 7, nothing in the others; the
+    // flag word from selects only (no wave-uniform branches)
+    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
+    const uint32_t em = wv == 0 ? 3u : wv == NW - 1 ? (3u << (RPWV - 2)) : 0u;
+    const uint64_t edge = __builtin_amdgcn_ballot_w64((tb & em) != 0);
+    const bool w0 = wv == 0;
+    flags = (orr ? FLAG_ANY : 0u) | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u) |
+            (edge ? (w0 ? FLAG_T : FLAG_B) : 0u) | ((edge & 3ull) ? (w0 ? FLAG_TL : FLAG_BL) : 0u) |
+            ((edge >> 62) ? (w0 ? FLAG_TR : FLAG_BR) : 0u);
+#else
     const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
     const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
     const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
@@ -767,6 +780,7 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
     if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
     flags = fl;
+#endif
 }
 
 // Horizontal taps with the byte window folded into the constants: output k of a quad sums its
@@ -875,20 +889,14 @@ struct P5Raw {
 // accumulateWeighted's scalar tail (h*w % 16 != 0), so some waves take the per-pixel test.  Fixed
 // per launch, so the common kernel has a single chain path: a per-wave 3-way branch inside the
 // frame loop made the background registers a phi and cost 8 v_mov_b64 per frame.
-// SPL (small work images, e.g. mode D's 100 x 56: two tiles, 256 frames in a row): 16 waves per tile,
-// waves 0-7 run the chain of their 8 rows and waves 8-15 the taps, gray and loads of the next frames, so a
-// frame's critical path is the longer of the two halves instead of their sum.  (The same split on full
-// grids, 8 chain + 4 producer waves: 375 vs 407 k frames/s, round 4 -- there the CU is issue-bound.)
 // Measured and withdrawn (round 4): 8- / 16-row bands for small images, two tiles per 1,024-thread
-// workgroup sharing the frame barrier, issue priority falling with progress.
-template <bool KEEP, bool TAIL, bool SPL = false>
-__global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
+// workgroup sharing the frame barrier, issue priority falling with progress, chain and producer waves
+// (DESIGN.md §3.1c); round 5: a wave-private variant without the frame barrier (k_pixq, each wave's own
+// gray and taps over its 12 rows: 345-357 vs 383-418 k frames/s) -- small images now take fm_small.hip.
+template <bool KEEP, bool TAIL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
     using G = P5G;
-    constexpr int NPW = 8;  // SPL: producer waves
-    // job rounds per wave: SPL deals the gray slots and tap jobs over the NPW producer waves only
-    constexpr int GJX = SPL ? (G::GSLOTS + NPW - 1) / NPW : G::GJ;
-    constexpr int HJX = SPL ? (G::NH + 64 * NPW - 1) / (64 * NPW) : G::HJ;
-    constexpr int HLASTX = SPL ? (G::NH - (HJX - 1) * 64 * NPW + 63) / 64 : G::HLASTW;
+    constexpr int GJX = G::GJ, HJX = G::HJ;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
@@ -896,8 +904,6 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
     double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);  // blur x alpha (f64)
     const int tid = (int)threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool cw = !SPL || wv < 8;  // SPL: a chain wave (0-7) or a producer (8-15: pw = wv - 8)
-    const int pw = wv - 8, ptid = tid - 512;
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
     const int ti = swizzle_tile(blockIdx.x, a.ntiles);  // contour tile
@@ -924,11 +930,11 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
     // ---- per-thread job plans (frame invariant)
     uint32_t goff[GJX];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
     uint32_t gdst[GJX];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
-    // this wave's gray slots (wave-uniform): the 4 / 4 deal, or SPL's producer waves in turn
-    const int gjobs = SPL ? (cw ? 0 : min(GJX, (G::GSLOTS - pw + NPW - 1) / NPW)) : (wv < 4 ? G::GFAST : G::GSLOW);
+    // this wave's gray slots (wave-uniform): the 4 / 4 deal
+    const int gjobs = wv < 4 ? G::GFAST : G::GSLOW;
 #pragma unroll
     for (int i = 0; i < GJX; i++) {
-        const int slot = SPL ? pw + NPW * i : (wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i);
+        const int slot = wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i;
         const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / G::GQ, gq = j - gr * G::GQ;
         const int x = x0 - 4 + 4 * gq;
@@ -938,10 +944,9 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
         gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
     }
     uint32_t hsrc[HJX], hdst[HJX];
-    const int hjobs = SPL ? (cw ? 0 : HJX) : G::HJ;  // this wave's tap rounds (wave-uniform)
 #pragma unroll
     for (int i = 0; i < HJX; i++) {
-        const int j = SPL ? (cw ? G::NH : ptid + 64 * NPW * i) : tid + G::NTB * i;
+        const int j = tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
         hsrc[i] = (uint32_t)(2 * hr * G::GQ + hq);
@@ -972,7 +977,7 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int j = 0; j < RPWV; j++) {
             const int y = y0 + RPWV * wv + j;
-            const bool in = cw && x < w && y < h;
+            const bool in = x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
@@ -999,6 +1004,11 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int i = 0; i < GJX; i++) load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
     };
+    auto load_at = [&](const uint8_t* fp) __attribute__((always_inline)) {
+        const gbytes_t src = frame_base(fp);
+#pragma unroll
+        for (int i = 0; i < GJX; i++) load12(rw.v[i], src, goff[i]);
+    };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < GJX; i++) {
@@ -1009,7 +1019,7 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
     auto tap_stage = [&](const uint32_t* gb, uint16_t* Hb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < HJX; i++) {
-            if (SPL ? (i >= hjobs || (i == HJX - 1 && pw >= HLASTX)) : (i == G::HJ - 1 && wv >= G::HLASTW)) break;  // wave-uniform
+            if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
             // (qv[3]: the last tap group's window reaches one byte into it, with zero taps there)
             uint32_t qv[4] = {gb[hsrc[i]], gb[hsrc[i] + 1], gb[hsrc[i] + 2], 0u};
             if (edge_tile) {
@@ -1041,50 +1051,22 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
     // All work after the frame's barrier: chain(t), taps(t+1), gray(t+2), then the load of frame
     // t+3 into the registers gray(t+2) just consumed (one iteration in flight).  Loads are
     // unconditional, frame indices clamped to the batch (see load).
-    if (!SPL || !cw) load((size_t)t0 * S + s);  // (SPL: the chain waves load nothing)
+    load((size_t)t0 * S + s);
     gray_stage(gray);
-    if (!SPL || !cw) load((size_t)min(t0 + 1, t1 - 1) * S + s);
+    load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
-    if (!SPL || !cw) load((size_t)min(t0 + 2, t1 - 1) * S + s);
+    load((size_t)min(t0 + 2, t1 - 1) * S + s);
 
     // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
     // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
-    if constexpr (SPL) {
-        if (cw) {  // chain waves: frame t's chain, its bits and flag word
-            for (int t = t0; t < t1; t++) {
-                const int b = (t - t0) & 1;
-                const size_t f = (size_t)t * S + s;
-                lds_barrier();
-                uint32_t colbits = 0, fl = 0;
-                ChainCtx ccf = cc;
-                ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
-                int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
-                asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-                var = __builtin_amdgcn_readfirstlane(var);
-                asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-                const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
-                if (!TAIL || var == 0)
-                    chain_rows_w<KC, KEEP, false, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
-                else
-                    chain_rows_w<KC, KEEP, true, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
-                reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-                if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
-            }
-        } else {  // producers: taps(t+1), gray(t+2), the load of frame t+3
-            for (int t = t0; t < t1; t++) {
-                const int b = (t - t0) & 1;
-                lds_barrier();
-                if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
-                gray_stage(gray + b * G::GBUF);
-                load((size_t)min(t + 3, t1 - 1) * S + s);
-            }
-        }
-    } else {
+    const size_t fstep = (size_t)S * fbytes;  // (FM_P5_LEAN: frame t + 3's address, advanced per frame)
+    const uint8_t* lp = a.src + ((size_t)min(t0 + 3, t1 - 1) * S + s) * fbytes;
+    {
         for (int t = t0; t < t1; t++) {
             const int b = (t - t0) & 1;
             const size_t f = (size_t)t * S + s;
@@ -1112,7 +1094,12 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
             reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
             if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
             // unconditional (see load): past the batch's last frame it re-reads that frame
-            load((size_t)min(t + 3, t1 - 1) * S + s);
+            if constexpr (FM_P5_LEAN) {
+                load_at(lp);
+                lp = t + 4 < t1 ? lp + fstep : lp;
+            } else {
+                load((size_t)min(t + 3, t1 - 1) * S + s);
+            }
         }
     }
 
@@ -1121,7 +1108,7 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int j = 0; j < RPWV; j++) {
         const int y = y0 + RPWV * wv + j;
-        if (cw && x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
+        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
     kstamp_end(a.kstamp);
 #ifdef FM_DEV_SWITCHES
@@ -1132,211 +1119,6 @@ __global__ __launch_bounds__(SPL ? 1024 : 512) __attribute__((amdgpu_waves_per_e
         pts[3] = mt - mt0;
     }
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// k_pixq: the k = 5 chain of k_pix5 with no workgroup barrier in the frame loop (round 5).
-//
-// k_pix5 shares each frame's gray and horizontal taps between the 8 waves of a tile, so every frame
-// ends in an s_barrier: the waves of a tile move in lock step, the slowest one (the younger waves
-// lose issue arbitration) sets each frame's pace, and the SIMD sees four waves that all wait, issue
-// and wait again together (round 4, 574 us per 256-frame 1080p launch: 35 % of wave cycles issuing,
-// 32 % in issue stalls, 32 % parked on s_waitcnt / the barrier).  Here every wave computes the gray
-// and horizontal taps of the 12 rows its 8 output rows need (its own and the 2-row halo each side)
-// into LDS of its own, so no wave ever waits for another: the 8 waves of a tile and the 4 waves of a
-// SIMD are independent pipelines whose stalls the others fill.  The price is the halo: 12 gray and
-// H rows per 8 output rows instead of 8.5 (k_pix5's 68 per 64), ~16 % more VALU work per pixel.
-// LDS order inside one wave needs no barrier: a wave's LDS instructions execute in issue order.
-//   per wave-frame : loads 216 pixel quads (12 rows x 18 quads, 12 B each, one frame ahead in
-//                    registers), gray4 into its gray buffer (4 job rounds); 96 tap jobs (6 row pairs x
-//                    16 quads, 2 rounds) into one of its two H buffers; the chain of its 8 rows from
-//                    the other H buffer (chain_rows_w), its bits and flag word
-// One atab (blur x alpha) per workgroup, filled before one barrier at the start.  Same arithmetic, in
-// the same order, as k_pix5 (gray4, HS taps, chain_rows_w).  Needs w % 4 == 0 and w >= 8.
-struct PQ {
-    static constexpr int GR = RPWV + 4;           // gray rows of a wave: its 8 rows and 2 each side
-    static constexpr int GQ = 18;                 // gray quads per row: columns x0-4 .. x0+67
-    static constexpr int NG = GR * GQ;            // gray jobs per wave-frame (216)
-    static constexpr int GJ = (NG + 63) / 64;     // job rounds (4)
-    static constexpr int NHP = GR / 2;            // H row pairs (6)
-    static constexpr int NH = NHP * (TS / 4);     // tap jobs (96)
-    static constexpr int HJ = (NH + 63) / 64;     // tap rounds (2)
-    static constexpr int GBUF = NG + 64;          // dwords, + a pad slot per lane (idle jobs store there)
-    static constexpr int HBUF = (NHP + 1) * TS;   // u32 pairs, + the pad pair row
-    static constexpr int WAVE_DW = GBUF + 2 * HBUF;
-    static constexpr int bytes = NW * WAVE_DW * 4 + 256 * 8;
-};
-static_assert(PQ::bytes <= 64 * 1024, "k_pixq LDS");
-
-// PF: register sets of in-flight frame loads (1: a frame's loads have the rest of one frame's work to
-// land; 2: two frames', the loop unrolled by two)
-template <bool KEEP, bool TAIL, int PF = 1>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pixq(FusedArgs a) {
-    using G = PQ;
-    constexpr int KC = 5, R = 2;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    double* atab = reinterpret_cast<double*>(smem);  // blur x alpha (f64), the workgroup's
-    const int tid = (int)threadIdx.x, ln = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    uint32_t* gray = reinterpret_cast<uint32_t*>(smem + 256 * 8) + wv * G::WAVE_DW;  // this wave's buffers
-    uint32_t* Hbuf = gray + G::GBUF;                                                 // [2][HBUF]
-    const int s = blockIdx.y;
-    const int h = a.h, w = a.w, S = a.S;
-    const int ti = swizzle_tile(blockIdx.x, a.ntiles);  // contour tile
-    const int tx = ti % a.ntx;
-    const int y0 = (ti / a.ntx) * TS;
-    const int x0 = tx * TS;
-    const int r0 = y0 + RPWV * wv;  // the wave's first row
-    const size_t plane = (size_t)h * w;
-    const size_t fbytes = plane * 3;
-    const bool hk = a.has_keep[s] != 0;
-    const uint8_t* keep = a.keep + (size_t)s * plane;
-    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
-    kstamp_begin(a.kstamp);
-
-    // ---- per-lane job plans (frame invariant)
-    uint32_t goff[G::GJ];  // byte offset of the job's pixel quad in a frame (0: a job that loads nothing)
-    uint32_t gdst[G::GJ];  // its gray dword in the wave's buffer (the lane's pad slot for idle jobs)
-#pragma unroll
-    for (int i = 0; i < G::GJ; i++) {
-        const int j = i * 64 + ln;
-        const int gr = j / G::GQ, gq = j - gr * G::GQ;
-        const int x = x0 - 4 + 4 * gq;
-        const bool live = j < G::NG && x >= 0 && x + 4 <= w;
-        const int y = reflect101(r0 - R + gr, h);
-        goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
-    }
-    // REFLECT_101 quads as k_pix5: left of column 0 (q0 := mirror of q1) and the quad starting at column
-    // w (q1 / q2 := mirror of the quad before it)
-    const bool edge_tile = x0 == 0 || x0 + TS + 4 > w;  // workgroup-uniform
-    const int vq = (w - x0 + 4) / 4;                   // gray quad index of the quad starting at column w
-    uint32_t hsrc[G::HJ], hdst[G::HJ], hfix[G::HJ];
-#pragma unroll
-    for (int i = 0; i < G::HJ; i++) {
-        const int j = i * 64 + ln;
-        const bool live = j < G::NH;
-        const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
-        hsrc[i] = (uint32_t)(2 * hp * G::GQ + hq);
-        hdst[i] = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);  // u32 index of the pair's 4 columns
-        hfix[i] = (x0 == 0 && hq == 0 ? 1u : 0u) | (hq + 1 == vq ? 2u : 0u) | (hq + 2 == vq ? 4u : 0u);
-    }
-
-    // background of the wave's 8 rows x 64 columns -> registers (as k_pix5)
-    double bg[RPWV];
-    ChainCtx cc;
-    {
-        const double* bgi = a.bg_in + (size_t)s * plane;
-        const int x = x0 + ln;
-        cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
-        cc.rowvalid = 0;
-        cc.keep_lo = cc.keep_hi = 0;
-        cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;
-#pragma unroll
-        for (int j = 0; j < RPWV; j++) {
-            const int y = r0 + j;
-            const bool in = x < w && y < h;
-            if (y < h) cc.rowvalid |= 1u << j;
-            bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
-            const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
-            if (j < 4) cc.keep_lo |= kb << (8 * j);
-            else cc.keep_hi |= kb << (8 * (j - 4));
-        }
-        const long long last = (long long)(r0 + RPWV - 1) * w + x0 + TS - 1;
-        cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
-        cc.tbmask = x < w ? cc.rowvalid : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
-    asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
-
-    uint32_t hcs[HS<KC>::NC];
-    hs_consts<KC>(hcs);
-    P5Raw<G::GJ> rw[PF];
-    // unconditional loads (idle jobs read the frame's first 12 B), as in k_pix5
-    auto load = [&](P5Raw<G::GJ>& rr, size_t f) __attribute__((always_inline)) {
-        const gbytes_t src = frame_base(a.src + f * fbytes);
-#pragma unroll
-        for (int i = 0; i < G::GJ; i++) load12(rr.v[i], src, goff[i]);
-    };
-    auto gray_stage = [&](const P5Raw<G::GJ>& rr) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < G::GJ; i++) gray[gdst[i]] = gray4(rr.v[i].x, rr.v[i].y, rr.v[i].z);
-    };
-    auto tap_stage = [&](uint32_t* Hb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < G::HJ; i++) {
-            uint32_t qv[4] = {gray[hsrc[i]], gray[hsrc[i] + 1], gray[hsrc[i] + 2], 0u};
-            uint32_t qw[4] = {gray[hsrc[i] + G::GQ], gray[hsrc[i] + G::GQ + 1], gray[hsrc[i] + G::GQ + 2], 0u};
-            if (edge_tile) {
-                if (hfix[i] & 1) qv[0] = __builtin_amdgcn_perm(qv[1], qv[1], 0x01020000u);
-                if (hfix[i] & 2) qv[1] = __builtin_amdgcn_perm(qv[0], qv[0], 0x00000102u);
-                if (hfix[i] & 4) qv[2] = __builtin_amdgcn_perm(qv[1], qv[1], 0x00000102u);
-                if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
-                if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
-                if (hfix[i] & 4) qw[2] = __builtin_amdgcn_perm(qw[1], qw[1], 0x00000102u);
-            }
-            const uint32_t h0 = hs_tap<KC, 0>(qv, hcs), k0 = hs_tap<KC, 0>(qw, hcs);
-            const uint32_t h1 = hs_tap<KC, 1>(qv, hcs), k1 = hs_tap<KC, 1>(qw, hcs);
-            const uint32_t h2 = hs_tap<KC, 2>(qv, hcs), k2 = hs_tap<KC, 2>(qw, hcs);
-            const uint32_t h3 = hs_tap<KC, 3>(qv, hcs), k3 = hs_tap<KC, 3>(qw, hcs);
-            *reinterpret_cast<uint4*>(Hb + hdst[i]) =
-                make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
-        }
-    };
-    const int t0 = a.t_begin, t1 = a.t_end;
-    const int var0 = TAIL ? (int)(cc.vec == 0) : 0;
-    // One frame step: frame t's chain from H buffer b (when `live`: a wave-uniform test, false only for
-    // the padding step of an odd frame count at PF = 2), its bits and flag word; then frame t + 1's gray
-    // from the registers rr, the loads of frame t + PF + 1 into rr (unconditional, clamped to the batch's
-    // last frame), and frame t + 1's taps into the other H buffer.
-    auto step = [&](int t, P5Raw<G::GJ>& rr, int b, bool live) __attribute__((always_inline)) {
-        const size_t f = (size_t)t * S + s;
-        if (live) {
-            uint32_t colbits = 0, fl = 0;
-            ChainCtx ccf = cc;
-            ccf.rowvalid = __builtin_amdgcn_readfirstlane(ccf.rowvalid);
-            int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
-            asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
-            var = __builtin_amdgcn_readfirstlane(var);
-            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
-            const uint32_t* Hp = Hbuf + b * G::HBUF;
-            if (!TAIL || var == 0)
-                chain_rows_w<KC, KEEP, false, false, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
-            else
-                chain_rows_w<KC, KEEP, true, false, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
-            // stored before the next loads: vmcnt counts stores and loads in issue order, so a store issued
-            // after the prefetch would be waited for with it
-            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
-        }
-        gray_stage(rr);
-        load(rr, (size_t)min(t + PF + 1, t1 - 1) * S + s);
-        tap_stage(Hbuf + (b ^ 1) * G::HBUF);
-    };
-    load(rw[0], (size_t)t0 * S + s);
-    gray_stage(rw[0]);
-    load(rw[0], (size_t)min(t0 + PF, t1 - 1) * S + s);
-    if constexpr (PF == 2) load(rw[1], (size_t)min(t0 + 1, t1 - 1) * S + s);
-    tap_stage(Hbuf);
-    __syncthreads();  // atab (the only cross-wave data)
-    if constexpr (PF == 1) {
-        for (int t = t0; t < t1; t++) step(t, rw[0], (t - t0) & 1, true);
-    } else {
-        for (int t = t0; t < t1; t += 2) {
-            step(t, rw[1], 0, true);
-            step(t + 1, rw[0], 1, t + 1 < t1);
-        }
-    }
-
-    double* bgo = a.bg_out + (size_t)s * plane;
-    const int x = x0 + ln;
-#pragma unroll
-    for (int j = 0; j < RPWV; j++) {
-        const int y = r0 + j;
-        if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
-    }
-    kstamp_end(a.kstamp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1556,32 +1338,10 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
         px::P5G::bytes <= 64 * 1024) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
         const size_t lds = px::P5G::dyn_bytes;
-        // small work images (<= 16 tiles, e.g. mode D's two): 16 waves per tile, chain and producer halves
-        // (k_pix5 SPL; mode D +3.4 %, round 4)
-        const bool spl = a.ntiles * a.S <= 16;
-#ifndef FM_PIXQ
-#define FM_PIXQ 0  // 1 / 2: larger images on k_pixq<PF = 1 / 2> (no frame barrier; round 5, A/B); 0: k_pix5
-#endif
-        if (FM_PIXQ && !spl) {
-            constexpr int PF = FM_PIXQ == 2 ? 2 : 1;
-            const size_t qlds = px::PQ::bytes;
-            if (keep && tail) hipLaunchKernelGGL((px::k_pixq<true, true, PF>), grid, dim3(512), qlds, st, a);
-            else if (keep) hipLaunchKernelGGL((px::k_pixq<true, false, PF>), grid, dim3(512), qlds, st, a);
-            else if (tail) hipLaunchKernelGGL((px::k_pixq<false, true, PF>), grid, dim3(512), qlds, st, a);
-            else hipLaunchKernelGGL((px::k_pixq<false, false, PF>), grid, dim3(512), qlds, st, a);
-            return hipGetLastError();
-        }
-#define FM_P5_LAUNCH(SP)                                                                                       \
-    do {                                                                                                       \
-        const dim3 blk(SP ? 1024 : 512);                                                                       \
-        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, SP>), grid, blk, lds, st, a);              \
-        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, SP>), grid, blk, lds, st, a);                \
-        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, SP>), grid, blk, lds, st, a);                \
-        else hipLaunchKernelGGL((px::k_pix5<false, false, SP>), grid, blk, lds, st, a);                         \
-    } while (0)
-        if (spl) FM_P5_LAUNCH(true);
-        else FM_P5_LAUNCH(false);
-#undef FM_P5_LAUNCH
+        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true>), grid, dim3(512), lds, st, a);
+        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false>), grid, dim3(512), lds, st, a);
+        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true>), grid, dim3(512), lds, st, a);
+        else hipLaunchKernelGGL((px::k_pix5<false, false>), grid, dim3(512), lds, st, a);
         return hipGetLastError();
     }
     // k = 21 steady state (config 5) on k_pixw

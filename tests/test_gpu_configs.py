@@ -401,8 +401,9 @@ def test_video_motion_live_area_filter_on_gpu(tmp_path):
 @pytest.mark.parametrize("W,H,box,bs,want", [
     (1920, 1080, 1920, 384, {"pix"}),                   # configs[1] mode F, k 5: the pixel kernel (not k_fused)
     (3840, 2160, 3840, 183, {"pix"}),                   # configs[4] geometry, k 21
-    (1920, 1080, 100, 20, {"pix", "small_scan"}),       # mode D, k 5 (the small-image path when it is on)
-    (640, 480, 640, 58, {"fused"}),                     # k 11: k_fused
+    (1920, 1080, 100, 20, {"small_scan"}),              # mode D, k 5: the small-image path (fm_small.hip)
+    (1920, 1080, 100, 9, {"small_scan"}),               # mode D at k 11: the small-image path takes any k
+    (640, 480, 640, 58, {"fused"}),                     # k 11 on a large image: k_fused
 ])
 def test_product_kernel_selection(W, H, box, bs, want):
     """Which kernel the product runs for each configuration, read from the engine's own launch timing (the

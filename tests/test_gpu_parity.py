@@ -78,6 +78,30 @@ def test_mode_d_1080p():
     run_pair(1920, 1080, 100, T=4, n_batches=2)
 
 
+MASKS_1080 = [((0, 0), (639, 359)), ((1919, 1079), (1500, 1079), (1919, 700))]
+
+
+@pytest.mark.parametrize("W,H,box,bs,S,T,nb,masks", [
+    (1920, 1080, 100, 20, 1, 5, 3, None),        # mode D, the reference CLI default (-B 100 -b 20): k 5
+    (1920, 1080, 100, 20, 1, 1, 4, None),        # one frame per batch (a first-frame launch, then singles)
+    (640, 480, 100, 20, 2, 4, 3, None),          # configs[0] geometry 100 x 75: accumulateWeighted's tail
+    (642, 481, 100, 20, 1, 3, 2, None),          # 100 x 74, 3*W % 4 == 2
+    (1920, 1080, 100, 9, 1, 3, 2, None),         # k 11
+    (1920, 1080, 100, 5, 1, 3, 2, None),         # k 21
+    (1920, 1080, 100, 3, 1, 3, 2, None),         # k 33 (REFLECT_101 past the 56-row image's edge rows)
+    (1920, 1080, 100, 20, 3, 3, 2, MASKS_1080),  # three streams with mask polygons
+    (3840, 2160, 100, 20, 1, 2, 2, None),        # 4K -> 100 x 56 (the 40-tap LDS-staged resize)
+    (1920, 1080, 128, 25, 1, 3, 2, None),        # 128 x 72: two tile rows and columns
+    (337, 203, 100, 20, 2, 3, 2, None),          # odd source size, 100 x 60
+])
+def test_small_image_path_vs_oracle(W, H, box, bs, S, T, nb, masks):
+    """The small-image path (fm_small.hip: every frame's gray / blur / keep-mask in parallel, then one wave
+    per column scanning the frames with the f64 background in a register; the contour tile's column words
+    by ballot) -- the product path for mode D -- against the oracle on every frame: masks, counts, boxes,
+    origins and the background bit for bit."""
+    run_pair(W, H, box, blur_scale=bs, S=S, T=T, n_batches=nb, masks=masks, keep_planes=False)
+
+
 def test_mode_d_resize_paths():
     # staged INTER_AREA (3*W % 16 == 0) with a ragged last tap, the plain kernel (3*W % 16 != 0),
     # two streams through the resize stream
