@@ -414,8 +414,12 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
     # completed inside the timed region.
     depth = eng.max_inflight
 
+    hostt = {"submit": 0.0, "wait": 0.0}  # host seconds in fm_submit / fm_wait (is the loop host-bound?)
+
     def submit(i: int) -> None:
+        t = time.perf_counter()
         eng.submit_device(base + (i % n_batches) * T * frame_bytes, T)
+        hostt["submit"] += time.perf_counter() - t
 
     ccl = {"heavy_tiles": 0, "shared_nodes_max": 0, "fallback_frames": 0, "batches": 0}
 
@@ -460,7 +464,9 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
         for i in range(min(depth, n)):
             submit(first + i)
         for i in range(n):
+            t = time.perf_counter()
             eng.wait()  # completes batch i and frees its slot
+            hostt["wait"] += time.perf_counter() - t
             if det is not None:
                 objects(first + i, i == n - 1)
             st = eng.ccl_stats()  # two mapped-memory words: no device sync
@@ -474,6 +480,7 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
     run(0, warmup)
     eng.reset_kernel_times()
     ccl.update(heavy_tiles=0, shared_nodes_max=0, fallback_frames=0, batches=0)
+    hostt.update(submit=0.0, wait=0.0)
 
     dist.barrier(active)
     torch.cuda.synchronize()
@@ -496,7 +503,8 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
     return {"cfg": cfg, "eng": eng, "host": host, "P": P, "wall": wall, "elapsed": elapsed,
             "value": total_frames / elapsed, "ms_per_step": ms_per_step,
             "roofline": roofline_of(ktimes, cfg, ms_per_step), "kernels": kernels, "haar": hs, "det": det,
-            "footprint": footprint, "ccl": ccl}
+            "footprint": footprint, "ccl": ccl,
+            "host_us_per_step": {k: round(1e6 * v / steps, 1) for k, v in hostt.items()}}
 
 
 def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, backend: str) -> dict:
@@ -507,7 +515,7 @@ def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, back
     leg["eng"].close()
     out = {"workload": leg["cfg"]["workload"], "value": round(leg["value"], 2), "unit": "frames/s",
            "steps": steps, "warmup": warmup, "ms_per_step": round(leg["ms_per_step"], 4), "roofline": leg["roofline"],
-           "kernels": leg["kernels"], "path_hbm_frac": round(leg["value"] / pl.world * path_bytes_per_frame(leg["cfg"])
+           "kernels": leg["kernels"], "host_us_per_step": leg["host_us_per_step"], "path_hbm_frac": round(leg["value"] / pl.world * path_bytes_per_frame(leg["cfg"])
                                                             / 1e9 / HBM_PEAK_GBS, 4)}
     del leg
     import torch
@@ -730,7 +738,8 @@ def main() -> None:
                             "note": "whole-path frames/s per GPU x SURVEY.md §8(d) bytes per frame"},
                "contour_pass": {"heavy_tiles_per_batch": round(ccl["heavy_tiles"] / max(ccl["batches"], 1), 2),
                                 "shared_nodes_max": ccl["shared_nodes_max"],
-                                "fallback_frames": ccl["fallback_frames"]}}
+                                "fallback_frames": ccl["fallback_frames"]},
+               "host_us_per_step": leg["host_us_per_step"]}
         print(json.dumps(out), flush=True)
     dist.finalize(active)
 

@@ -758,20 +758,6 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     });
     tb &= cc.tbmask;
     colbits = tb;
-#ifndef FM_P5_LEAN
-#define FM_P5_LEAN 0  // round-5 A/B: branch-free flag word (one edge ballot), frame pointers by increment
-#endif
-#if FM_P5_LEAN
-    // one edge ballot: the tile's rows 0-1 in wave 0, rows 62-63 in wave 7, nothing in the others; the
-    // flag word from selects only (no wave-uniform branches)
-    const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
-    const uint32_t em = wv == 0 ? 3u : wv == NW - 1 ? (3u << (RPWV - 2)) : 0u;
-    const uint64_t edge = __builtin_amdgcn_ballot_w64((tb & em) != 0);
-    const bool w0 = wv == 0;
-    flags = (orr ? FLAG_ANY : 0u) | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u) |
-            (edge ? (w0 ? FLAG_T : FLAG_B) : 0u) | ((edge & 3ull) ? (w0 ? FLAG_TL : FLAG_BL) : 0u) |
-            ((edge >> 62) ? (w0 ? FLAG_TR : FLAG_BR) : 0u);
-#else
     const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
     const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
     const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
@@ -780,7 +766,6 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
     if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
     if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
     flags = fl;
-#endif
 }
 
 // Horizontal taps with the byte window folded into the constants: output k of a quad sums its
@@ -1004,11 +989,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
 #pragma unroll
         for (int i = 0; i < GJX; i++) load12(rw.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
     };
-    auto load_at = [&](const uint8_t* fp) __attribute__((always_inline)) {
-        const gbytes_t src = frame_base(fp);
-#pragma unroll
-        for (int i = 0; i < GJX; i++) load12(rw.v[i], src, goff[i]);
-    };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < GJX; i++) {
@@ -1064,8 +1044,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
-    const size_t fstep = (size_t)S * fbytes;  // (FM_P5_LEAN: frame t + 3's address, advanced per frame)
-    const uint8_t* lp = a.src + ((size_t)min(t0 + 3, t1 - 1) * S + s) * fbytes;
     {
         for (int t = t0; t < t1; t++) {
             const int b = (t - t0) & 1;
@@ -1094,12 +1072,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
             if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
             // unconditional (see load): past the batch's last frame it re-reads that frame
-            if constexpr (FM_P5_LEAN) {
-                load_at(lp);
-                lp = t + 4 < t1 ? lp + fstep : lp;
-            } else {
-                load((size_t)min(t + 3, t1 - 1) * S + s);
-            }
+            load((size_t)min(t + 3, t1 - 1) * S + s);
         }
     }
 

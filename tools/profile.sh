@@ -10,7 +10,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 PROG=${PROG:-bench.py}
-if [ "$PROG" = bench.py ]; then ARGS="--no-cpu-baseline --no-host-fed --no-mjpeg $*"; else ARGS="$*"; fi
+if [ "$PROG" = bench.py ]; then ARGS="--no-cpu-baseline --no-host-fed --no-mjpeg --no-side $*"; else ARGS="$*"; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $PROG $ARGS > "$OUT/trace.log" 2>&1 || exit 1
 i=0
 for PMC in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
