@@ -5,6 +5,7 @@
 // taps, fixed-point Gaussian taps) once at fm_create, and sequences the
 // kernels of fm_kernels.hip on one HIP stream per context.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -481,7 +482,10 @@ int KernelTimer::fold_stamps() {
     const size_t n = stamp_ids.size();
     std::vector<uint64_t> v(2 * n);
     if (hipMemcpy(v.data(), d_stamps, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    const bool dump = dev_env("FM_STAMP_DUMP") != nullptr;  // dev build: every launch's window to stderr
     for (size_t i = 0; i < n; i++) {
+        if (dump) std::fprintf(stderr, "kstamp %s %llu %llu\n", names[stamp_ids[i]], (unsigned long long)v[2 * i],
+                               (unsigned long long)v[2 * i + 1]);
         if (v[2 * i] == ~0ull || v[2 * i + 1] <= v[2 * i]) continue;  // (a kernel that does not stamp)
         ms[stamp_ids[i]] += (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
         launches[stamp_ids[i]] += 1;
@@ -1104,11 +1108,17 @@ int fm_wait(fm_ctx* c) {
     const int si = c->inflight.front();
     c->inflight.erase(c->inflight.begin());
     BatchSlot& B = c->slots[si];
+#ifdef FM_DEV_SWITCHES  // host time in fm_wait (dev build): blocked on the batch vs the post-pass after it
+    const auto hw0 = std::chrono::steady_clock::now();
+#endif
     hipError_t e = hipEventSynchronize(B.ev_done);
     if (e != hipSuccess) {
         B.n = 0;
         return fail(c, FM_EHIP, "hipEventSynchronize: %s", hipGetErrorString(e));
     }
+#ifdef FM_DEV_SWITCHES
+    const auto hw1 = std::chrono::steady_clock::now();
+#endif
     const int n = B.n, S = c->p.n_streams, cap = c->rec_cap;
     const size_t F = (size_t)n * S;
     // Frames whose records do not fit the cap are fetched whole, so len(frame.contours)
@@ -1154,6 +1164,9 @@ int fm_wait(fm_ctx* c) {
             }
         }
     }
+#ifdef FM_DEV_SWITCHES
+    const auto hw2 = std::chrono::steady_clock::now();
+#endif
     c->ready_counts.assign(B.h_count, B.h_count + F);
     c->contours.assign(F, {});
     size_t wi = 0;
@@ -1183,6 +1196,19 @@ int fm_wait(fm_ctx* c) {
             o.reserved1 = 0;
         }
     }
+#ifdef FM_DEV_SWITCHES
+    if (c->timer.enabled) {
+        const auto hw3 = std::chrono::steady_clock::now();
+        auto add = [&](const char* name, std::chrono::steady_clock::duration d) {
+            const int id = c->timer.id_of(name);
+            c->timer.ms[id] += std::chrono::duration<double, std::milli>(d).count();
+            c->timer.launches[id] += 1;
+        };
+        add("host:wait_sync", hw1 - hw0);
+        add("host:wait_scan", hw2 - hw1);
+        add("host:wait_records", hw3 - hw2);
+    }
+#endif
     if (c->p.flags & FM_FLAG_CONTOUR_AREA)
         if (int rc = contour_areas(c, B, F)) return rc;
     c->ready = n;

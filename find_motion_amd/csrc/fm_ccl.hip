@@ -594,6 +594,10 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     extern __shared__ int uf[];  // [a.ntiles]
     __shared__ int s_nc, s_nr;
     const int f = blockIdx.x;
+#ifdef FM_DEV_SWITCHES
+    kstamp_begin_grid(a.kstamp);
+    kstamp_end_wg(a.kstamp);  // (the window of interest is the chain's start)
+#endif
     const int nt = a.ntiles, ntx = a.ntx, nty = a.nty;
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -984,6 +988,9 @@ constexpr int FT = 256;
 __global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
     const size_t f = blockIdx.x;
     const size_t F = (size_t)a.T * a.S;
+#ifdef FM_DEV_SWITCHES
+    kstamp_begin_grid(a.kstamp);
+#endif
     if (a.tflag_waves == 1)
         for (int t = threadIdx.x; t < a.ntiles; t += FT) a.tflag[f * a.ntiles + t] = 0;
     if (threadIdx.x == 0) {
@@ -995,6 +1002,9 @@ __global__ __launch_bounds__(FT) void k_counts(FusedArgs a) {
             a.h_stats[1] = a.count[2 * F + 1];
         }
     }
+#ifdef FM_DEV_SWITCHES
+    kstamp_end_wg(a.kstamp);
+#endif
 }
 
 // one thread per 8 mask bytes of one frame; non-candidate tiles are empty
@@ -1103,8 +1113,13 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     const dim3 gf(cc::GW, F);
     int tok = tm ? tm->begin("regions", st) : -1;
     const size_t rg_lds = (size_t)a.ntiles * sizeof(int);
-    if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), rg_lds, st, a);
-    else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), rg_lds, st, a);
+    FusedArgs ar = a, ac = a;  // (dev build: the chain's first and last kernels stamped, for pipeline traces)
+#ifdef FM_DEV_SWITCHES
+    ar.kstamp = tm ? tm->stamp("chain_regions") : nullptr;
+    ac.kstamp = tm ? tm->stamp("chain_counts") : nullptr;
+#endif
+    if (dilate) hipLaunchKernelGGL(cc::k_regions<true>, dim3(F), dim3(cc::RG), rg_lds, st, ar);
+    else hipLaunchKernelGGL(cc::k_regions<false>, dim3(F), dim3(cc::RG), rg_lds, st, ar);
     if (tm) tm->end(tok);
     if (gate_wait) {
         const hipError_t e = hipStreamWaitEvent(st, gate_wait, 0);
@@ -1125,7 +1140,7 @@ hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, Kern
     tok = tm ? tm->begin("fold_emit", st) : -1;
     hipLaunchKernelGGL(cc::k_fold, gf, dim3(64 * cc::CW), 0, st, a);
     hipLaunchKernelGGL(cc::k_emit, gf, dim3(64 * cc::CW), 0, st, a);
-    hipLaunchKernelGGL(cc::k_counts, dim3(F), dim3(cc::FT), 0, st, a);
+    hipLaunchKernelGGL(cc::k_counts, dim3(F), dim3(cc::FT), 0, st, ac);
     if (tm) tm->end(tok);
     return hipGetLastError();
 }

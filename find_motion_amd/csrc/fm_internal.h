@@ -13,6 +13,16 @@
 
 namespace fm {
 
+template <int I> struct IntC { static constexpr int value = I; };
+// compile-time unrolled loop: fn(IntC<0>{}), ..., fn(IntC<N-1>{})
+template <int N, int I = 0, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+    if constexpr (I < N) {
+        fn(IntC<I>{});
+        static_for<N, I + 1>(fn);
+    }
+}
+
 // Developer switches (A/B experiments, profiling stamps) are read from the environment
 // only by the dev build (make VARIANT=dev -> libfm_hip_dev.so); the product library
 // ignores the environment.

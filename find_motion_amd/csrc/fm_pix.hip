@@ -82,15 +82,6 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 
-template <int I> struct IntC { static constexpr int value = I; };
-// compile-time unrolled loop: fn(IntC<0>{}), ..., fn(IntC<N-1>{})
-template <int N, int I = 0, typename Fn>
-__device__ __forceinline__ void static_for(Fn&& fn) {
-    if constexpr (I < N) {
-        fn(IntC<I>{});
-        static_for<N, I + 1>(fn);
-    }
-}
 
 // BGR2GRAY of 4 consecutive pixels packed in 3 dwords (B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3):
 // (1868 B + 9617 G + 4899 R + 8192) >> 14 computed with all constants x4, so that

@@ -30,7 +30,11 @@ namespace sm {
 
 constexpr int BT = 256;  // k_small_blur threads
 constexpr int ST = 256;  // k_small_scan threads (4 waves, each its own job)
-constexpr int PFD = 8;   // k_small_scan: frames of blur bytes loaded ahead
+#ifndef FM_SMALL_NG
+#define FM_SMALL_NG 2
+#endif
+constexpr int PFD = 8;            // k_small_scan: frames per group of blur-byte loads
+constexpr int NG = FM_SMALL_NG;   // groups in flight
 
 __device__ __forceinline__ int refl(int p, int len) {  // BORDER_REFLECT_101 (any distance)
     if ((unsigned)p < (unsigned)len) return p;
@@ -141,22 +145,20 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
         const uint8_t* col = sblur + (size_t)x * CS + yl;
         const size_t fstride = (size_t)S * w * CS;
         const uint8_t* base = col + (size_t)s * w * CS;
-        uint32_t nb[PFD];
-#pragma unroll
-        for (int k = 0; k < PFD; k++) nb[k] = base[(size_t)min(t0 + k, t1 - 1) * fstride];
         const uint32_t flagL = c < 2 ? (FLAG_L) : 0u, flagR = c >= 62 ? FLAG_R : 0u;
-        for (int tg = t0; tg < t1; tg += PFD) {
-            uint32_t cur[PFD];
+        // blur bytes of NG groups of PFD frames in flight (HBM latency is ~2 us beside the resize; one group
+        // of 8 frames ahead left the scan waiting for every group)
+        uint32_t rg[NG][PFD];
+        auto load_group = [&](uint32_t (&r)[PFD], int tg) __attribute__((always_inline)) {
 #pragma unroll
-            for (int k = 0; k < PFD; k++) cur[k] = nb[k];
-            // the next group's bytes (unconditional, clamped to the batch's last frame)
-#pragma unroll
-            for (int k = 0; k < PFD; k++) nb[k] = base[(size_t)min(tg + PFD + k, t1 - 1) * fstride];
+            for (int k = 0; k < PFD; k++) r[k] = base[(size_t)min(tg + k, t1 - 1) * fstride];  // clamped: unconditional
+        };
+        auto run_group = [&](const uint32_t (&r)[PFD], int tg) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFD; k++) {
                 const int t = tg + k;
                 if (t >= t1) break;  // wave-uniform
-                const uint32_t blur = cur[k];
+                const uint32_t blur = r[k];
                 const double bv = (init0 && t == t0) ? (double)blur : bg;
                 const int q = min(max(__float2int_rn(fabsf(__double2float_rn(bv))), 0), 255);
                 const int d = abs((int)blur - q);
@@ -174,6 +176,14 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                     }
                 }
             }
+        };
+        static_for<NG>([&](auto g) { load_group(rg[decltype(g)::value], t0 + decltype(g)::value * PFD); });
+        for (int tg = t0; tg < t1; tg += NG * PFD) {
+            static_for<NG>([&](auto g) {
+                constexpr int G = decltype(g)::value;
+                run_group(rg[G], tg + G * PFD);
+                load_group(rg[G], tg + (NG + G) * PFD);
+            });
         }
         if (valid) a.bg_out[(size_t)s * plane + li] = bg;
     }
