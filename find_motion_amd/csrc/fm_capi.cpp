@@ -59,7 +59,7 @@ struct BatchSlot {
     int32_t* d_regrep = nullptr;    // [F][ntiles] empty tile -> region representative
     int32_t* d_ncr = nullptr;       // [F][2]
     int32_t* d_heavy = nullptr;     // [F * ntiles] heavy-tile list
-    int32_t* d_count = nullptr;     // [2F+2]
+    int32_t* d_count = nullptr;     // [3F+3]: counts, overflow flags, pool / heavy words, frame quotas, frames done
     int32_t* h_count = nullptr;     // pinned [F]
     int32_t* h_overflow = nullptr;  // pinned [F]
     int32_t* dh_count = nullptr;     // device aliases of the two (mapped): the fused path's k_counts writes them
@@ -118,6 +118,7 @@ struct fm_ctx {
     bool use_fused = false;
     bool use_pix = false;          // k_pix + dilating tile CCL (else k_fused dilates itself)
     bool use_small = false;        // the pixel stage as k_small_blur + k_small_scan (small work images)
+    bool frame_ccl = false;        // the contour pass as one workgroup per frame (ntiles <= kFrameCclTiles)
     int ntx = 0, nty = 0, ntiles = 0, nnodes = 0;  // nnodes: per batch slot
     int nquota = 0;                                             // nodes of each frame's quota
     int32_t *d_xofs = nullptr, *d_xcnt = nullptr, *d_yofs = nullptr, *d_ycnt = nullptr;
@@ -619,6 +620,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         c->ntx = (c->w + 63) / 64;
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
+        c->frame_ccl = c->ntiles <= kFrameCclTiles;
+        if (const char* e = dev_env("FM_FRAME_CCL")) c->frame_ccl = c->frame_ccl && std::atoi(e) != 0;
         // union-find nodes: one per empty-tile region slot, each frame's quota, and a shared
         // overflow pool that holds at least one worst-case frame (frames past it take the
         // pixel-level fallback)
@@ -640,7 +643,10 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
     for (int i = 0; i < c->nslots; i++) {
         BatchSlot& b = c->slots[i];
         if (c->rmode != ResizeMode::Identity && (rc = dalloc(cp, &b.d_work, px * 3))) return rc;
-        if ((rc = dalloc(cp, &b.d_count, 3 * frames + 2))) return rc;
+        if ((rc = dalloc(cp, &b.d_count, 3 * frames + 3))) return rc;
+        // (k_frame_contours re-arms its slot-wide words at the end of each batch: they start at zero)
+        if (hipMemset(b.d_count, 0, (3 * frames + 3) * sizeof(int32_t)) != hipSuccess)
+            return fail(cp, FM_EHIP, "hipMemset of the batch counters failed");
         if ((p.flags & FM_FLAG_KEEP_PLANES) && (rc = dalloc(cp, &b.d_planes, px * 3))) return rc;
         if (c->use_fused) {
             if ((rc = dalloc(cp, &b.d_heavy, frames * c->ntiles)) ||
@@ -1020,10 +1026,18 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
         // the labelling gate: one batch's labelling kernel at a time (the previous batch's, on another contour
         // stream, is waited for), so the labelling of consecutive chains never bunches beside a pixel launch
         // (+1.5 %, 388.1 vs 382.3 k, 4 alternating rounds, round 3)
-        hipEvent_t gate_wait = nullptr;
-        if (!c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
-        HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, B.ev_lab));
-        c->lab_prev = si;  // counts land in mapped h_count / h_overflow
+        if (c->frame_ccl) {  // small work images: the whole pass of a frame in one workgroup (no gate needed)
+            FusedArgs fc = fa;
+#ifdef FM_DEV_SWITCHES
+            fc.kstamp = c->timer.stamp("frame_contours");
+#endif
+            HIP_TRY(c, launch_frame_contours(cs, fc, c->use_pix));
+        } else {
+            hipEvent_t gate_wait = nullptr;
+            if (!c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
+            HIP_TRY(c, launch_tile_ccl(cs, fa, c->use_pix, &c->timer, gate_wait, B.ev_lab));
+            c->lab_prev = si;
+        }  // counts land in mapped h_count / h_overflow
         B.fa = fa;
         HIP_TRY(c, hipEventRecord(B.ev_done, cs));
     } else {

@@ -586,18 +586,12 @@ __device__ __forceinline__ bool is_candidate_lds(const int* fl, const FusedArgs&
 
 // one workgroup per frame: candidate list, empty-tile regions (4-connected: two
 // empty tiles share a whole background edge), one node per region
-template <bool DILATE>
 // (uf is sized to the frame's tiles at launch: a fixed MAX_REGION_TILES array was 32 KB of LDS per
 // workgroup, which the contour kernels resident beside the pixel kernel often did not leave free,
 // so a batch's k_regions waited for the pixel kernel to end: 269 µs instead of 10)
-__global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
-    extern __shared__ int uf[];  // [a.ntiles]
-    __shared__ int s_nc, s_nr;
-    const int f = blockIdx.x;
-#ifdef FM_DEV_SWITCHES
-    kstamp_begin_grid(a.kstamp);
-    kstamp_end_wg(a.kstamp);  // (the window of interest is the chain's start)
-#endif
+// RG threads of one workgroup; SLOT: frame 0 also zeroes the slot-wide counters (node pool, heavy list)
+template <bool DILATE, int RG, bool SLOT>
+__device__ __forceinline__ void regions_frame(const FusedArgs& a, int f, int* uf, int& s_nc, int& s_nr) {
     const int nt = a.ntiles, ntx = a.ntx, nty = a.nty;
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -606,7 +600,7 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
         a.count[f] = 0;
         a.count[(size_t)a.T * a.S + f] = 0;
         a.count[2 * (size_t)a.T * a.S + 2 + f] = 0;
-        if (f == 0) {  // node pool and heavy scratch of the slot (read only by later kernels)
+        if (SLOT && f == 0) {  // node pool and heavy scratch of the slot (read only by later kernels)
             a.count[2 * (size_t)a.T * a.S] = 0;
             a.count[2 * (size_t)a.T * a.S + 1] = 0;
         }
@@ -665,6 +659,17 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
     }
 }
 
+template <bool DILATE>
+__global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
+    extern __shared__ int uf[];  // [a.ntiles]
+    __shared__ int s_nc, s_nr;
+#ifdef FM_DEV_SWITCHES
+    kstamp_begin_grid(a.kstamp);
+    kstamp_end_wg(a.kstamp);  // (the window of interest is the chain's start)
+#endif
+    regions_frame<DILATE, RG, true>(a, blockIdx.x, uf, s_nc, s_nr);
+}
+
 
 // grid (GW, F); each wave labels candidates of the frame's list with a stride, in LDS
 // (LIGHT runs); a tile with more runs (a dense texture of small blobs) goes to the
@@ -672,18 +677,36 @@ __global__ __launch_bounds__(RG) void k_regions(FusedArgs a) {
 // k_tile_ccl is compiled for 6 waves per SIMD: 80 VGPRs (was 96, no spills), so two of its workgroups
 // fit beside two k_pix5 workgroups (4 x 88 VGPRs per SIMD): +1.2 %, 4 rounds.  Its scratch is dynamic
 // LDS, so the compiler takes its occupancy from that, not from a static 30 KB (see k_tile_heavy).
+// dilation (fm.py:266) of candidate ti into its dbits, then the light labelling (tile_ccl)
+template <bool DILATE>
+__device__ __forceinline__ int label_tile(const FusedArgs& a, size_t f, int ti, int ln, const Scratch& sc) {
+    FM_STAMP(1);
+    uint64_t m;
+    if (DILATE && !(a.dbg_skip & 128)) {
+        m = dilate_tile(a, f, ti, ln, nullptr);
+        a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
+    } else {
+        m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
+    }
+    FM_STAMP(2);
+    return tile_ccl<LIGHT>(a, f, ti, ln, m, sc);
+}
+
 constexpr size_t TC_WAVE_LDS = ((size_t)(6 * LIGHT + 66) * 4 + 2 * LIGHT + 3 * LIGHT + 15) / 16 * 16;
 constexpr size_t TC_LDS = CW * TC_WAVE_LDS;
+// wave wv's light scratch: par, amin, amax, ay, pairs (u32), rb | ord (u16) | rx0, rx1, rf (u8)
+__device__ __forceinline__ Scratch light_scratch(int* lds, int wv) {
+    int* wb = lds + (size_t)wv * (TC_WAVE_LDS / 4);
+    uint16_t* word = reinterpret_cast<uint16_t*>(wb + 6 * LIGHT + 66);
+    uint8_t* wbyte = reinterpret_cast<uint8_t*>(word + LIGHT);
+    return Scratch{wb, wb + LIGHT, wb + 2 * LIGHT, wb + 3 * LIGHT, wbyte, wbyte + LIGHT, wbyte + 2 * LIGHT,
+                   wb + 6 * LIGHT, word, reinterpret_cast<uint32_t*>(wb + 4 * LIGHT)};
+}
 template <bool DILATE>
 __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(6))) void k_tile_ccl(FusedArgs a) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    // per wave: par, amin, amax, ay, pairs (u32), rb | ord (u16) | rx0, rx1, rf (u8)
     extern __shared__ __attribute__((aligned(16))) int tc_lds[];
-    int* wb = tc_lds + (size_t)wv * (TC_WAVE_LDS / 4);
-    uint16_t* word = reinterpret_cast<uint16_t*>(wb + 6 * LIGHT + 66);
-    uint8_t* wbyte = reinterpret_cast<uint8_t*>(word + LIGHT);
-    const Scratch sc{wb, wb + LIGHT, wb + 2 * LIGHT, wb + 3 * LIGHT, wbyte, wbyte + LIGHT, wbyte + 2 * LIGHT,
-                     wb + 6 * LIGHT, word, reinterpret_cast<uint32_t*>(wb + 4 * LIGHT)};
+    const Scratch sc = light_scratch(tc_lds, wv);
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     const int nc = a.ncr[2 * f];
@@ -691,17 +714,8 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(6))) vo
     for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
         const int ti = a.clist[f * a.ntiles + k];
         if (FM_OOB(a, ti >= 0 && ti < a.ntiles, 1)) continue;
-        FM_STAMP(1);
-        uint64_t m;
-        if (DILATE && !(a.dbg_skip & 128)) {
-            m = dilate_tile(a, f, ti, ln, nullptr);
-            a.dbits[(f * a.ntiles + ti) * 64 + ln] = m;
-        } else {
-            m = a.dbits[(f * a.ntiles + ti) * 64 + ln];
-        }
-        FM_STAMP(2);
         if (a.dbg_skip & 64) continue;  // profiling ablation (results invalid)
-        const int r = tile_ccl<LIGHT>(a, f, ti, ln, m, sc);
+        const int r = label_tile<DILATE>(a, f, ti, ln, sc);
         if (ln == 0) {
             if (r == TCCL_RUNS) {
                 const int hi = atomicAdd(&a.count[2 * F + 1], 1);
@@ -724,9 +738,8 @@ constexpr int NHW = kHeavyWaves;
 // beside it, 26 us alone).  Sized at launch, the allocation is what the code uses.
 constexpr int HV_INT = 4 * MAXR + 2 * MAXR + 68;   // par, amin, amax, ay | pairs (u32) | rb
 constexpr size_t HEAVY_LDS = (size_t)HV_INT * 4 + 3 * MAXR + 2 * MAXR;  // + rx0, rx1, rf (u8), ord (u16)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_tile_heavy(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int hv_lds[];
-    int* par = hv_lds;
+__device__ __forceinline__ Scratch heavy_scratch(int* lds) {
+    int* par = lds;
     int* amin = par + MAXR;
     int* amax = amin + MAXR;
     int* ay = amax + MAXR;
@@ -736,11 +749,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
     uint8_t* rx0 = reinterpret_cast<uint8_t*>(ord + MAXR);
     uint8_t* rx1 = rx0 + MAXR;
     uint8_t* rf = rx1 + MAXR;
+    return Scratch{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_tile_heavy(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int hv_lds[];
     const size_t F = (size_t)a.T * a.S;
     const int n = a.count[2 * F + 1];
     const int ln = threadIdx.x;
     if (FM_OOB(a, n <= (int)(F * a.ntiles), 2)) return;
-    const Scratch sc{par, amin, amax, ay, rx0, rx1, rf, rb, ord, pairs};
+    const Scratch sc = heavy_scratch(hv_lds);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int item = a.heavy[i];
         if (FM_OOB(a, item >= 0 && item < (int)(F * a.ntiles), 4)) continue;
@@ -856,22 +873,26 @@ __device__ __forceinline__ void merge_tile(const FusedArgs& a, size_t f, int t, 
     }
 }
 
+// candidates wave, wave + nwaves, ... of frame f's list (nc of them)
+__device__ __forceinline__ void merge_frame(const FusedArgs& a, size_t f, int nc, int wave, int nwaves, int ln) {
+    const int nt = a.ntiles;
+    const TileRec* TR = a.tiles + f * nt;
+    (void)TR;  // (read by the bounds check of the checked build)
+    const GlobalUF U{a.nodes};
+    for (int k = wave; k < nc; k += nwaves) {
+        const int t = a.clist[f * nt + k];
+        if (FM_OOB(a, t >= 0 && t < nt && TR[t].nbase >= 0 && TR[t].nbase + TR[t].nroots <= a.nnodes, 5)) continue;
+        merge_tile(a, f, t, ln, U);
+    }
+}
+
 // one wave per candidate, lane = edge position
 __global__ __launch_bounds__(64 * CW) void k_merge(FusedArgs a) {
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const size_t f = blockIdx.y;
     const size_t F = (size_t)a.T * a.S;
     if (a.count[F + f]) return;
-    const int nt = a.ntiles;
-    const TileRec* TR = a.tiles + f * nt;
-    (void)TR;  // (read by the bounds check of the checked build)
-    const int nc = a.ncr[2 * f];
-    const GlobalUF U{a.nodes};
-    for (int k = blockIdx.x * CW + wv; k < nc; k += gridDim.x * CW) {
-        const int t = a.clist[f * nt + k];
-        if (FM_OOB(a, t >= 0 && t < nt && TR[t].nbase >= 0 && TR[t].nbase + TR[t].nroots <= a.nnodes, 5)) continue;
-        merge_tile(a, f, t, ln, U);
-    }
+    merge_frame(a, f, a.ncr[2 * f], blockIdx.x * CW + wv, gridDim.x * CW, ln);
 }
 
 __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
@@ -891,15 +912,10 @@ __device__ __forceinline__ void fold_node(NodeRec* N, int n) {
 
 // one wave per candidate tile (lanes = its components) or per empty-tile region: path
 // compression with outer flags, bboxes and raster-first pixels folded into the roots
-__global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const size_t f = blockIdx.y;
-    const size_t F = (size_t)a.T * a.S;
-    if (a.count[F + f]) return;  // relabelled by the host's pixel-level fallback
+__device__ __forceinline__ void fold_frame(const FusedArgs& a, size_t f, int nc, int nr, int wave, int nwaves, int ln) {
     NodeRec* N = a.nodes;
     const TileRec* TRf = a.tiles + f * a.ntiles;
-    const int nc = a.ncr[2 * f], nr = a.ncr[2 * f + 1];
-    for (int k = blockIdx.x * CW + wv; k < nc + nr; k += gridDim.x * CW) {
+    for (int k = wave; k < nc + nr; k += nwaves) {
         if (k < nc) {
             const int t = a.clist[f * a.ntiles + k];
             if (FM_OOB(a, t >= 0 && t < a.ntiles, 1)) continue;
@@ -912,6 +928,14 @@ __global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
             fold_node(N, (int)(f * a.ntiles) + r);
         }
     }
+}
+
+__global__ __launch_bounds__(64 * CW) void k_fold(FusedArgs a) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const size_t f = blockIdx.y;
+    const size_t F = (size_t)a.T * a.S;
+    if (a.count[F + f]) return;  // relabelled by the host's pixel-level fallback
+    fold_frame(a, f, a.ncr[2 * f], a.ncr[2 * f + 1], blockIdx.x * CW + wv, gridDim.x * CW, ln);
 }
 
 // one wave per candidate tile, lanes = its components: the external test at every
@@ -1096,6 +1120,95 @@ __global__ __launch_bounds__(256) void k_contour_area(AreaMask m, const int32_t*
     area2[i] = (int32_t)(a < 0 ? -a : a);
 }
 
+// ---------------------------------------------------------------------------
+// Small work images (round 5): the whole contour pass of one frame in one workgroup.  Mode D's 100 x 56
+// image is two tiles; the seven-kernel chain above spent its time in launch and cross-queue latency
+// (each batch's chain ran 0.5-1.4 ms after its pixel stage, so with six slots the host waited for
+// chains and the input stream's resizes went idle).  Here the same steps run back to back in one
+// launch, separated by workgroup barriers: regions, dilation + light labelling (a wave per candidate),
+// heavy tiles (wave 0, the workgroup's whole LDS), edge merge, fold, external test + records, counts.
+// Every union-find node a frame touches is its own (its region nodes and its quota; only the shared
+// overflow pool is slot-wide), so no step waits for other frames.  Global writes of one step are read
+// by other waves of the same workgroup in the next: workgroup scope, which a barrier gives on one CU (its
+// L1 is shared by the workgroup).  (Agent-scope fences around each barrier -- an L2 write-back and
+// invalidate each -- made the kernel 500 us per 256 frames and the resize beside it 2.4x slower.)
+constexpr int FW = 4;                     // waves per frame workgroup
+constexpr size_t FR_SCRATCH = FW * TC_WAVE_LDS > HEAVY_LDS ? FW * TC_WAVE_LDS : HEAVY_LDS;
+__device__ __forceinline__ void step_barrier() { __syncthreads(); }
+template <bool DILATE>
+__global__ __launch_bounds__(64 * FW) void k_frame_contours(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int fr_lds[];  // FR_SCRATCH
+    __shared__ int uf[kFrameCclTiles], hl[kFrameCclTiles];
+    __shared__ int s_nc, s_nr, s_nh, s_ovf;
+    const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+    const size_t f = blockIdx.x;
+    const size_t F = (size_t)a.T * a.S;
+#ifdef FM_DEV_SWITCHES
+    kstamp_begin_grid(a.kstamp);
+#endif
+    if (tid == 0) s_nh = s_ovf = 0;
+    regions_frame<DILATE, 64 * FW, false>(a, (int)f, uf, s_nc, s_nr);  // (ends with a barrier)
+    step_barrier();
+    const int nc = s_nc, nr = s_nr;
+    {
+        const Scratch sc = light_scratch(fr_lds, wv);
+        for (int k = wv; k < nc; k += FW) {
+            const int ti = a.clist[f * a.ntiles + k];
+            if (FM_OOB(a, ti >= 0 && ti < a.ntiles, 1)) continue;
+            const int r = label_tile<DILATE>(a, f, ti, ln, sc);
+            if (ln == 0) {
+                if (r == TCCL_RUNS) hl[atomicAdd(&s_nh, 1)] = ti;
+                else if (r != TCCL_OK) s_ovf = 1;
+            }
+        }
+    }
+    step_barrier();
+    const int nh = s_nh;
+    if (nh && wv == 0) {  // tiles with more than LIGHT runs: the whole scratch, one wave
+        const Scratch sc = heavy_scratch(fr_lds);
+        for (int i = 0; i < nh; i++) {
+            const int ti = hl[i];
+            const int r = tile_ccl<MAXR>(a, f, ti, ln, a.dbits[(f * a.ntiles + ti) * 64 + ln], sc);
+            if (r != TCCL_OK && ln == 0) s_ovf = 1;
+        }
+    }
+    step_barrier();
+    const bool ovf = s_ovf != 0;  // (workgroup-uniform) the host relabels the frame (pixel-level fallback)
+    if (!ovf) {
+        merge_frame(a, f, nc, wv, FW, ln);
+        step_barrier();
+        fold_frame(a, f, nc, nr, wv, FW, ln);
+        step_barrier();
+        emit_frame(a, f, wv, FW, ln, a.rec + f * a.cap * 5, &a.count[f], a.cap);
+        step_barrier();
+    }
+    if (tid == 0) {
+        if (ovf) a.count[F + f] = 1;
+        a.h_count[f] = ovf ? 0 : a.count[f];
+        a.h_overflow[f] = ovf ? 1 : 0;
+        // slot-wide tallies: the frame's heavy tiles; the last frame to finish reports them with the shared
+        // pool's use and re-arms the three words for the slot's next batch (the next launch sees the stores).
+        // Every pool and heavy-tally atomic of a workgroup has returned before its frames-done increment is
+        // issued (take_nodes uses its result; the tally's is tested below), so the last workgroup's reads
+        // see them all.
+        const int hb = nh ? atomicAdd(&a.count[2 * F + 1], nh) : 0;
+        if (atomicAdd(&a.count[3 * F + 2], hb < 0 ? 0 : 1) == (int)F - 1) {
+            const int shared = __hip_atomic_load(&a.count[2 * F], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int heavy = __hip_atomic_load(&a.count[2 * F + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.h_stats[0] = shared;
+            a.h_stats[1] = heavy;
+            a.count[2 * F] = 0;
+            a.count[2 * F + 1] = 0;
+            a.count[3 * F + 2] = 0;
+        }
+    }
+    if (a.tflag_waves == 1)  // (the k_fused path's per-tile flag words, as k_counts)
+        for (int t = tid; t < a.ntiles; t += 64 * FW) a.tflag[f * a.ntiles + t] = 0;
+#ifdef FM_DEV_SWITCHES
+    kstamp_end_wg(a.kstamp);
+#endif
+}
+
 }  // namespace cc
 
 hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint8_t* candf, const uint8_t* mask, int ntiles,
@@ -1103,6 +1216,14 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
     if (n <= 0) return hipSuccess;
     const cc::AreaMask m{dbits, candf, mask, ntiles, ntx, h, w};
     hipLaunchKernelGGL(cc::k_contour_area, dim3((n + 255) / 256), dim3(256), 0, st, m, jobs, n, area2);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_contours(hipStream_t st, const FusedArgs& a, bool dilate) {
+    if (a.ntiles > kFrameCclTiles) return hipErrorInvalidValue;
+    const unsigned F = (unsigned)(a.T * a.S);
+    if (dilate) hipLaunchKernelGGL(cc::k_frame_contours<true>, dim3(F), dim3(64 * cc::FW), cc::FR_SCRATCH, st, a);
+    else hipLaunchKernelGGL(cc::k_frame_contours<false>, dim3(F), dim3(64 * cc::FW), cc::FR_SCRATCH, st, a);
     return hipGetLastError();
 }
 

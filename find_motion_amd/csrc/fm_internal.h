@@ -49,6 +49,7 @@ constexpr int kCclBlock = 32;     // CCL block edge (pixels)
 constexpr int kTileMaxRuns = 1600; // runs per 64x64 tile of a dilated mask (<= 24 per row => 1536)
 constexpr int kHeavyWaves = 64;       // k_tile_heavy persistent waves (fm_ccl.hip)
 constexpr int kNodesPerTileFrame = 32; // union-find nodes each frame owns per tile (its quota)
+constexpr int kFrameCclTiles = 16;     // work images of at most this many tiles: one contour workgroup per frame
 constexpr int kNodesShared = 16;       // + a shared overflow pool of this many per tile-frame (at least one
                                        //   worst-case frame), taken from only by frames past their quota
 
@@ -214,6 +215,9 @@ hipError_t launch_small(hipStream_t st, const FusedArgs& a, uint8_t* sblur, uint
 // labelling) and gate_done is recorded after it, so that one batch's labelling runs at a time
 hipError_t launch_tile_ccl(hipStream_t st, const FusedArgs& a, bool dilate, KernelTimer* timer,
                            hipEvent_t gate_wait = nullptr, hipEvent_t gate_done = nullptr);
+// the whole contour pass of each frame in one workgroup (a.ntiles <= kFrameCclTiles; count[] sized 3F + 3, the
+// slot-wide words count[2F], count[2F + 1], count[3F + 2] zero before the first batch: the kernel re-arms them)
+hipError_t launch_frame_contours(hipStream_t st, const FusedArgs& a, bool dilate);
 // every external-contour record of frame f of a finished batch (all of them, unlike the
 // capped k_emit), into rec [cap][5]; *cnt must be 0 before
 hipError_t launch_emit_all(hipStream_t st, const FusedArgs& a, int f, int32_t* rec, int32_t* cnt, int cap);

@@ -33,6 +33,9 @@ constexpr int ST = 256;  // k_small_scan threads (4 waves, each its own job)
 #ifndef FM_SMALL_NG
 #define FM_SMALL_NG 2
 #endif
+#ifndef FM_SCAN_BLOCK
+#define FM_SCAN_BLOCK 0
+#endif
 constexpr int PFD = 8;            // k_small_scan: frames per group of blur-byte loads
 constexpr int NG = FM_SMALL_NG;   // groups in flight
 
@@ -149,6 +152,28 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
         // blur bytes of NG groups of PFD frames in flight (HBM latency is ~2 us beside the resize; one group
         // of 8 frames ahead left the scan waiting for every group)
         uint32_t rg[NG][PFD];
+#if FM_SCAN_BLOCK
+        // each frame's column word into lane (t - t0) % 64 of (wlo, whi); every 64 frames the
+        // block's words are stored (one store, a frame per lane) and their flag words ORed into the tile-frame
+        // flags (one atomic, lanes with bits): no per-frame store, branch or address arithmetic
+        uint32_t wlo = 0, whi = 0;
+        uint64_t* const bits0 = a.bits + ((size_t)s * a.ntiles + tile) * 64 + c;  // frame 0's word of (s, tile, c)
+        uint32_t* const flag0 = a.tflag + ((size_t)s * a.ntiles + tile) * 8;
+        const size_t bstride = (size_t)S * a.ntiles * 64, fstride8 = (size_t)S * a.ntiles * 8;
+        auto flush = [&](int tb, int n) __attribute__((always_inline)) {  // frames tb .. tb + n - 1 in lanes 0 .. n - 1
+            if (ln < n) {
+                const size_t ft = (size_t)(tb + ln);
+                const uint64_t word = ((uint64_t)whi << 32) | wlo;
+                bits0[ft * bstride] = word;
+                if (word) {
+                    const uint32_t fl = FLAG_ANY | flagL | flagR |
+                                        ((word & 3ull) ? (FLAG_T | (c < 2 ? FLAG_TL : 0u) | (c >= 62 ? FLAG_TR : 0u)) : 0u) |
+                                        ((word >> 62) ? (FLAG_B | (c < 2 ? FLAG_BL : 0u) | (c >= 62 ? FLAG_BR : 0u)) : 0u);
+                    atomicOr(&flag0[ft * fstride8], fl);
+                }
+            }
+        };
+#endif
         auto load_group = [&](uint32_t (&r)[PFD], int tg) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFD; k++) r[k] = base[(size_t)min(tg + k, t1 - 1) * fstride];  // clamped: unconditional
@@ -165,6 +190,13 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 const uint64_t word = __builtin_amdgcn_ballot_w64(d > thr) & vmask;
                 const double bl = atab[blur];
                 bg = tail ? __dadd_rn(bl, __dmul_rn(bv, beta)) : __fma_rn(bv, beta, bl);
+#if FM_SCAN_BLOCK
+                const int kb = (t - t0) & 63;
+                const bool mine = ln == kb;
+                wlo = mine ? (uint32_t)word : wlo;
+                whi = mine ? (uint32_t)(word >> 32) : whi;
+                if (kb == 63) flush(t - 63, 64);
+#else
                 const size_t f = (size_t)t * S + s;
                 if (ln == 0) {
                     a.bits[(f * a.ntiles + tile) * 64 + c] = word;
@@ -175,6 +207,7 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                         atomicOr(&a.tflag[(f * a.ntiles + tile) * 8], fl);
                     }
                 }
+#endif
             }
         };
         static_for<NG>([&](auto g) { load_group(rg[decltype(g)::value], t0 + decltype(g)::value * PFD); });
@@ -185,6 +218,9 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 load_group(rg[G], tg + (NG + G) * PFD);
             });
         }
+#if FM_SCAN_BLOCK
+        if (const int nrem = (t1 - t0) & 63) flush(t1 - nrem, nrem);  // the last, partial block
+#endif
         if (valid) a.bg_out[(size_t)s * plane + li] = bg;
     }
     kstamp_end_wg(a.kstamp);

@@ -231,6 +231,57 @@ def test_node_pool_exhaustion_falls_back_to_pixel_ccl():
     eng.close()
 
 
+@pytest.mark.parametrize("depth", [1, 4])
+def test_frame_contour_pass_pool_heavy_tiles_and_slot_reuse(depth):
+    """Work images of at most 16 tiles run the whole contour pass of a frame in one workgroup
+    (k_frame_contours, fm_ccl.hip).  A 200 x 150 dot lattice (12 tiles, ~825 contours per frame, every
+    tile heavy: ~1,100 runs) overflows each frame's node quota into the slot's shared pool, and the heavy
+    tiles run in the workgroup's own LDS; 8 batches of 16 frames reuse the 6 slots, so a pool word not
+    re-armed after a batch would exhaust the pool (fallbacks); depth 4 keeps batches in flight."""
+    H, W, T, NB = 150, 200, 16, 8
+    seq = _lattice_frames(H, W, 6, T * NB - 1, offset=1)  # frame 0 black; avg 0 keeps the background black
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.0,
+                       max_batch=T, max_contours=1024)
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=1, thresh=0, alpha=0.0))
+    res = orc.run(seq[:, 0], cap=1 << 14, mask_frames=range(0, T * NB, 7))
+    assert res.counts[1:].min() > 700
+    submitted = 0
+    for b in range(NB):
+        while submitted < NB and submitted < b + depth:
+            eng.submit(seq[submitted * T:(submitted + 1) * T])
+            submitted += 1
+        eng.wait()
+        st = eng.ccl_stats()
+        assert eng.fallbacks() == 0, f"batch {b}: the shared pool ran out"
+        assert st["shared_nodes"] > 0 and st["heavy_tiles"] >= T, (b, st)
+        for t in range(T):
+            _check_frame(eng, res, t, 0, b * T + t, f"batch {b} frame {t}")
+    eng.close()
+
+
+def test_frame_contour_pass_pool_exhaustion_falls_back():
+    """The same lattice, 64 frames in one batch: the frames' overflow nodes exceed the slot's shared pool
+    (12 tiles x 1,600), so some frames are flagged and relabelled by the host's pixel-level CCL -- every
+    frame still equals the oracle, and the next batch (pool re-armed) needs no fallback."""
+    H, W, T = 150, 200, 64
+    seq = _lattice_frames(H, W, 6, 2 * T - 1, offset=2)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.0,
+                       max_batch=T, max_contours=1024)
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=1, thresh=0, alpha=0.0))
+    res = orc.run(seq[:, 0], cap=1 << 14, mask_frames=range(0, 2 * T, 9))
+    eng.submit(seq[:T])
+    eng.wait()
+    assert eng.fallbacks() > 0
+    for t in range(T):
+        _check_frame(eng, res, t, 0, t, f"frame {t}")
+    eng.submit(seq[T:T + 8])
+    eng.wait()
+    assert eng.fallbacks() == 0
+    for t in range(8):
+        _check_frame(eng, res, t, 0, T + t, f"second batch frame {t}")
+    eng.close()
+
+
 def test_k97_per_frame_path():
     """-B 1920 -b 20 (the CLI's default blur scale at full width): k = 97 > 49 takes the per-frame k_pixel
     kernel and the pixel-level CCL (fm_kernels.hip)."""

@@ -13,7 +13,7 @@ def main(path, last=20):
         p = line.split()
         if len(p) == 4 and p[0] == "kstamp":
             seq[p[1]].append((int(p[2]), int(p[3])))
-    names = [n for n in ("resize_area", "small_blur", "small_scan", "pix", "chain_regions", "chain_counts") if seq.get(n)]
+    names = [n for n in ("resize_area", "small_blur", "small_scan", "pix", "chain_regions", "chain_counts", "frame_contours") if seq.get(n)]
     n = min(len(seq[k]) for k in names)
     rows = [{k: seq[k][len(seq[k]) - n + i] for k in names} for i in range(n)][-last:]
     first = names[0]
@@ -26,8 +26,9 @@ def main(path, last=20):
         d = [(r[k][1] - r[k][0]) / 100 for r in rows]
         print(f"{k:14s} duration avg {sum(d) / len(d):7.1f} us; gap to the next launch avg {sum(g) / max(len(g), 1):7.1f} "
               f"min {min(g, default=0):7.1f} max {max(g, default=0):7.1f}")
-    if "chain_counts" in names:
-        lag = [(r["chain_counts"][1] - r[first][0]) / 100 for r in rows]
+    last_stage = "chain_counts" if "chain_counts" in names else "frame_contours" if "frame_contours" in names else None
+    if last_stage:
+        lag = [(r[last_stage][1] - r[first][0]) / 100 for r in rows]
         print(f"batch latency ({first} start -> chain end): avg {sum(lag) / len(lag):.1f} us, max {max(lag):.1f}")
 
 
