@@ -90,7 +90,9 @@ def pmc_traffic(kernel: str, cfg: dict) -> tuple[int | None, str | None, dict | 
     except (OSError, ValueError):
         return None, None, None
     entries = t.get("entries", [t])  # one entry per profiled workload (tools/traffic.py)
-    e = next((e for e in entries if e.get("workload") == cfg["workload"] and kernel in e.get("kernels", {})), None)
+    # the most recent profile of this workload (entries are appended round by round)
+    e = next((e for e in reversed(entries) if e.get("workload") == cfg["workload"] and kernel in e.get("kernels", {})),
+             None)
     if e is None:
         return None, None, None
     k = e["kernels"][kernel]
@@ -300,7 +302,7 @@ def synthetic_ring(W: int, H: int, S: int, R: int, P: int, streams: list, local:
     return host, ring
 
 
-def roofline_of(ktimes: dict, cfg: dict, ms_per_step: float) -> dict | None:
+def roofline_of(ktimes: dict, cfg: dict, ms_per_step: float, kstd: dict | None = None) -> dict | None:
     """Roofline of the dominant kernel from the engine's per-kernel times (every pixel / resize launch
     timed by in-kernel stamps: first workgroup's start to last wave's end).  In mode D the dominant
     kernel is the INTER_AREA resize, the one kernel there that streams whole frames (the pixel kernel's
@@ -329,6 +331,8 @@ def roofline_of(ktimes: dict, cfg: dict, ms_per_step: float) -> dict | None:
             # the launches of one stream are serialised, so each is at most a step: a larger figure is a
             # timing fault, never a kernel fraction
             "launch_le_step": bool(avg_s * 1e3 <= ms_per_step * (1 + 1e-6))}
+    if kstd and dom in kstd:
+        roof["launch_std_us"] = round(1e3 * kstd[dom], 2)
     if not roof["launch_le_step"]:
         print(f"[bench] WARNING: {dom} averages {avg_s * 1e6:.1f} us per launch, more than the "
               f"{ms_per_step * 1e3:.1f} us step", file=sys.stderr)
@@ -495,14 +499,16 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
         det.close()
 
     ktimes = eng.kernel_times()
+    kstd = eng.kernel_time_std()  # stamped launches: the spread of the launch time over the timed steps
     total_frames = world * S * T * steps
     ms_per_step = 1e3 * elapsed / steps
-    kernels = {name: {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3)}
+    kernels = {name: {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3),
+                      **({"std_us": round(1e3 * kstd[name], 2)} if name in kstd else {})}
                for name, (ms, n) in ktimes.items()}
     del ring
     return {"cfg": cfg, "eng": eng, "host": host, "P": P, "wall": wall, "elapsed": elapsed,
             "value": total_frames / elapsed, "ms_per_step": ms_per_step,
-            "roofline": roofline_of(ktimes, cfg, ms_per_step), "kernels": kernels, "haar": hs, "det": det,
+            "roofline": roofline_of(ktimes, cfg, ms_per_step, kstd), "kernels": kernels, "haar": hs, "det": det,
             "footprint": footprint, "ccl": ccl,
             "host_us_per_step": {k: round(1e6 * v / steps, 1) for k, v in hostt.items()}}
 
@@ -510,7 +516,10 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
 def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, backend: str) -> dict:
     """A compact figure of another configuration for the same JSON line (mode D, the reference CLI's
     default -B 100; configs[2], 8 streams per GPU): value, step time, its own roofline."""
-    steps, warmup = max(5, min(args.steps, 20)), max(2, min(args.warmup, 5))
+    # 60 timed steps whatever the headline's K: a step's batch is submitted and completed inside the timed
+    # region, so the pipeline's fill and drain (the last batch's pixel stage and contour pass after its resize,
+    # ~0.3 ms in mode D) is a fixed cost that 20 steps of ~0.32 ms amortise ~3x less than 60 do
+    steps, warmup = 60, max(2, min(args.warmup, 5))
     leg = run_leg(args, mode, S, T, steps, warmup, pl, local, active, backend)
     leg["eng"].close()
     out = {"workload": leg["cfg"]["workload"], "value": round(leg["value"], 2), "unit": "frames/s",

@@ -405,6 +405,7 @@ int KernelTimer::id_of(const char* name) {
         if (names[i] == name || std::strcmp(names[i], name) == 0) return (int)i;
     names.push_back(name);
     ms.push_back(0);
+    ms_sq.push_back(0);
     launches.push_back(0);
     calls.push_back(0);
     return (int)names.size() - 1;
@@ -488,7 +489,9 @@ int KernelTimer::fold_stamps() {
         if (dump) std::fprintf(stderr, "kstamp %s %llu %llu\n", names[stamp_ids[i]], (unsigned long long)v[2 * i],
                                (unsigned long long)v[2 * i + 1]);
         if (v[2 * i] == ~0ull || v[2 * i + 1] <= v[2 * i]) continue;  // (a kernel that does not stamp)
-        ms[stamp_ids[i]] += (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
+        const double t = (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
+        ms[stamp_ids[i]] += t;
+        ms_sq[stamp_ids[i]] += t * t;
         launches[stamp_ids[i]] += 1;
     }
     for (size_t i = 0; i < n; i++) v[2 * i] = ~0ull, v[2 * i + 1] = 0;
@@ -498,6 +501,7 @@ int KernelTimer::fold_stamps() {
 void KernelTimer::reset() {
     fold_stamps();  // (launches stamped before the reset are dropped with the sums below)
     std::fill(ms.begin(), ms.end(), 0.0);
+    std::fill(ms_sq.begin(), ms_sq.end(), 0.0);
     std::fill(launches.begin(), launches.end(), 0);
     std::fill(calls.begin(), calls.end(), 0);
     unstamped = 0;
@@ -1355,6 +1359,15 @@ int fm_kernel_times(fm_ctx* c, const char** names, double* ms, int64_t* launches
         if (ms) ms[i] = c->timer.ms[i];
         if (launches) launches[i] = c->timer.launches[i];
     }
+    return n;
+}
+
+int fm_kernel_time_spread(fm_ctx* c, double* ms_sq, int cap) {
+    if (!c || !ms_sq) return fail(c, FM_EINVAL, "null argument");
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    if (c->timer.fold_stamps() != 0) return fail(c, FM_EHIP, "reading the launch stamps failed");
+    const int n = (int)c->timer.names.size();
+    for (int i = 0; i < std::min(n, cap); i++) ms_sq[i] = c->timer.ms_sq[i];
     return n;
 }
 

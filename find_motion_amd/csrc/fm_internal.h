@@ -247,6 +247,7 @@ struct KernelTimer {
     std::vector<const char*> names;
     std::vector<double> ms;
     std::vector<int64_t> launches;
+    std::vector<double> ms_sq;      // sum of squared stamped launch times (ms^2)
     uint64_t* d_stamps = nullptr;   // device [kStampRing][2]: (first start, last end), ticks of 10 ns
     std::vector<int> stamp_ids;     // name id of ring entries [0, stamp_ids.size()) not yet folded
     int64_t unstamped = 0;          // launches that found the ring full

@@ -16,8 +16,11 @@
 //   k_small_scan  one wave per (stream, image column, 64-row tile row), lane = row: the frames in order
 //                 with the f64 background in a register -- diff (convertScaleAbs + absdiff), threshold,
 //                 accumulateWeighted -- and __ballot of `d > t` is the tile's column word of threshold
-//                 bits directly (word c = column c, bit r = row r: the contour pass's layout); flags by
-//                 atomic OR into word 0 of the tile-frame's 8 (the reader ORs them), only when set.
+//                 bits directly (word c = column c, bit r = row r: the contour pass's layout).  A block of
+//                 64 frames' words is held one frame per lane and stored at once, with the frames' flags
+//                 ORed atomically into word 0 of each tile-frame's 8 (the reader ORs them) where a word has
+//                 bits: no per-frame store, branch or address arithmetic (1,450 -> 1,002 instructions in the
+//                 kernel, the scan 120 -> 65 us per 256 frames beside the resize, round 5).
 //
 // Same arithmetic as k_pix5 / the oracle: gray (1868 B + 9617 G + 4899 R + 8192) >> 14, blur
 // (sum_y c_y sum_x c_x g + 2^15) >> 16 with OpenCV's 8-bit taps, q = sat_u8(rne(|(float)bg|)),
@@ -30,14 +33,8 @@ namespace sm {
 
 constexpr int BT = 256;  // k_small_blur threads
 constexpr int ST = 256;  // k_small_scan threads (4 waves, each its own job)
-#ifndef FM_SMALL_NG
-#define FM_SMALL_NG 2
-#endif
-#ifndef FM_SCAN_BLOCK
-#define FM_SCAN_BLOCK 0
-#endif
-constexpr int PFD = 8;            // k_small_scan: frames per group of blur-byte loads
-constexpr int NG = FM_SMALL_NG;   // groups in flight
+constexpr int PFD = 8;  // k_small_scan: frames per group of blur-byte loads
+constexpr int NG = 2;   // groups in flight (4 and 8: scans 5 % shorter, mode D unchanged, round 5)
 
 __device__ __forceinline__ int refl(int p, int len) {  // BORDER_REFLECT_101 (any distance)
     if ((unsigned)p < (unsigned)len) return p;
@@ -152,7 +149,6 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
         // blur bytes of NG groups of PFD frames in flight (HBM latency is ~2 us beside the resize; one group
         // of 8 frames ahead left the scan waiting for every group)
         uint32_t rg[NG][PFD];
-#if FM_SCAN_BLOCK
         // each frame's column word into lane (t - t0) % 64 of (wlo, whi); every 64 frames the
         // block's words are stored (one store, a frame per lane) and their flag words ORed into the tile-frame
         // flags (one atomic, lanes with bits): no per-frame store, branch or address arithmetic
@@ -173,7 +169,6 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 }
             }
         };
-#endif
         auto load_group = [&](uint32_t (&r)[PFD], int tg) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFD; k++) r[k] = base[(size_t)min(tg + k, t1 - 1) * fstride];  // clamped: unconditional
@@ -190,24 +185,11 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 const uint64_t word = __builtin_amdgcn_ballot_w64(d > thr) & vmask;
                 const double bl = atab[blur];
                 bg = tail ? __dadd_rn(bl, __dmul_rn(bv, beta)) : __fma_rn(bv, beta, bl);
-#if FM_SCAN_BLOCK
                 const int kb = (t - t0) & 63;
                 const bool mine = ln == kb;
                 wlo = mine ? (uint32_t)word : wlo;
                 whi = mine ? (uint32_t)(word >> 32) : whi;
                 if (kb == 63) flush(t - 63, 64);
-#else
-                const size_t f = (size_t)t * S + s;
-                if (ln == 0) {
-                    a.bits[(f * a.ntiles + tile) * 64 + c] = word;
-                    if (word) {
-                        const uint32_t fl = FLAG_ANY | flagL | flagR |
-                                            ((word & 3ull) ? (FLAG_T | (c < 2 ? FLAG_TL : 0u) | (c >= 62 ? FLAG_TR : 0u)) : 0u) |
-                                            ((word >> 62) ? (FLAG_B | (c < 2 ? FLAG_BL : 0u) | (c >= 62 ? FLAG_BR : 0u)) : 0u);
-                        atomicOr(&a.tflag[(f * a.ntiles + tile) * 8], fl);
-                    }
-                }
-#endif
             }
         };
         static_for<NG>([&](auto g) { load_group(rg[decltype(g)::value], t0 + decltype(g)::value * PFD); });
@@ -218,9 +200,7 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 load_group(rg[G], tg + (NG + G) * PFD);
             });
         }
-#if FM_SCAN_BLOCK
         if (const int nrem = (t1 - t0) & 63) flush(t1 - nrem, nrem);  // the last, partial block
-#endif
         if (valid) a.bg_out[(size_t)s * plane + li] = bg;
     }
     kstamp_end_wg(a.kstamp);

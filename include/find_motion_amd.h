@@ -178,6 +178,10 @@ int fm_footprint(const fm_ctx* ctx, size_t* device_bytes, size_t* pinned_bytes);
 /* FM_FLAG_PROFILE: per-kernel accumulated device time since the last reset.
  * names[i] (static strings), ms[i], launches[i] for i < returned count. */
 int fm_kernel_times(fm_ctx* ctx, const char** names, double* ms, int64_t* launches, int cap);
+/* The same kernels in the same order, with ms_sq[i] = the sum of the squared launch times (ms^2) of the
+ * launches timed by in-kernel stamps (the pixel kernel and the INTER_AREA resize under FM_FLAG_PROFILE_PIX;
+ * 0 for event-timed kernels), for the spread of the launch time across a run. */
+int fm_kernel_time_spread(fm_ctx* ctx, double* ms_sq, int cap);
 int fm_reset_kernel_times(fm_ctx* ctx);
 
 /* Rasterise mask polygons to a keep-mask (mask_off_areas, fm.py:611-636):

@@ -71,3 +71,9 @@ def test_roofline_mode_d_prices_the_resize(bench):
     assert roof["kernel"] == "resize_area"
     assert roof["bytes_per_launch"] == 256 * (1920 * 1080 * 3 + 56 * 100 * 3)
     assert roof["launch_le_step"] is True
+
+
+def test_roofline_carries_the_launch_spread(bench):
+    roof = bench.roofline_of({"pix": (20 * 0.6, 20)}, _cfg(), ms_per_step=0.62, kstd={"pix": 0.0214})
+    assert roof["launch_std_us"] == pytest.approx(21.4)
+    assert "launch_std_us" not in bench.roofline_of({"pix": (20 * 0.6, 20)}, _cfg(), ms_per_step=0.62)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5, call k: k_small_scan storing its column words once per 64 frames (SBLK) vs per frame (P):
-# small-path parity on SBLK, mode D 3 alternating rounds; mode D kernel trace + PMC passes (product).
+# small-path parity on SBLK, mode D 3 alternating rounds; configs[4] with Haar, the detector stream at high (P)
+# or normal (H) priority, 2 rounds; mode D kernel trace + PMC passes (product).
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -16,6 +17,16 @@ for r in 1 2 3; do
     lib=${!v}
     o=$(FM_HIP_LIB=$lib timeout -k 10 200 python bench.py --mode D $J | q) || exit 1
     echo "D r$r $v $o"
+  done
+done
+C5="--width 3840 --height 2160 --blur-scale 183 --streams 4 --batch 64 --ring 64 --ring-period 16 --steps 20 --warmup 10"
+qh() { python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); r=d['roofline']; h=d.get('haar_stage') or {}; print(round(d['value']), d['ms_per_step'], r['avg_launch_us'], r['frac'], {k: h.get(k) for k in ('calls', 'roi_frames', 'detections', 'wall_ms', 'device_ms', 'share_of_step_time')})"; }
+H=$PWD/abvar/hlo/libfm_hip.so
+for r in 1 2; do
+  for v in P H; do
+    lib=${!v}
+    o=$(FM_HIP_LIB=$lib timeout -k 10 300 python bench.py $C5 $J --haar | qh) || exit 1
+    echo "C5 r$r $v $o"
   done
 done
 tools/profile.sh ${TAG}_D --mode D --steps 20 --warmup 5 || exit 1

@@ -18,7 +18,8 @@ import sys
 from collections import defaultdict
 
 SHORT = {"k_pix": "pix", "k_pix5": "pix", "k_pixw": "pix", "k_tile_ccl": "tile_ccl", "k_merge": "merge", "k_fold_emit": "fold_emit", "k_fold": "fold", "k_emit": "emit",
-         "k_regions": "regions", "k_resize_area": "resize_area", "k_pixel": "pixel"}
+         "k_regions": "regions", "k_resize_area": "resize_area", "k_resize_area_nt": "resize_area",
+         "k_small_blur": "small_blur", "k_small_scan": "small_scan", "k_frame_contours": "frame_contours", "k_pixel": "pixel"}
 
 
 def short(name):
