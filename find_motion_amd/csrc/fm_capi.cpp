@@ -589,9 +589,11 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
 #define FM_CCL_QMODE_DEFAULT 2  // contour streams take their own hardware queues (A/B: +3 %)
 #endif
 #ifndef FM_NCCL_DEFAULT
-// two contour streams (round 5, 3 alternating rounds of the driver's command): 1 stream 363-367 k (chains in a
-// row fall behind), 2 streams 400-402 k with the pixel launch's spread 14-22 us, 3 streams 388-400 k, 14-58 us
-#define FM_NCCL_DEFAULT 2
+// three contour streams.  Round 5, 3 alternating rounds each: the driver's command 1 stream 363-367 k (chains in
+// a row fall behind), 2 streams 400-403 k, 3 streams 388-403 k (pixel launch std 14-22 us either way but for
+// one 58 us run); mode D (60 steps) 2 streams 679-697 k, 3 streams 803-810 k (profiles/r05m_ccl_streams_ab.txt,
+// r05o_ccl_streams_ab.txt)
+#define FM_NCCL_DEFAULT 3
 #endif
     int ccl_qmode = FM_CCL_QMODE_DEFAULT;
     if (const char* e = dev_env("FM_CCL_QMODE")) ccl_qmode = std::atoi(e);
