@@ -671,7 +671,7 @@ def main() -> None:
     # PCIe-inclusive, so it is reported beside `value`, never as it.
     host_fed = None
     # per-GPU figure, measured in the 1-GPU run only: every rank would page-lock (depth + 2) batches of
-    # T frames (≈12.7 GB at 6 slots x 256 frames of 1080p), ≈100 GB of pinned host memory on an 8-GPU node
+    # T frames (≈21 GB at 10 slots x 256 frames of 1080p), ≈170 GB of pinned host memory on an 8-GPU node
     if not args.no_host_fed and world == 1:
         from find_motion_amd import videoio
         from find_motion_amd.feeder import BatchFeeder

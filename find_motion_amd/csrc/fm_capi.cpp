@@ -39,8 +39,11 @@ enum class ResizeMode { Identity, Fast, General };
 // contour passes of consecutive batches overlap each other and the next
 // batches' pixel kernels.
 #ifndef FM_SLOTS
-#define FM_SLOTS 6  // with the labelling gate a chain finishes later, and 4 slots left the pixel stream idle
-                    // while the host waited to reuse one: 6 slots 406.4 vs 396.4 k frames/s (4 alternating rounds)
+// with the labelling gate a chain finishes later, and 4 slots left the pixel stream idle while the host waited
+// to reuse one: 6 slots 406.4 vs 396.4 k frames/s (4 alternating rounds, round 3).  Round 5, 6 / 8 / 10 slots
+// (profiles/r05q_slots_ab.txt): the driver's command 374-409 / 401-403 / 393-413 k, mode D (60 steps)
+// 762-767 / 775-792 / 801-805 k; a slot is ~0.41 GB of device memory at the headline shape
+#define FM_SLOTS 10
 #endif
 constexpr int kSlots = FM_SLOTS;
 struct BatchSlot {

@@ -5,10 +5,11 @@ allows, so full-size sequences finish in seconds).
 
 * the bench workload itself: 1080p, mode F, T = 256 frames per launch from a
   256-frame device-resident ring cycling 64 synthetic frames, the production
-  k_pix5 (no planes kept), fm_max_inflight (6) batches submitted before the
-  first wait, 8 batches so that slots are reused;
+  k_pix5 (no planes kept), fm_max_inflight (10) batches submitted before the
+  first wait, 12 batches so that slots are reused;
 * configs[2]: 8 x 1080p streams on one GPU, batches in flight -- also at the
-  perf shape quoted for it (T = 128 per launch, 4 in flight, 7 batches on 6 slots, device ring);
+  perf shape quoted for it (T = 128 per launch, 4 in flight, 7 batches, device ring) and every slot reused
+  at 32 frames per launch;
 * configs[4] geometry: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the two
   MASK_SCHEMA polygons (find_motion.py:86-100) -- also at its perf shape
   (T = 64, 2 in flight);
@@ -46,8 +47,8 @@ def _check_frame(eng, res, t, s, f, tag, mask=True):
 def test_bench_shape_inflight_ring_wrap():
     """bench.py's exact workload (its defaults: --batch 256 --ring 256 --ring-period 64, max_contours 1 << 14,
     fm_max_inflight batches submitted before the first wait) through the production kernel, against the
-    oracle on every frame: 256-frame launches from a 256-frame device ring cycling 64 synthetic frames, six
-    batches in flight, eight batches so that two slots are reused, node pools sized for 256 frames."""
+    oracle on every frame: 256-frame launches from a 256-frame device ring cycling 64 synthetic frames, ten
+    batches in flight, twelve batches so that two slots are reused, node pools sized for 256 frames."""
     torch = pytest.importorskip("torch")
     W, H, T, PERIOD = 1920, 1080, 256, 64
     uniq = batch(W, H, 1, 0, PERIOD)                   # bench: ring slot t holds synthetic frame t % 64
@@ -59,7 +60,7 @@ def test_bench_shape_inflight_ring_wrap():
     assert not eng.keep_planes
     orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=5))
     depth = eng.max_inflight
-    assert depth == 6
+    assert depth == 10
     NB = depth + 2                                     # two batches onto reused slots
     for b in range(depth):
         eng.submit_device(ring.data_ptr(), T)
@@ -168,9 +169,18 @@ def _run_ring(W, H, box, k, S, T, NB, depth, period, masks=None, mask_every=23, 
 @pytest.mark.timeout(400)
 def test_config3_perf_shape_eight_streams_t128():
     """configs[2] at the shape its throughput is quoted on (bench.py --streams 8 --batch 128): 8 x 1080p
-    streams, 128 frames per stream per launch, 4 batches in flight, 7 batches (the 6 slots used round-robin:
-    the last batch reuses the first's slot)."""
+    streams, 128 frames per stream per launch, 4 batches in flight, 7 batches."""
     _run_ring(1920, 1080, 1920, 5, S=8, T=128, NB=7, depth=4, period=64)
+
+
+@pytest.mark.timeout(400)
+def test_eight_streams_slot_reuse():
+    """8 x 1080p streams through every batch slot and round again (fm_max_inflight + 2 batches of 32 frames per
+    stream, 4 in flight): the slots' node pools, records and counters re-armed between batches."""
+    eng = MotionEngine(n_streams=1, src_w=64, src_h=64, box_size=64, ksize=5, max_batch=1)
+    nb = eng.max_inflight + 2
+    eng.close()
+    _run_ring(1920, 1080, 1920, 5, S=8, T=32, NB=nb, depth=4, period=32)
 
 
 @pytest.mark.timeout(400)
@@ -236,9 +246,9 @@ def test_frame_contour_pass_pool_heavy_tiles_and_slot_reuse(depth):
     """Work images of at most 16 tiles run the whole contour pass of a frame in one workgroup
     (k_frame_contours, fm_ccl.hip).  A 200 x 150 dot lattice (12 tiles, ~825 contours per frame, every
     tile heavy: ~1,100 runs) overflows each frame's node quota into the slot's shared pool, and the heavy
-    tiles run in the workgroup's own LDS; 8 batches of 16 frames reuse the 6 slots, so a pool word not
+    tiles run in the workgroup's own LDS; 14 batches of 16 frames reuse the 10 slots, so a pool word not
     re-armed after a batch would exhaust the pool (fallbacks); depth 4 keeps batches in flight."""
-    H, W, T, NB = 150, 200, 16, 8
+    H, W, T, NB = 150, 200, 16, 14
     seq = _lattice_frames(H, W, 6, T * NB - 1, offset=1)  # frame 0 black; avg 0 keeps the background black
     eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.0,
                        max_batch=T, max_contours=1024)
