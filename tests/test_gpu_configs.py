@@ -177,7 +177,7 @@ def test_config3_perf_shape_eight_streams_t128():
 def test_eight_streams_slot_reuse():
     """8 x 1080p streams through every batch slot and round again (fm_max_inflight + 2 batches of 32 frames per
     stream, 4 in flight): the slots' node pools, records and counters re-armed between batches."""
-    eng = MotionEngine(n_streams=1, src_w=64, src_h=64, box_size=64, ksize=5, max_batch=1)
+    eng = MotionEngine(n_streams=1, src_w=64, src_h=64, box_size=64, ksize=5, threshold=12, avg=0.1, max_batch=1)
     nb = eng.max_inflight + 2
     eng.close()
     _run_ring(1920, 1080, 1920, 5, S=8, T=32, NB=nb, depth=4, period=32)
