@@ -44,10 +44,7 @@ constexpr int LIGHT = 256;      // runs held by the light pass
 constexpr int CW = 4;           // waves (tiles) per workgroup in k_tile_ccl / k_merge
 // workgroups per frame in k_tile_ccl / k_merge / k_fold / k_emit.  Measured: with the labelling gate
 // (round 3) 4 392.3k, 6 389.0k, 8 388.4k frames/s (4 alternating rounds)
-#ifndef FM_CCL_GW
-#define FM_CCL_GW 4
-#endif
-constexpr int GW = FM_CCL_GW;
+constexpr int GW = 4;  // (round 5 with ten slots: 4 / 3 / 2 -> 402-407 / 404-413 / 395-406 k, 3 alternating rounds)
 constexpr int RG = 512;         // k_regions threads
 // The contour waves run at the pixel waves' issue priority 0.  (Raised -- labelling 2, heavy tiles 3,
 // merge 2 -- they gained 4 % in round 2; in round 3, 0 gave the same throughput, 368.1 vs 368.2 k,
