@@ -78,6 +78,40 @@ def test_bench_shape_inflight_ring_wrap():
     eng.close()
 
 
+def test_mode_d_bench_shape_inflight_ring_wrap():
+    """bench.py's mode D side leg (`--mode D`: -B 100 -b 20, the reference CLI's default; 256-frame launches
+    from the same device ring, fm_max_inflight batches in flight, two slots reused) through the product path
+    for small work images -- the INTER_AREA resize, k_small_blur + k_small_scan, k_frame_contours -- against
+    the oracle on every frame, and the final background."""
+    torch = pytest.importorskip("torch")
+    W, H, T, PERIOD = 1920, 1080, 256, 64
+    uniq = batch(W, H, 1, 0, PERIOD)
+    ring_h = np.concatenate([uniq] * (T // PERIOD))
+    ring = torch.from_numpy(ring_h).to("cuda:0")
+    torch.cuda.synchronize()
+    k = make_gaussian(100, 20)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=100, ksize=k, threshold=12, avg=0.1, max_batch=T,
+                       max_contours=1 << 14, profile="pix")
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=100, ksize=k))
+    depth = eng.max_inflight
+    NB = depth + 2
+    for b in range(depth):
+        eng.submit_device(ring.data_ptr(), T)
+    total = 0
+    for b in range(NB):
+        res = orc.run(ring_h[:, 0], mask_frames=range(b % 5, T, 17))
+        eng.wait()
+        for t in range(T):
+            _check_frame(eng, res, t, 0, t, f"batch {b} frame {t}")
+        total += int(res.counts.sum())
+        if b + depth < NB:
+            eng.submit_device(ring.data_ptr(), T)
+    np.testing.assert_array_equal(eng.background(0), orc.bg)
+    assert total > 0
+    assert "small_scan" in {n for n, (ms, c) in eng.kernel_times().items() if c > 0}
+    eng.close()
+
+
 def _run_streams(W, H, box, k, S, T, NB, masks=None, start=0, mask_every=7, threads=4):
     eng = MotionEngine(n_streams=S, src_w=W, src_h=H, box_size=box, ksize=k, threshold=12, avg=0.1, max_batch=T)
     h, w = eng.work_shape
