@@ -248,6 +248,41 @@ def test_heavy_tiles_stripes_and_rings():
     run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
 
 
+def _convex_blobs(H, W, rng, n):
+    """n random convex shapes (ellipses, rectangles, parallelograms, dots), some past the image edges: after the
+    5x5 dilation most tiles they touch hold at most one foreground run per row (the contour pass's simple tiles),
+    others two shapes side by side or stacked (the general run labelling)."""
+    yy, xx = np.mgrid[:H, :W]
+    p = np.zeros((H, W), bool)
+    for _ in range(n):
+        kind = rng.integers(4)
+        cy, cx = rng.integers(-20, H + 20), rng.integers(-20, W + 20)
+        if kind == 0:
+            ry, rx = rng.integers(2, 70), rng.integers(2, 70)
+            p |= ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1
+        elif kind == 1:
+            hy, hx = rng.integers(1, 60), rng.integers(1, 90)
+            p |= (np.abs(yy - cy) <= hy) & (np.abs(xx - cx) <= hx)
+        elif kind == 2:  # parallelogram: a slanted band of limited height
+            slope, half, hy = rng.uniform(-3, 3), rng.integers(1, 12), rng.integers(5, 80)
+            p |= (np.abs(xx - cx - slope * (yy - cy)) <= half) & (np.abs(yy - cy) <= hy)
+        else:
+            p[np.clip(cy, 0, H - 1), np.clip(cx, 0, W - 1)] = True
+    return p
+
+
+@pytest.mark.parametrize("W,H,seed", [(200, 150, 1), (200, 150, 2), (330, 260, 3), (330, 260, 4), (128, 64, 5)])
+def test_simple_tiles_vs_oracle(W, H, seed):
+    """Convex blobs whose tiles mostly hold one foreground run per row -- the contour pass's simple-tile path
+    (one component, background chains left and right of it, top and bottom regions, tiles cut by the image's
+    right / bottom edge) -- and mixes with two shapes per tile (the general labelling), on both contour pass
+    layouts (12 / 2 tiles: one workgroup per frame; 30 tiles: the kernel chain), against the oracle."""
+    rng = np.random.default_rng(seed)
+    pats = [_convex_blobs(H, W, rng, n) for n in (1, 2, 3, 5, 8)]
+    frames = _pattern_frames(pats)
+    run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
+
+
 @pytest.mark.parametrize("k", [1, 5])
 @pytest.mark.parametrize("W,H", [(320, 256), (300, 204)])
 def test_full_tiles(W, H, k):
