@@ -77,6 +77,7 @@ struct BatchSlot {
     int n = 0;                      // frames in flight in this slot (0 = none)
     FusedArgs fa{};                 // the contour pass's arguments (fm_wait re-emits frames past the cap)
     uint64_t gen = 0;               // submits into this slot
+    size_t ccl_F = 0;               // frames (T*S) of the slot's last k_frame_contours batch (its re-armed words)
     const uint8_t* src = nullptr;   // the batch's source frames [T][S][H][W][3] on the device (fm_read_frame)
 };
 
@@ -1042,6 +1043,14 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
 #ifdef FM_DEV_SWITCHES
             fc.kstamp = c->timer.stamp("frame_contours");
 #endif
+            // the slot-wide words (shared pool, heavy tally, frames done) sit at indices that depend on the batch's
+            // frame count; the last workgroup re-arms them for a batch of the same size, so a slot whose batch size
+            // changed (a stream's last, partial batch) zeroes them at the new indices first
+            if (B.ccl_F != F) {
+                HIP_TRY(c, hipMemsetAsync(B.d_count + 2 * F, 0, 2 * sizeof(int32_t), cs));
+                HIP_TRY(c, hipMemsetAsync(B.d_count + 3 * F + 2, 0, sizeof(int32_t), cs));
+                B.ccl_F = F;
+            }
             HIP_TRY(c, launch_frame_contours(cs, fc, c->use_pix));
         } else {
             hipEvent_t gate_wait = nullptr;

@@ -303,6 +303,32 @@ def test_frame_contour_pass_pool_heavy_tiles_and_slot_reuse(depth):
     eng.close()
 
 
+def test_frame_contour_pass_varying_batch_sizes():
+    """k_frame_contours keeps its slot-wide words (shared pool, heavy tally, frames done) at indices set by the
+    batch's frame count and re-arms them for the next batch of the same size; a stream's last, partial batch --
+    or any change of size -- lands on a slot whose words sit elsewhere.  Batches of 16, 5, 16, 3, 9, ... frames
+    of the dot lattice (the shared pool in use) over the 10 slots, 3 in flight: every frame against the oracle,
+    no frame falling back."""
+    H, W = 150, 200
+    sizes = [16, 5, 16, 3, 9, 16, 1, 12, 16, 4, 16, 7, 2, 16, 11, 16, 6, 13, 16, 5]
+    seq = _lattice_frames(H, W, 6, sum(sizes) - 1, offset=3)
+    eng = MotionEngine(n_streams=1, src_w=W, src_h=H, box_size=W, ksize=1, threshold=0, avg=0.0,
+                       max_batch=16, max_contours=1024)
+    orc = oracle.OracleStream(oracle.OracleConfig(H=H, W=W, box=W, ksize=1, thresh=0, alpha=0.0))
+    res = orc.run(seq[:, 0], cap=1 << 14, mask_frames=range(0, sum(sizes), 11))
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    depth, submitted = 3, 0
+    for b, n in enumerate(sizes):
+        while submitted < len(sizes) and submitted < b + depth:
+            eng.submit(seq[starts[submitted]:starts[submitted + 1]])
+            submitted += 1
+        eng.wait()
+        assert eng.fallbacks() == 0, f"batch {b} ({n} frames)"
+        for t in range(n):
+            _check_frame(eng, res, t, 0, int(starts[b]) + t, f"batch {b} ({n} frames) frame {t}")
+    eng.close()
+
+
 def test_frame_contour_pass_pool_exhaustion_falls_back():
     """The same lattice, 64 frames in one batch: the frames' overflow nodes exceed the slot's shared pool
     (12 tiles x 1,600), so some frames are flagged and relabelled by the host's pixel-level CCL -- every
