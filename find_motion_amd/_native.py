@@ -25,7 +25,7 @@ EXPORTED = (
     "fm_abi_version", "fm_create", "fm_destroy", "fm_last_error", "fm_work_size", "fm_set_mask",
     "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
-    "fm_kernel_times", "fm_kernel_time_spread", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
+    "fm_kernel_times", "fm_kernel_time_spread", "fm_kernel_time_busy", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
     "fm_host_alloc", "fm_host_free", "fm_last_fallbacks", "fm_last_ccl_stats",
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
@@ -103,6 +103,7 @@ def load() -> C.CDLL:
     L.fm_host_alloc.argtypes = [vp, C.c_size_t, C.POINTER(vp)]
     L.fm_host_free.argtypes = [vp, vp]
     L.fm_kernel_time_spread.argtypes = [vp, vp, i32]
+    L.fm_kernel_time_busy.argtypes = [vp, vp, i32]
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
     L.fm_max_inflight.argtypes = [vp]
@@ -422,6 +423,13 @@ class MotionEngine:
         n = self._check(self._L.fm_kernel_times(self._h, C.cast(names, C.c_void_p), C.cast(ms, C.c_void_p),
                                                 C.cast(n_l, C.c_void_p), 32))
         return {names[i].decode(): (ms[i], n_l[i]) for i in range(min(n, 32))}
+
+    def kernel_time_busy(self) -> dict:
+        """{kernel: ms during which at least one of its stamped launches ran} (fm_kernel_time_busy)."""
+        names = list(self.kernel_times())
+        b = (C.c_double * 32)()
+        n = self._check(self._L.fm_kernel_time_busy(self._h, C.cast(b, C.c_void_p), 32))
+        return {names[i]: b[i] for i in range(min(n, 32, len(names)))}
 
     def kernel_time_std(self) -> dict:
         """{kernel: standard deviation of its launch time in ms} over the stamped launches (the pixel kernel and

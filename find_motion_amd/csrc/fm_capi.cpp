@@ -93,6 +93,7 @@ struct fm_ctx {
     // streams: pixel work (caller-replaceable), contour pass, synchronous reads
     hipStream_t own_stream = nullptr, stream = nullptr, aux_stream = nullptr;
     hipStream_t rs_stream = nullptr;  // input stream: host copies + resize, ahead of the pixel stream
+    hipStream_t rs_stream2 = nullptr; // second input stream (odd slots' resizes), created with the first resize
     hipStream_t ccl_streams[kSlots] = {};
     int lab_prev = -1;  // slot of the last batch whose labelling was enqueued (the labelling gate)
     int nccl = 1;
@@ -410,6 +411,7 @@ int KernelTimer::id_of(const char* name) {
     names.push_back(name);
     ms.push_back(0);
     ms_sq.push_back(0);
+    busy.push_back(Busy{});
     launches.push_back(0);
     calls.push_back(0);
     return (int)names.size() - 1;
@@ -485,6 +487,7 @@ int KernelTimer::fold_stamps() {
     if (stamp_ids.empty()) return 0;
     if (stream) (void)hipStreamSynchronize(stream);
     if (stream2) (void)hipStreamSynchronize(stream2);
+    if (stream3) (void)hipStreamSynchronize(stream3);
     const size_t n = stamp_ids.size();
     std::vector<uint64_t> v(2 * n);
     if (hipMemcpy(v.data(), d_stamps, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -498,6 +501,23 @@ int KernelTimer::fold_stamps() {
         ms_sq[stamp_ids[i]] += t * t;
         launches[stamp_ids[i]] += 1;
     }
+    // the union of each kernel's launch windows (launches of one kernel may overlap: two input streams)
+    std::vector<std::pair<uint64_t, uint64_t>> iv;
+    for (size_t id = 0; id < names.size(); id++) {
+        iv.clear();
+        for (size_t i = 0; i < n; i++)
+            if (stamp_ids[i] == (int)id && v[2 * i] != ~0ull && v[2 * i + 1] > v[2 * i]) iv.emplace_back(v[2 * i], v[2 * i + 1]);
+        std::sort(iv.begin(), iv.end());
+        Busy& b = busy[id];
+        for (const auto& [s0, e0] : iv) {
+            if (b.open && s0 <= b.e) {
+                b.e = std::max(b.e, e0);
+                continue;
+            }
+            if (b.open) b.ms += (double)(b.e - b.s) * 1e-5;
+            b.s = s0, b.e = e0, b.open = true;
+        }
+    }
     for (size_t i = 0; i < n; i++) v[2 * i] = ~0ull, v[2 * i + 1] = 0;
     stamp_ids.clear();
     return hipMemcpy(d_stamps, v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
@@ -506,6 +526,7 @@ void KernelTimer::reset() {
     fold_stamps();  // (launches stamped before the reset are dropped with the sums below)
     std::fill(ms.begin(), ms.end(), 0.0);
     std::fill(ms_sq.begin(), ms_sq.end(), 0.0);
+    std::fill(busy.begin(), busy.end(), Busy{});
     std::fill(launches.begin(), launches.end(), 0);
     std::fill(calls.begin(), calls.end(), 0);
     unstamped = 0;
@@ -771,7 +792,7 @@ void fm_destroy(fm_ctx* c) {
         dfree(c->d_ts);
     }
     (void)hipSetDevice(c->p.device);
-    for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream, c->rs_stream})
+    for (hipStream_t st : {c->own_stream, c->stream, c->aux_stream, c->rs_stream, c->rs_stream2})
         if (st) (void)hipStreamSynchronize(st);
     for (hipStream_t& st : c->ccl_streams)
         if (st) {
@@ -793,7 +814,7 @@ void fm_destroy(fm_ctx* c) {
     dfree(c->d_bg[0]); dfree(c->d_bg[1]); dfree(c->d_keep); dfree(c->d_has_keep); dfree(c->d_init); dfree(c->d_mask);
     dfree(c->d_label); dfree(c->d_cid); dfree(c->d_outer); dfree(c->d_rec_dev); dfree(c->d_rec_one); dfree(c->d_rec_all); dfree(c->d_area);
     dfree(c->d_xofs); dfree(c->d_xcnt); dfree(c->d_xwt); dfree(c->d_yofs); dfree(c->d_ycnt); dfree(c->d_ywt);
-    for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream})
+    for (hipStream_t st : {c->own_stream, c->aux_stream, c->rs_stream, c->rs_stream2})
         if (st) (void)hipStreamDestroy(st);
     if (c->h_err) (void)hipHostFree(c->h_err);
     delete c;
@@ -880,6 +901,20 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
     // resize (many workgroups, HBM-bound) overlaps batch i's pixel kernel (few, when the
     // work image is small); the pixel stream waits for it below
     hipStream_t rs = c->rs_stream ? c->rs_stream : ps;
+#ifndef FM_RS_TWO
+#define FM_RS_TWO 1
+#endif
+    // Consecutive batches' resizes on two input streams (odd slots on the second): in one in-order stream each
+    // waited for the previous one's last wave and then its own dispatch (6-19 us a batch in mode D), on two the
+    // next one's workgroups fill the previous one's tail.  Each batch's resize writes its own slot's buffer, and
+    // the pixel stream waits for its batch's event, so the order of the batches is unchanged.
+    if (FM_RS_TWO && c->rs_stream && !dec && c->rmode != ResizeMode::Identity && (si & 1)) {
+        if (!c->rs_stream2) {
+            HIP_TRY(c, hipStreamCreateWithFlags(&c->rs_stream2, hipStreamNonBlocking));
+            c->timer.stream3 = c->rs_stream2;
+        }
+        rs = c->rs_stream2;
+    }
     const uint8_t* src = frames;
     if (dec) {  // the decode side (§8(f)-3): JPEGs -> BGR frames in the batch's device buffer
         if (!B.d_in) {
@@ -1384,6 +1419,18 @@ int fm_kernel_time_spread(fm_ctx* c, double* ms_sq, int cap) {
     if (c->timer.fold_stamps() != 0) return fail(c, FM_EHIP, "reading the launch stamps failed");
     const int n = (int)c->timer.names.size();
     for (int i = 0; i < std::min(n, cap); i++) ms_sq[i] = c->timer.ms_sq[i];
+    return n;
+}
+
+int fm_kernel_time_busy(fm_ctx* c, double* busy_ms, int cap) {
+    if (!c || !busy_ms) return fail(c, FM_EINVAL, "null argument");
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    if (c->timer.fold_stamps() != 0) return fail(c, FM_EHIP, "reading the launch stamps failed");
+    const int n = (int)c->timer.names.size();
+    for (int i = 0; i < std::min(n, cap); i++) {
+        const auto& b = c->timer.busy[i];
+        busy_ms[i] = b.ms + (b.open ? (double)(b.e - b.s) * 1e-5 : 0.0);
+    }
     return n;
 }
 

@@ -241,6 +241,7 @@ struct KernelTimer {
     std::vector<int64_t> calls;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // also timed in the pixel-only mode: the input stream's resize
+    hipStream_t stream3 = nullptr;  // (the second input stream)
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
@@ -248,6 +249,8 @@ struct KernelTimer {
     std::vector<double> ms;
     std::vector<int64_t> launches;
     std::vector<double> ms_sq;      // sum of squared stamped launch times (ms^2)
+    struct Busy { double ms = 0; uint64_t s = 0, e = 0; bool open = false; };
+    std::vector<Busy> busy;         // union of the stamped launch windows (closed part + the open interval)
     uint64_t* d_stamps = nullptr;   // device [kStampRing][2]: (first start, last end), ticks of 10 ns
     std::vector<int> stamp_ids;     // name id of ring entries [0, stamp_ids.size()) not yet folded
     int64_t unstamped = 0;          // launches that found the ring full

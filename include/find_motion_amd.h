@@ -182,6 +182,10 @@ int fm_kernel_times(fm_ctx* ctx, const char** names, double* ms, int64_t* launch
  * launches timed by in-kernel stamps (the pixel kernel and the INTER_AREA resize under FM_FLAG_PROFILE_PIX;
  * 0 for event-timed kernels), for the spread of the launch time across a run. */
 int fm_kernel_time_spread(fm_ctx* ctx, double* ms_sq, int cap);
+/* The same kernels in the same order, with busy_ms[i] = the time during which at least one of the kernel's
+ * stamped launches was running (the union of their windows; less than the summed launch times when launches
+ * of one kernel overlap, e.g. the resizes of consecutive batches on the two input streams). */
+int fm_kernel_time_busy(fm_ctx* ctx, double* busy_ms, int cap);
 int fm_reset_kernel_times(fm_ctx* ctx);
 
 /* Rasterise mask polygons to a keep-mask (mask_off_areas, fm.py:611-636):

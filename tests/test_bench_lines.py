@@ -77,3 +77,19 @@ def test_roofline_carries_the_launch_spread(bench):
     roof = bench.roofline_of({"pix": (20 * 0.6, 20)}, _cfg(), ms_per_step=0.62, kstd={"pix": 0.0214})
     assert roof["launch_std_us"] == pytest.approx(21.4)
     assert "launch_std_us" not in bench.roofline_of({"pix": (20 * 0.6, 20)}, _cfg(), ms_per_step=0.62)
+
+
+def test_roofline_of_overlapping_launches_uses_their_union(bench):
+    """Mode D's resizes of consecutive batches run on two input streams: each launch lasts ~2 steps, but at most
+    two run at once, so the kernel's throughput is its bytes over the union of the launch windows."""
+    cfg = _cfg(mode="D")
+    ktimes = {"resize_area": (60 * 0.55, 60)}
+    roof = bench.roofline_of(ktimes, cfg, ms_per_step=0.31, kbusy={"resize_area": 60 * 0.3})
+    assert roof["launches_overlap"] and roof["launch_le_step"]
+    assert roof["avg_launch_us"] == pytest.approx(550.0)
+    assert roof["busy_us_per_launch"] == pytest.approx(300.0)
+    assert roof["frac"] == pytest.approx(roof["bytes_per_launch"] / 300e-6 / 1e9 / 8000.0, abs=1e-4)
+    assert roof["frac_per_launch_duration"] == pytest.approx(roof["bytes_per_launch"] / 550e-6 / 1e9 / 8000.0, abs=1e-4)
+    # no overlap: the busy time equals the summed launch times and nothing changes
+    plain = bench.roofline_of(ktimes, cfg, ms_per_step=0.6, kbusy={"resize_area": 60 * 0.55})
+    assert "launches_overlap" not in plain and plain["frac"] == pytest.approx(roof["frac_per_launch_duration"], abs=1e-4)
