@@ -502,6 +502,176 @@ __device__ __forceinline__ bool simple_tile(const FusedArgs& a, size_t f, int ti
     return true;
 }
 
+// Tiles that are neither simple nor full, with at most 64 runs once each streak of identical consecutive rows is
+// kept once (the bench video's other tiles: the jagged edges of large regions, ~100 runs over 64 rows, ~30 runs over
+// ~10 distinct rows).  A row identical to the one above adds nothing to the components -- each of its runs touches
+// exactly the same run above and nothing else -- so it takes the labels of its streak's first row, and the streak's
+// last row is the runs' lowest row.  With one lane per run instead of one per row there are no per-row run loops:
+// a run finds its row from a ballot of the rows' first runs, its extent by clearing the row's lower run starts, the
+// runs it touches in the row above as one range; the union rounds run over those ranges, the fold by LDS atomics,
+// ordinals and the root count by ballot.  Writes the same TileRec and NodeRecs as the run labelling below (roots are
+// raster-first runs, which never lie in a repeated row).  Returns false (nothing written) past 64 runs.
+__device__ __forceinline__ uint64_t lane_up1_64(uint64_t v) {
+    return ((uint64_t)(uint32_t)lane_up1((int)(uint32_t)(v >> 32)) << 32) | (uint32_t)lane_up1((int)(uint32_t)v);
+}
+__device__ __forceinline__ bool compact_tile(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc,
+                                             int& rc) {
+    const int h = a.h, w = a.w;
+    const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
+    // ---- lane = row
+    const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
+    const uint64_t mu = lane_up1_64(m), su = lane_up1_64(starts);  // the row above (row 0: its own)
+    const bool dup = ln > 0 && m == mu;
+    const int nrr = __popcll(starts);
+    const int nr = dup ? 0 : nrr;
+    const int incl = wave_incl_sum(nr);
+    const int total = lane_at(incl, 63);
+    if (total > 64) return false;
+    const int base = incl - nr;
+    const uint64_t ND = __builtin_amdgcn_ballot_w64(!dup);  // each streak's first row (bit 0 always)
+    const int sr = hibit(ND & bits_between(0, ln));
+    const uint64_t nxt = ND & ~bits_between(0, ln);
+    const int se = nxt ? __builtin_ctzll(nxt) - 1 : 63;  // the streak's last row
+    const int bs = __shfl(base, sr, 64);                 // the streak's first run
+    const int ab = lane_up1(bs);                         // first run of the row above (its streak's)
+    int* mark = sc.rb;
+    int* aux = reinterpret_cast<int*>(sc.ord);
+    uint4* rows = reinterpret_cast<uint4*>(sc.pairs);
+    mark[ln] = 0;
+    if (nr > 0) mark[base] = ln + 1;  // (same wave: the stores land in order)
+    rows[2 * ln] = make_uint4((uint32_t)starts, (uint32_t)(starts >> 32), (uint32_t)m, (uint32_t)(m >> 32));
+    rows[2 * ln + 1] = make_uint4((uint32_t)su, (uint32_t)(su >> 32), (uint32_t)mu, (uint32_t)(mu >> 32));
+    aux[ln] = ab | (se << 8);
+    lds_fence();
+    // ---- lane = run (ln < total)
+    const bool live = ln < total;
+    const int mk = mark[ln];
+    const uint64_t SEG = __builtin_amdgcn_ballot_w64(mk != 0);  // runs that start a row (bit 0 always)
+    const int st = hibit(SEG & bits_between(0, ln));
+    const int r = __shfl(mk, st, 64) - 1;  // the run's row
+    const int k = live ? ln - st : 0;      // its index in the row
+    const uint4 q0 = rows[2 * r], q1 = rows[2 * r + 1];
+    const int ax = aux[r];
+    uint64_t sk = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
+    const uint64_t mr = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+    for (int i = 0; i < k; i++) sk &= sk - 1;
+    const int xs = __builtin_ctzll(sk);
+    const uint64_t sk2 = sk & (sk - 1);
+    const int xe = sk2 ? __builtin_ctzll(sk2) - 1 : 63;
+    const bool fg = (mr >> xs) & 1;
+    const int rab = ax & 0xFF, rse = ax >> 8;
+    // the same-colour runs it touches in the row above: ia, ia + 2, .., ib (8-connected foreground, 4-connected background)
+    int ia = 1, ib = 0;
+    if (live && r > 0) {
+        const uint64_t sU = (uint64_t)q1.x | ((uint64_t)q1.y << 32), mU = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
+        const int w0 = fg ? max(xs - 1, 0) : xs, w1 = fg ? min(xe + 1, 63) : xe;
+        const uint64_t hits = (fg ? mU : ~mU) & bits_between(w0, w1);
+        if (hits) {
+            ia = run_at(rab, sU, __builtin_ctzll(hits));
+            ib = run_at(rab, sU, hibit(hits));
+        }
+    }
+    int* par = sc.par;
+    int* amin = sc.amin;
+    int* amax = sc.amax;
+    int* ay = sc.ay;
+    if (live) par[ln] = ln;
+    lds_fence();
+    // union rounds as tile_ccl's (hook the larger parent under the smaller, then shortcut)
+    for (int round = 0; round < 64; round++) {
+        bool ch = false;
+        for (int j = ia; j <= ib; j += 2) {
+            const int ra = lload(&par[ln]), rb2 = lload(&par[j]);
+            if (ra != rb2) {
+                atomicMin(&par[max(ra, rb2)], min(ra, rb2));
+                ch = true;
+            }
+        }
+        lds_fence();
+        if (live) {
+            const int pi = lload(&par[ln]);
+            const int ppi = lload(&par[pi]);
+            if (ppi != pi) {
+                atomicMin(&par[ln], ppi);
+                ch = true;
+            }
+        }
+        lds_fence();
+        if (__builtin_amdgcn_ballot_w64(ch) == 0) break;
+    }
+    // fold into the roots: bounding box and lowest row of foreground components, the outer flag of background ones
+    const int gy = y0 + r;
+    const bool outer = !fg && (x0 + xs == 0 || x0 + xe >= w - 1 || gy == 0 || y0 + rse >= h - 1);
+    const int rt = live ? lload(&par[ln]) : ln;
+    if (live) {
+        amin[ln] = fg ? xs : (int)outer;
+        amax[ln] = xe;
+        ay[ln] = rse;
+    }
+    lds_fence();
+    if (live && rt != ln) {
+        if (fg) {
+            atomicMin(&amin[rt], xs);
+            atomicMax(&amax[rt], xe);
+            atomicMax(&ay[rt], rse);
+        } else if (outer) {
+            atomicOr(&amin[rt], 1);
+        }
+    }
+    lds_fence();
+    const uint64_t RM = __builtin_amdgcn_ballot_w64(live && rt == ln);  // roots, in raster order
+    const int nroots = __popcll(RM);
+    auto ordof = [&](int root) -> int { return __popcll(RM & ((1ull << root) - 1)); };
+    const int nb = take_nodes(a, f, nroots, ln);
+    if (nb < 0) {
+        rc = TCCL_NODES;
+        return true;
+    }
+    TileRec* TR = a.tiles + f * a.ntiles + ti;
+    if (ln == 63) {
+        TR->nroots = nroots;
+        TR->nbase = nb;
+    }
+    if (FM_OOB(a, (long long)nb + nroots <= (long long)a.nnodes, 3)) {
+        rc = TCCL_NODES;
+        return true;
+    }
+    NodeRec* NR = a.nodes + nb;
+    if (live && rt == ln) {
+        const int o = ordof(ln);
+        NodeRec nrec;
+        nrec.parent = nb + o;
+        nrec.key = 0;
+        nrec.minx = nrec.maxx = nrec.maxy = nrec.pad = 0;
+        if (fg) {
+            uint32_t ref;
+            if (x0 + xs == 0) ref = REF_OUTER;
+            else if (xs == 0) ref = REF_EDGE | (uint32_t)r;
+            else ref = (uint32_t)ordof(lload(&par[ln - 1]));  // the background run left of it (same row: k > 0)
+            nrec.key = ((uint64_t)(uint32_t)(gy * w + x0 + xs) << 32) | ref;
+            nrec.flags = 1u;
+            nrec.minx = x0 + amin[ln];
+            nrec.maxx = x0 + amax[ln];
+            nrec.maxy = y0 + ay[ln];
+        } else {
+            nrec.flags = amin[ln] ? 2u : 0u;
+        }
+        NR[o] = nrec;
+    }
+    // ---- lane = row again: edge labels (component ordinal | fg << 15)
+    const uint64_t mask_c = (2ull << ln) - 1;
+    const uint64_t s0 = lane_at64(starts, 0), m0 = lane_at64(m, 0);
+    const uint64_t s63 = lane_at64(starts, 63), m63 = lane_at64(m, 63);
+    const int id0 = __popcll(s0 & mask_c) - 1;
+    const int id63 = lane_at(bs, 63) + __popcll(s63 & mask_c) - 1;
+    TR->edges[ln] = (uint16_t)(ordof(lload(&par[bs])) | (int)((m & 1ull) << 15));
+    TR->edges[64 + ln] = (uint16_t)(ordof(lload(&par[bs + nrr - 1])) | (int)((m >> 63) << 15));
+    TR->edges[128 + ln] = (uint16_t)(ordof(lload(&par[id0])) | (int)(((m0 >> ln) & 1ull) << 15));
+    TR->edges[192 + ln] = (uint16_t)(ordof(lload(&par[id63])) | (int)(((m63 >> ln) & 1ull) << 15));
+    rc = TCCL_OK;
+    return true;
+}
+
 // TCCL_RUNS (nothing written) if the tile has more than CAP runs
 template <int CAP>
 __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m, const Scratch& sc) {
@@ -518,7 +688,18 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
     const int x0 = (ti % a.ntx) * TS, y0 = (ti / a.ntx) * TS;
     TileRec* TR = a.tiles + f * a.ntiles + ti;
 
-    if (__ballot(m != 0) == 0) {  // empty tile: one background component
+    bool empty = __ballot(m != 0) == 0;
+#ifdef FM_DEV_SWITCHES
+    // profiling-only ablations (results invalid): 512 = every tile that is not full takes the empty-tile
+    // record; 256 = every tile that is neither full nor simple does
+    if ((a.dbg_skip & 512) && __ballot(m != ~0ull) != 0) empty = true;
+    if ((a.dbg_skip & 256) && !empty && __ballot(m != ~0ull) != 0) {
+        int rc = TCCL_OK;
+        if (simple_tile(a, f, ti, ln, m, rc)) return rc;
+        empty = true;
+    }
+#endif
+    if (empty) {  // empty tile: one background component
         const int nb = take_nodes(a, f, 1, ln);
         if (nb < 0) return TCCL_NODES;
         TR->edges[ln] = 0;
@@ -568,6 +749,7 @@ __device__ int tile_ccl(const FusedArgs& a, size_t f, int ti, int ln, uint64_t m
        // non-empty tiles; the driver's command 405.9 -> 416.6 k frames/s, 3 alternating rounds, round 5)
         int rc = TCCL_OK;
         if (simple_tile(a, f, ti, ln, m, rc)) return rc;
+        if (compact_tile(a, f, ti, ln, m, sc, rc)) return rc;
     }
     const uint64_t starts = (m ^ (m << 1)) | 1ull;  // run starts (bit 0 always)
     const int nr = __popcll(starts);

@@ -283,6 +283,35 @@ def test_simple_tiles_vs_oracle(W, H, seed):
     run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
 
 
+def _streak_rows(H, W, rng, maxruns, maxlen=23):
+    """Streaks of identical rows (1..maxlen rows each, 0..maxruns random runs per row, some past the image edges):
+    after the dilation most tiles hold several runs per row, holes and separate components, but few distinct
+    rows -- the contour pass's compact tiles (one lane per run of the distinct rows); the busiest exceed 64
+    such runs and take the row-per-lane labelling."""
+    p = np.zeros((H, W), bool)
+    y = 0
+    while y < H:
+        n = int(rng.integers(1, maxlen + 1))
+        row = np.zeros(W, bool)
+        for _ in range(int(rng.integers(0, maxruns + 1))):
+            x, ln = int(rng.integers(-10, W)), int(rng.integers(1, 80))
+            row[max(x, 0):max(x + ln, 0)] = True
+        p[y:y + n] = row
+        y += n
+    return p
+
+
+@pytest.mark.parametrize("W,H,seed", [(200, 150, 11), (330, 260, 12), (330, 260, 13), (128, 64, 14), (700, 300, 15)])
+def test_compact_tiles_vs_oracle(W, H, seed):
+    """Tiles with few distinct rows (streaks of repeated rows with several runs each: holes, nested and side-by-side
+    components, background regions split by them, rows cut by the image's right / bottom edge), on both contour
+    pass layouts, against the oracle; the denser patterns exceed 64 runs and cover the fallback labelling too."""
+    rng = np.random.default_rng(seed)
+    pats = [_streak_rows(H, W, rng, r) for r in (1, 2, 3, 4, 6, 8)] + [_streak_rows(H, W, rng, 6, maxlen=2)]
+    frames = _pattern_frames(pats)
+    run_pair(W, H, W, ksize=1, T=frames.shape[0], n_batches=1, thresh=100, alpha=0.5, frames=[frames])
+
+
 @pytest.mark.parametrize("k", [1, 5])
 @pytest.mark.parametrize("W,H", [(320, 256), (300, 204)])
 def test_full_tiles(W, H, k):
