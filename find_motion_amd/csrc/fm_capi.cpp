@@ -654,7 +654,8 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
         c->nty = (c->h + 63) / 64;
         c->ntiles = c->ntx * c->nty;
         c->frame_ccl = c->ntiles <= kFrameCclTiles;
-        if (const char* e = dev_env("FM_FRAME_CCL")) c->frame_ccl = c->frame_ccl && std::atoi(e) != 0;
+        // (dev: 0 = never, 2 = at any size)
+        if (const char* e = dev_env("FM_FRAME_CCL")) c->frame_ccl = std::atoi(e) == 2 || (c->frame_ccl && std::atoi(e) != 0);
         // union-find nodes: one per empty-tile region slot, each frame's quota, and a shared
         // overflow pool that holds at least one worst-case frame (frames past it take the
         // pixel-level fallback)

@@ -1510,8 +1510,9 @@ constexpr size_t FR_SCRATCH = FW * TC_WAVE_LDS > HEAVY_LDS ? FW * TC_WAVE_LDS : 
 __device__ __forceinline__ void step_barrier() { __syncthreads(); }
 template <bool DILATE>
 __global__ __launch_bounds__(64 * FW) void k_frame_contours(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int fr_lds[];  // FR_SCRATCH
-    __shared__ int uf[kFrameCclTiles], hl[kFrameCclTiles];
+    extern __shared__ __attribute__((aligned(16))) int fr_lds[];  // FR_SCRATCH, then uf and hl: a.ntiles ints each
+    int* uf = fr_lds + FR_SCRATCH / 4;
+    int* hl = uf + a.ntiles;
     __shared__ int s_nc, s_nr, s_nh, s_ovf;
     const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
     const size_t f = blockIdx.x;
@@ -1593,10 +1594,12 @@ hipError_t launch_contour_area(hipStream_t st, const uint64_t* dbits, const uint
 }
 
 hipError_t launch_frame_contours(hipStream_t st, const FusedArgs& a, bool dilate) {
-    if (a.ntiles > kFrameCclTiles) return hipErrorInvalidValue;
+    if (a.ntiles > cc::MAX_REGION_TILES) return hipErrorInvalidValue;
     const unsigned F = (unsigned)(a.T * a.S);
-    if (dilate) hipLaunchKernelGGL(cc::k_frame_contours<true>, dim3(F), dim3(64 * cc::FW), cc::FR_SCRATCH, st, a);
-    else hipLaunchKernelGGL(cc::k_frame_contours<false>, dim3(F), dim3(64 * cc::FW), cc::FR_SCRATCH, st, a);
+    const size_t lds = cc::FR_SCRATCH + 2 * sizeof(int) * (size_t)a.ntiles;
+    if (lds > 65536) return hipErrorInvalidValue;
+    if (dilate) hipLaunchKernelGGL(cc::k_frame_contours<true>, dim3(F), dim3(64 * cc::FW), lds, st, a);
+    else hipLaunchKernelGGL(cc::k_frame_contours<false>, dim3(F), dim3(64 * cc::FW), lds, st, a);
     return hipGetLastError();
 }
 
