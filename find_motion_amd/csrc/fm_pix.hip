@@ -869,6 +869,12 @@ struct P5Raw {
 // workgroup sharing the frame barrier, issue priority falling with progress, chain and producer waves
 // (DESIGN.md §3.1c); round 5: a wave-private variant without the frame barrier (k_pixq, each wave's own
 // gray and taps over its 12 rows: 345-357 vs 383-418 k frames/s) -- small images now take fm_small.hip.
+#ifndef FM_P5_SDWA
+#define FM_P5_SDWA 0
+#endif
+#ifndef FM_P5_PERMPACK
+#define FM_P5_PERMPACK 0
+#endif
 template <bool KEEP, bool TAIL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
     using G = P5G;
@@ -877,7 +883,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
+#if FM_P5_SDWA
+    __shared__ double atab_s[256];  // blur x alpha (f64), static LDS at address 0 (the SDWA table offset)
+    double* atab = atab_s;
+#else
     double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);  // blur x alpha (f64)
+#endif
     const int tid = (int)threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1014,8 +1025,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             const uint32_t k1 = hs_tap<KC, 1>(qw, hcs);
             const uint32_t k2 = hs_tap<KC, 2>(qw, hcs);
             const uint32_t k3 = hs_tap<KC, 3>(qw, hcs);
+#if FM_P5_PERMPACK
+            // (each sum < 2^16: one v_perm per pair instead of a shift and an or)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
+                make_uint4(__builtin_amdgcn_perm(k0, h0, 0x05040100u), __builtin_amdgcn_perm(k1, h1, 0x05040100u),
+                           __builtin_amdgcn_perm(k2, h2, 0x05040100u), __builtin_amdgcn_perm(k3, h3, 0x05040100u));
+#else
             *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
                 make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
+#endif
         }
     };
     const int t0 = a.t_begin, t1 = a.t_end;
@@ -1049,9 +1067,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
             const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
             if (!TAIL || var == 0)
-                chain_rows_w<KC, KEEP, false, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, false, FM_P5_SDWA>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             else
-                chain_rows_w<KC, KEEP, true, false>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, true, FM_P5_SDWA>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
             // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
             // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
