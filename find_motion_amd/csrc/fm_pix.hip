@@ -243,7 +243,8 @@ __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) 
 // v_lshl_add_u32 (the dynamic LDS array's base is a link-time symbol the compiler adds to every index).
 // Measured (round 4, 3 alternating rounds of the driver's command and 2 of config 5): both in k_pixw
 // gain 1.9 % (80.9 vs 79.5 k frames/s, 3.07-3.12 vs 3.16-3.17 ms per launch); both in k_pix5 cost 3.4 %
-// (396.0 vs 410.1 k frames/s), which keeps global loads and the dynamic table.
+// (396.0 vs 410.1 k frames/s), which keeps global loads.  (Round 5: the static table and SDWA offset alone in
+// k_pix5, with its tap jobs' row pairs packed by v_perm: 430.3 vs 417.5 k, 4 alternating rounds; kept.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* p, uint32_t bytes) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
@@ -852,7 +853,7 @@ struct P5G {
     static constexpr int GBUF = NG + 64;                 // + a pad slot per lane for the idle jobs' stores (branch-free)
     static constexpr int HBUF = (GH + 2) * TS;           // u16; + the pad pair row idle tap jobs store to
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
-    static constexpr int dyn_bytes = bytes;
+    static constexpr int dyn_bytes = bytes - 256 * 8;  // (the table is static LDS)
 };
 static_assert(P5G::GSLOW >= 0 && 4 * (P5G::GFAST + P5G::GSLOW) >= P5G::GSLOTS, "gray slots");
 
@@ -869,12 +870,6 @@ struct P5Raw {
 // workgroup sharing the frame barrier, issue priority falling with progress, chain and producer waves
 // (DESIGN.md §3.1c); round 5: a wave-private variant without the frame barrier (k_pixq, each wave's own
 // gray and taps over its 12 rows: 345-357 vs 383-418 k frames/s) -- small images now take fm_small.hip.
-#ifndef FM_P5_SDWA
-#define FM_P5_SDWA 0
-#endif
-#ifndef FM_P5_PERMPACK
-#define FM_P5_PERMPACK 0
-#endif
 template <bool KEEP, bool TAIL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
     using G = P5G;
@@ -883,12 +878,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     constexpr int KC = 5, R = 2;
     uint32_t* gray = reinterpret_cast<uint32_t*>(smem);                          // [2][G::GBUF]
     uint16_t* Hs = reinterpret_cast<uint16_t*>(smem + 2 * G::GBUF * 4);          // [2][G::HBUF]
-#if FM_P5_SDWA
-    __shared__ double atab_s[256];  // blur x alpha (f64), static LDS at address 0 (the SDWA table offset)
+    // blur x alpha (f64) as static LDS at address 0: the chain's table offset is ONE SDWA shift of the
+    // accumulator (byte 2 times 8) instead of v_bfe_u32 + v_lshl_add_u32 with the dynamic array's base
+    __shared__ double atab_s[256];
     double* atab = atab_s;
-#else
-    double* atab = reinterpret_cast<double*>(smem + 2 * G::GBUF * 4 + 2 * G::HBUF * 2);  // blur x alpha (f64)
-#endif
     const int tid = (int)threadIdx.x, ln = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
@@ -1025,15 +1018,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             const uint32_t k1 = hs_tap<KC, 1>(qw, hcs);
             const uint32_t k2 = hs_tap<KC, 2>(qw, hcs);
             const uint32_t k3 = hs_tap<KC, 3>(qw, hcs);
-#if FM_P5_PERMPACK
-            // (each sum < 2^16: one v_perm per pair instead of a shift and an or)
+            // row pairs by one v_perm each (every sum < 2^16) instead of a shift and an or
             *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
                 make_uint4(__builtin_amdgcn_perm(k0, h0, 0x05040100u), __builtin_amdgcn_perm(k1, h1, 0x05040100u),
                            __builtin_amdgcn_perm(k2, h2, 0x05040100u), __builtin_amdgcn_perm(k3, h3, 0x05040100u));
-#else
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(Hb) + hdst[i]) =
-                make_uint4(h0 | (k0 << 16), h1 | (k1 << 16), h2 | (k2 << 16), h3 | (k3 << 16));
-#endif
         }
     };
     const int t0 = a.t_begin, t1 = a.t_end;
@@ -1053,9 +1041,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
-    {
-        for (int t = t0; t < t1; t++) {
-            const int b = (t - t0) & 1;
+    auto frame = [&](int t, int b) __attribute__((always_inline)) {
             const size_t f = (size_t)t * S + s;
             lds_barrier();
             uint32_t colbits = 0, fl = 0;
@@ -1064,12 +1050,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             int x0f = __builtin_amdgcn_readfirstlane(x0), y0f = __builtin_amdgcn_readfirstlane(y0), wvf = wv, var = var0;
             asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
             var = __builtin_amdgcn_readfirstlane(var);
-            asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+            if constexpr (KEEP) asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
             const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
             if (!TAIL || var == 0)
-                chain_rows_w<KC, KEEP, false, FM_P5_SDWA>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, false, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             else
-                chain_rows_w<KC, KEEP, true, FM_P5_SDWA>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, true, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
             // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
             // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
@@ -1082,8 +1068,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
             // unconditional (see load): past the batch's last frame it re-reads that frame
             load((size_t)min(t + 3, t1 - 1) * S + s);
-        }
-    }
+    };
+    for (int t = t0; t < t1; t++) frame(t, (t - t0) & 1);
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
