@@ -244,7 +244,8 @@ __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) 
 // Measured (round 4, 3 alternating rounds of the driver's command and 2 of config 5): both in k_pixw
 // gain 1.9 % (80.9 vs 79.5 k frames/s, 3.07-3.12 vs 3.16-3.17 ms per launch); both in k_pix5 cost 3.4 %
 // (396.0 vs 410.1 k frames/s), which keeps global loads.  (Round 5: the static table and SDWA offset alone in
-// k_pix5, with its tap jobs' row pairs packed by v_perm: 430.3 vs 417.5 k, 4 alternating rounds; kept.)
+// k_pix5, with its tap jobs' row pairs packed by v_perm: 430.3 vs 417.5 k, 4 alternating rounds; kept.  The
+// buffer loads alone in k_pix5: 400-406 vs 414-428 k, 4 rounds; not kept.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* p, uint32_t bytes) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(p));
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uintptr_t>(p) >> 32));
