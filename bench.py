@@ -379,7 +379,8 @@ def face_painter(W: int, H: int):
 
 
 def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local: int, active: bool, backend: str,
-            haar: bool = False, masks: bool = False, ring_frames: int | None = None) -> dict:
+            haar: bool = False, masks: bool = False, ring_frames: int | None = None, shape: tuple | None = None,
+            blur_scale: int | None = None, ring_period: int | None = None) -> dict:
     """One workload: S streams per GPU of synthetic frames in a device-resident ring, `warmup` untimed then
     `steps` timed steps (one step = one batch of T frames per stream submitted and one completed), the
     barrier + synchronize on both sides, max over ranks.  Returns the line's figures and the live engine."""
@@ -387,25 +388,27 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
 
     from find_motion_amd import MotionEngine, dist, make_gaussian, work_height
     world = pl.world
-    W, H = args.width, args.height
-    box, blur_scale = (W, W // 5) if mode == "F" else (100, 20)
+    W, H = (args.width, args.height) if shape is None else shape
+    box, bscale = (W, W // 5) if mode == "F" else (100, 20)
     if mode == "F" and W == 1920:
-        blur_scale = 384
-    if args.blur_scale is not None:
+        bscale = 384
+    if blur_scale is None and args.blur_scale is not None and shape is None:
         blur_scale = args.blur_scale
+    blur_scale = bscale if blur_scale is None else blur_scale
     k = make_gaussian(box, blur_scale)
     ring_frames = args.ring if ring_frames is None else ring_frames
+    ring_period = args.ring_period if ring_period is None else ring_period
     R = max(ring_frames - ring_frames % T, T)
     cfg = {"workload": f"{config_name(S, W, H, mode, k, haar, world)}: {S}x{W}x{H} stream(s) per GPU, mode {mode} "
                        f"(-B {box} -b {blur_scale}, k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
-                       + (f" cycling {args.ring_period} synthetic frames" if args.ring_period < R else ""),
+                       + (f" cycling {ring_period} synthetic frames" if ring_period < R else ""),
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
            "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
 
     # synthetic ring [R][S][H][W][3] on the device, distinct streams per rank (stream s -> rank s // S):
     # ring slot t holds synthetic frame t % P; only the P distinct frames exist on the host (at 8 streams a
     # host copy of the whole ring would be 12.7 GB per rank)
-    P = max(1, min(args.ring_period, R))
+    P = max(1, min(ring_period, R))
     paint = face_painter(W, H) if haar else None
     host, ring = synthetic_ring(W, H, S, R, P, dist.rank_streams(pl, S), local, paint)
     frame_bytes = S * H * W * 3
@@ -510,9 +513,13 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
     if det is not None:
         det.close()
 
-    ktimes = eng.kernel_times()
-    kstd = eng.kernel_time_std()  # stamped launches: the spread of the launch time over the timed steps
-    kbusy = eng.kernel_time_busy()  # the union of each kernel's launch windows
+    kst = eng.kernel_time_stats()  # one fold of the launch stamps: sums, spreads and busy time over the same launches
+    unstamped = kst.pop("_unstamped")
+    ktimes = {k: (v["ms"], v["launches"]) for k, v in kst.items()}
+    # stamped launches: the spread of the launch time over the timed steps
+    kstd = {k: max(v["ms_sq"] / v["stamped"] - (v["stamped_ms"] / v["stamped"]) ** 2, 0.0) ** 0.5
+            for k, v in kst.items() if v["stamped"] > 0 and v["ms_sq"] > 0}
+    kbusy = {k: v["busy_ms"] for k, v in kst.items()}  # the union of each kernel's launch windows
     total_frames = world * S * T * steps
     ms_per_step = 1e3 * elapsed / steps
     kernels = {name: {"avg_us": round(1e3 * ms / max(n, 1), 3), "launches": int(n), "total_ms": round(ms, 3),
@@ -520,26 +527,43 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
                       **({"busy_ms": round(kbusy[name], 3)} if kbusy.get(name) and kbusy[name] < ms * (1 - 1e-3) else {})}
                for name, (ms, n) in ktimes.items()}
     del ring
-    return {"cfg": cfg, "eng": eng, "host": host, "P": P, "wall": wall, "elapsed": elapsed,
+    return {"cfg": cfg, "eng": eng, "host": host, "P": P, "wall": wall, "elapsed": elapsed, "unstamped": int(unstamped),
             "value": total_frames / elapsed, "ms_per_step": ms_per_step,
             "roofline": roofline_of(ktimes, cfg, ms_per_step, kstd, kbusy), "kernels": kernels, "haar": hs, "det": det,
             "footprint": footprint, "ccl": ccl,
             "host_us_per_step": {k: round(1e6 * v / steps, 1) for k, v in hostt.items()}}
 
 
-def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, backend: str) -> dict:
+def haar_summary(hs: dict, wall: float) -> dict:
+    return {"cascade": "haarcascade_frontalface_default (reference XML as tests/golden fixture arrays)",
+            "rule": "every 15th written frame per stream (find_objects skip=15, fm.py:549-575, 703-731)",
+            "calls": hs["calls"], "roi_frames": hs["roi_frames"], "detections": hs["detections"],
+            "wall_ms": round(1e3 * hs["wall_s"], 3), "device_ms": round(hs["device_ms"], 3),
+            "share_of_step_time": round(hs["wall_s"] / wall, 4),
+            "overlap": "each batch's detection queued on the detector's stream, collected after the next "
+                       "batch is waited (host time in the loop: wall_ms)",
+            "frames": "synthetic frames with a cartoon frontal face drawn in (tests/haar_cases.py draw_faces)"}
+
+
+def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, backend: str, steps: int = 60,
+             warmup: int | None = None, **kw) -> dict:
     """A compact figure of another configuration for the same JSON line (mode D, the reference CLI's
-    default -B 100; configs[2], 8 streams per GPU): value, step time, its own roofline."""
-    # 60 timed steps whatever the headline's K: a step's batch is submitted and completed inside the timed
-    # region, so the pipeline's fill and drain (the last batch's pixel stage and contour pass after its resize,
-    # ~0.3 ms in mode D) is a fixed cost that 20 steps of ~0.32 ms amortise ~3x less than 60 do
-    steps, warmup = 60, max(2, min(args.warmup, 5))
-    leg = run_leg(args, mode, S, T, steps, warmup, pl, local, active, backend)
+    default -B 100; configs[2], 8 streams per GPU; configs[4], 4 x 4K with k 21, masks and the Haar stage):
+    value, step time, its own roofline."""
+    # mode D / configs[2]: 60 timed steps whatever the headline's K: a step's batch is submitted and completed
+    # inside the timed region, so the pipeline's fill and drain (the last batch's pixel stage and contour pass
+    # after its resize, ~0.3 ms in mode D) is a fixed cost that 20 steps of ~0.32 ms amortise ~3x less than 60 do
+    warmup = max(2, min(args.warmup, 5)) if warmup is None else warmup
+    leg = run_leg(args, mode, S, T, steps, warmup, pl, local, active, backend, **kw)
     leg["eng"].close()
     out = {"workload": leg["cfg"]["workload"], "value": round(leg["value"], 2), "unit": "frames/s",
            "steps": steps, "warmup": warmup, "ms_per_step": round(leg["ms_per_step"], 4), "roofline": leg["roofline"],
            "kernels": leg["kernels"], "host_us_per_step": leg["host_us_per_step"], "path_hbm_frac": round(leg["value"] / pl.world * path_bytes_per_frame(leg["cfg"])
                                                             / 1e9 / HBM_PEAK_GBS, 4)}
+    if leg["det"] is not None:
+        out["haar_stage"] = haar_summary(leg["haar"], leg["wall"])
+    if "masks" in leg["cfg"]:
+        out["masks"] = leg["cfg"]["masks"]
     del leg
     import torch
     torch.cuda.empty_cache()
@@ -732,6 +756,12 @@ def main() -> None:
     if world == 1 and default_shape and not args.no_side:
         side = {"mode_d": side_leg(args, "D", 1, args.batch, pl, local, active, backend),
                 "configs2": side_leg(args, "F", 8, 128, pl, local, active, backend)}
+        # configs[4]: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the polygon masks, 64 frames per stream per step
+        # from a 64-frame ring cycling 16 synthetic frames; with the frontalface cascade on every 15th written frame
+        # (faces drawn in), and the same geometry without the Haar stage
+        c4 = dict(shape=(3840, 2160), blur_scale=183, ring_frames=64, ring_period=16, steps=20, warmup=10)
+        side["configs4"] = side_leg(args, "F", 4, 64, pl, local, active, backend, haar=True, **c4)
+        side["configs4_no_haar"] = side_leg(args, "F", 4, 64, pl, local, active, backend, masks=True, **c4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -743,18 +773,12 @@ def main() -> None:
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8+f64",
                "data": "synthetic (find_motion_amd/synthetic.py, SURVEY.md §8d)", "config": cfg,
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "side_configs": side,
+               # launches that found the stamp ring full between two folds (timed by events on one in four, or not)
+               "unstamped_launches": leg["unstamped"],
                "ranks": {"world_size_seen": dist.world_size(active), "devices": ranks}, "host_fed_per_gpu": host_fed,
                "mjpeg_fed_per_gpu": mjpeg, "footprint_per_gpu": footprint,
                "hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-               "haar_stage": None if det is None else {
-                   "cascade": "haarcascade_frontalface_default (reference XML as tests/golden fixture arrays)",
-                   "rule": "every 15th written frame per stream (find_objects skip=15, fm.py:549-575, 703-731)",
-                   "calls": haar["calls"], "roi_frames": haar["roi_frames"], "detections": haar["detections"],
-                   "wall_ms": round(1e3 * haar["wall_s"], 3), "device_ms": round(haar["device_ms"], 3),
-                   "share_of_step_time": round(haar["wall_s"] / wall, 4),
-                   "overlap": "each batch's detection queued on the detector's stream, collected after the next "
-                              "batch is waited (host time in the loop: wall_ms)",
-                   "frames": "synthetic frames with a cartoon frontal face drawn in (tests/haar_cases.py draw_faces)"},
+               "haar_stage": None if det is None else haar_summary(haar, wall),
                "path_hbm": {"bytes_per_frame": path_bytes_per_frame(cfg),
                             "achieved": round(value / world * path_bytes_per_frame(cfg) / 1e9, 1), "unit": "GB/s",
                             "frac": round(value / world * path_bytes_per_frame(cfg) / 1e9 / HBM_PEAK_GBS, 4),

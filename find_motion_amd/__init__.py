@@ -18,8 +18,9 @@ def use_hw_queues(n: int = 8, force: bool = False) -> int:
     frames/s, the device-resident figure unchanged).  It changes the queue setup of every
     HIP user in the process (torch included) and takes effect only before the process's first HIP call, so
     it is never set on import: the CLI and bench.py call this first thing.  A value already in the
-    environment wins unless `force` (the CLI forces: machines commonly export HIP's default, 4, and with 4
-    the input stream shares an in-order queue with a contour stream -- mode D 498 k vs 591 k frames/s).
+    environment wins unless `force` (the CLI forces only when FM_HW_QUEUES is set, cli.hw_queues_from_env; an
+    exported GPU_MAX_HW_QUEUES is otherwise kept -- with HIP's 4 the input stream shares an in-order queue with a
+    contour stream: mode D 498 k vs 591 k frames/s).
     Returns the value in effect."""
     if force:
         _os.environ["GPU_MAX_HW_QUEUES"] = str(int(n))

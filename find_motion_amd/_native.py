@@ -25,7 +25,7 @@ EXPORTED = (
     "fm_abi_version", "fm_create", "fm_destroy", "fm_last_error", "fm_work_size", "fm_set_mask",
     "fm_reset_stream", "fm_submit", "fm_wait", "fm_get_counts", "fm_get_contours", "fm_read_mask",
     "fm_read_plane", "fm_read_background", "fm_write_background", "fm_set_hip_stream",
-    "fm_kernel_times", "fm_kernel_time_spread", "fm_kernel_time_busy", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
+    "fm_kernel_times", "fm_kernel_time_spread", "fm_kernel_time_busy", "fm_kernel_time_stats", "fm_reset_kernel_times", "fm_rasterize_masks", "fm_max_inflight",
     "fm_host_alloc", "fm_host_free", "fm_last_fallbacks", "fm_last_ccl_stats",
     "fm_haar_create", "fm_haar_destroy", "fm_haar_last_error", "fm_haar_window", "fm_haar_detect",
     "fm_haar_candidates", "fm_haar_last_ms", "fm_haar_detect_frames",
@@ -104,6 +104,7 @@ def load() -> C.CDLL:
     L.fm_host_free.argtypes = [vp, vp]
     L.fm_kernel_time_spread.argtypes = [vp, vp, i32]
     L.fm_kernel_time_busy.argtypes = [vp, vp, i32]
+    L.fm_kernel_time_stats.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
     L.fm_reset_kernel_times.argtypes = [vp]
     L.fm_rasterize_masks.argtypes = [i32, i32, C.c_double, vp, vp, i32, vp]
     L.fm_max_inflight.argtypes = [vp]
@@ -416,31 +417,38 @@ class MotionEngine:
         self._check(self._L.fm_read_plane(self._h, which, frame, stream, _ptr(out)))
         return out
 
+    def kernel_time_stats(self) -> dict:
+        """{kernel: {ms, launches, stamped, ms_sq, busy_ms}} plus {"_unstamped": n}, from ONE fold of the launch
+        stamps (fm_kernel_time_stats), so every figure covers the same launches."""
+        N = 32
+        names = (C.c_char_p * N)()
+        ms, sms, sq, busy = (C.c_double * N)(), (C.c_double * N)(), (C.c_double * N)(), (C.c_double * N)()
+        nl, ns = (C.c_int64 * N)(), (C.c_int64 * N)()
+        un = C.c_int64(0)
+        v = [C.cast(x, C.c_void_p) for x in (names, ms, nl, sms, ns, sq, busy)]
+        n = self._check(self._L.fm_kernel_time_stats(self._h, *v, C.byref(un), N))
+        out = {names[i].decode(): {"ms": ms[i], "launches": nl[i], "stamped_ms": sms[i], "stamped": ns[i],
+                                   "ms_sq": sq[i], "busy_ms": busy[i]} for i in range(min(n, N))}
+        out["_unstamped"] = int(un.value)
+        return out
+
     def kernel_times(self) -> dict:
-        names = (C.c_char_p * 32)()
-        ms = (C.c_double * 32)()
-        n_l = (C.c_int64 * 32)()
-        n = self._check(self._L.fm_kernel_times(self._h, C.cast(names, C.c_void_p), C.cast(ms, C.c_void_p),
-                                                C.cast(n_l, C.c_void_p), 32))
-        return {names[i].decode(): (ms[i], n_l[i]) for i in range(min(n, 32))}
+        """{kernel: (ms, launches)} since the last reset."""
+        return {k: (v["ms"], v["launches"]) for k, v in self.kernel_time_stats().items() if k != "_unstamped"}
 
     def kernel_time_busy(self) -> dict:
-        """{kernel: ms during which at least one of its stamped launches ran} (fm_kernel_time_busy)."""
-        names = list(self.kernel_times())
-        b = (C.c_double * 32)()
-        n = self._check(self._L.fm_kernel_time_busy(self._h, C.cast(b, C.c_void_p), 32))
-        return {names[i]: b[i] for i in range(min(n, 32, len(names)))}
+        """{kernel: ms during which at least one of its stamped launches ran}."""
+        return {k: v["busy_ms"] for k, v in self.kernel_time_stats().items() if k != "_unstamped"}
 
     def kernel_time_std(self) -> dict:
-        """{kernel: standard deviation of its launch time in ms} over the stamped launches (the pixel kernel and
-        the resize); fm_kernel_time_spread's sums of squares with fm_kernel_times' sums and counts."""
-        t = self.kernel_times()
-        sq = (C.c_double * 32)()
-        n = self._check(self._L.fm_kernel_time_spread(self._h, C.cast(sq, C.c_void_p), 32))
+        """{kernel: standard deviation of its launch time in ms} over its stamped launches only (the pixel kernel
+        and the resize; event-timed launches add to ms but not to ms_sq, so they are left out of both)."""
         out = {}
-        for i, (name, (ms, cnt)) in enumerate(list(t.items())[:min(n, 32)]):
-            if cnt > 0 and sq[i] > 0:
-                out[name] = max(sq[i] / cnt - (ms / cnt) ** 2, 0.0) ** 0.5
+        for name, v in self.kernel_time_stats().items():
+            if name == "_unstamped" or v["stamped"] < 1 or v["ms_sq"] <= 0:
+                continue
+            cnt = v["stamped"]
+            out[name] = max(v["ms_sq"] / cnt - (v["stamped_ms"] / cnt) ** 2, 0.0) ** 0.5
         return out
 
     def reset_kernel_times(self) -> None:

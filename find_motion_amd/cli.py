@@ -292,16 +292,23 @@ def hw_queues_from_env(env=None) -> tuple:
     and forced over any GPU_MAX_HW_QUEUES; otherwise an exported GPU_MAX_HW_QUEUES is honoured and 8 is
     the default (with HIP's 4 the input stream shares an in-order queue with a contour stream)."""
     env = os.environ if env is None else env
+
+    def checked(name: str, v: str) -> int:
+        try:
+            n = int(v)
+        except ValueError:
+            raise SystemExit(f"{name}={v!r}: expected an integer in 1..32") from None
+        if not 1 <= n <= 32:
+            raise SystemExit(f"{name}={n}: expected an integer in 1..32")
+        return n
+
     v = env.get("FM_HW_QUEUES")
     if v is None:
+        # an exported GPU_MAX_HW_QUEUES is kept (use_hw_queues does not force), but only a value HIP accepts
+        if env.get("GPU_MAX_HW_QUEUES") is not None:
+            checked("GPU_MAX_HW_QUEUES", env["GPU_MAX_HW_QUEUES"])
         return 8, False
-    try:
-        n = int(v)
-    except ValueError:
-        raise SystemExit(f"FM_HW_QUEUES={v!r}: expected an integer in 1..32") from None
-    if not 1 <= n <= 32:
-        raise SystemExit(f"FM_HW_QUEUES={n}: expected an integer in 1..32")
-    return n, True
+    return checked("FM_HW_QUEUES", v), True
 
 
 def main(argv=None) -> None:

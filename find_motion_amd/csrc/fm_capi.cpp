@@ -411,6 +411,8 @@ int KernelTimer::id_of(const char* name) {
     names.push_back(name);
     ms.push_back(0);
     ms_sq.push_back(0);
+    stamped.push_back(0);
+    stamped_ms.push_back(0);
     busy.push_back(Busy{});
     launches.push_back(0);
     calls.push_back(0);
@@ -488,6 +490,7 @@ int KernelTimer::fold_stamps() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (stream2) (void)hipStreamSynchronize(stream2);
     if (stream3) (void)hipStreamSynchronize(stream3);
+    for (hipStream_t st : extra) (void)hipStreamSynchronize(st);  // (an entry read while its kernel runs is lost)
     const size_t n = stamp_ids.size();
     std::vector<uint64_t> v(2 * n);
     if (hipMemcpy(v.data(), d_stamps, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -499,6 +502,8 @@ int KernelTimer::fold_stamps() {
         const double t = (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
         ms[stamp_ids[i]] += t;
         ms_sq[stamp_ids[i]] += t * t;
+        stamped[stamp_ids[i]] += 1;
+        stamped_ms[stamp_ids[i]] += t;
         launches[stamp_ids[i]] += 1;
     }
     // the union of each kernel's launch windows (launches of one kernel may overlap: two input streams)
@@ -526,6 +531,8 @@ void KernelTimer::reset() {
     fold_stamps();  // (launches stamped before the reset are dropped with the sums below)
     std::fill(ms.begin(), ms.end(), 0.0);
     std::fill(ms_sq.begin(), ms_sq.end(), 0.0);
+    std::fill(stamped.begin(), stamped.end(), 0);
+    std::fill(stamped_ms.begin(), stamped_ms.end(), 0.0);
     std::fill(busy.begin(), busy.end(), Busy{});
     std::fill(launches.begin(), launches.end(), 0);
     std::fill(calls.begin(), calls.end(), 0);
@@ -716,6 +723,7 @@ int fm_create(fm_ctx** out, const fm_params* prm) {
             }
         }
         b.ccl_stream = c->ccl_streams[i % c->nccl];
+        if (i < c->nccl) c->timer.extra.push_back(b.ccl_stream);  // fold_stamps waits for it too
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_pix, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_done, hipEventDisableTiming));
         HIP_TRY(cp, hipEventCreateWithFlags(&b.ev_rs, hipEventDisableTiming));
@@ -1041,7 +1049,10 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
                 if (c->use_small) {
                     uint64_t* k1 = c->timer.stamp(init ? "small_blur_init" : "small_blur");
                     uint64_t* k2 = c->timer.stamp(init ? "small_scan_init" : "small_scan");
+                    // not stamping (FM_FLAG_PROFILE, or the stamp ring full): the pair timed by events
+                    int tok = (k1 && k2) ? -1 : c->timer.begin(init ? "small_init" : "small", ps);
                     HIP_TRY(c, launch_small(ps, fp, B.d_sblur, k1, k2));
+                    c->timer.end(tok);
                 } else {
                     fp.kstamp = c->timer.stamp(name);
                     int tok = fp.kstamp ? -1 : c->timer.begin(name, ps);
@@ -1079,6 +1090,8 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
 #ifdef FM_DEV_SWITCHES
             fc.kstamp = c->timer.stamp("frame_contours");
 #endif
+            // FM_FLAG_PROFILE: events around it (a contour stream: never in the pixel-only mode)
+            const int tok_fc = fc.kstamp ? -1 : c->timer.begin("frame_contours", cs);
             // the slot-wide words (shared pool, heavy tally, frames done) sit at indices that depend on the batch's
             // frame count; the last workgroup re-arms them for a batch of the same size, so a slot whose batch size
             // changed (a stream's last, partial batch) zeroes them at the new indices first
@@ -1088,6 +1101,7 @@ static int submit_impl(fm_ctx* c, const uint8_t* frames, int n, int on_device, f
                 B.ccl_F = F;
             }
             HIP_TRY(c, launch_frame_contours(cs, fc, c->use_pix));
+            c->timer.end(tok_fc);
         } else {
             hipEvent_t gate_wait = nullptr;
             if (!c->serial && c->lab_prev >= 0 && c->lab_prev != si) gate_wait = c->slots[c->lab_prev].ev_lab;
@@ -1432,6 +1446,26 @@ int fm_kernel_time_busy(fm_ctx* c, double* busy_ms, int cap) {
         const auto& b = c->timer.busy[i];
         busy_ms[i] = b.ms + (b.open ? (double)(b.e - b.s) * 1e-5 : 0.0);
     }
+    return n;
+}
+
+int fm_kernel_time_stats(fm_ctx* c, const char** names, double* ms, int64_t* launches, double* stamped_ms,
+                         int64_t* stamped, double* ms_sq, double* busy_ms, int64_t* unstamped, int cap) {
+    if (!c) return fail(nullptr, FM_EINVAL, "null context");
+    HIP_TRY(c, hipSetDevice(c->p.device));
+    if (c->timer.fold_stamps() != 0) return fail(c, FM_EHIP, "reading the launch stamps failed");
+    const auto& T = c->timer;
+    const int n = (int)T.names.size();
+    for (int i = 0; i < std::min(n, cap); i++) {
+        if (names) names[i] = T.names[i];
+        if (ms) ms[i] = T.ms[i];
+        if (launches) launches[i] = T.launches[i];
+        if (ms_sq) ms_sq[i] = T.ms_sq[i];
+        if (stamped) stamped[i] = T.stamped[i];
+        if (stamped_ms) stamped_ms[i] = T.stamped_ms[i];
+        if (busy_ms) busy_ms[i] = T.busy[i].ms + (T.busy[i].open ? (double)(T.busy[i].e - T.busy[i].s) * 1e-5 : 0.0);
+    }
+    if (unstamped) *unstamped = T.unstamped;
     return n;
 }
 

@@ -139,10 +139,11 @@ struct FusedArgs {
     int32_t* regrep;             // [F][ntiles] empty tile -> its region's representative tile
     int32_t* ncr;                // [F][2] candidates, regions
     NodeRec* nodes;              // [nnodes]: F*ntiles region nodes, then the pool of candidate-tile nodes
-    int32_t* count;              // [3F+2]: [f] external contours, [F+f] overflow flag, [2F] shared node-pool
-                                 // fill, [2F+1] heavy tiles listed, [2F+2+f] frame f's node-quota fill
+    int32_t* count;              // [3F+3]: [f] external contours, [F+f] overflow flag, [2F] shared node-pool
+                                 // fill, [2F+1] heavy tiles listed, [2F+2+f] frame f's node-quota fill, [3F+2]
+                                 // frames done (k_frame_contours; its last workgroup re-arms [2F], [2F+1], [3F+2])
     int32_t* h_stats;            // mapped host [2]: nodes taken from the shared pool, heavy tiles (written by
-                                 // k_counts; diagnostics)
+                                 // k_counts, or by the last k_frame_contours workgroup; diagnostics)
     int32_t* heavy;              // [F * ntiles] tiles with more runs than the light CCL pass holds
     int32_t* rec;                // [F][cap][5]
     int32_t* h_count;            // mapped host [F]: external contours per frame (written by k_fold_emit)
@@ -242,6 +243,7 @@ struct KernelTimer {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // also timed in the pixel-only mode: the input stream's resize
     hipStream_t stream3 = nullptr;  // (the second input stream)
+    std::vector<hipStream_t> extra; // other streams stamped kernels run on (the contour streams; dev-build stamps)
     struct Rec { int id; hipEvent_t a, b; hipStream_t st; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
@@ -249,6 +251,8 @@ struct KernelTimer {
     std::vector<double> ms;
     std::vector<int64_t> launches;
     std::vector<double> ms_sq;      // sum of squared stamped launch times (ms^2)
+    std::vector<int64_t> stamped;   // launches timed by stamps (ms_sq's count; `launches` adds event-timed ones)
+    std::vector<double> stamped_ms; // their summed time (ms)
     struct Busy { double ms = 0; uint64_t s = 0, e = 0; bool open = false; };
     std::vector<Busy> busy;         // union of the stamped launch windows (closed part + the open interval)
     uint64_t* d_stamps = nullptr;   // device [kStampRing][2]: (first start, last end), ticks of 10 ns

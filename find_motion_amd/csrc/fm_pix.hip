@@ -267,6 +267,7 @@ struct ChainCtx {
     uint64_t colmask;   // lanes whose column is inside the image
     uint32_t rowvalid;  // bit j: tile row 8*wv + j is inside the image
     uint32_t keep_lo, keep_hi;  // keep-mask bytes of the wave's 8 rows for this lane's column (1 = keep)
+    uint32_t keep_2, keep_3;    // rows 8..15 of a 16-row wave (k_pix5<.., 4>)
     bool hk;            // stream has a keep-mask
     uint32_t vec;       // every pixel of the wave's rows lies in accumulateWeighted's vector body
     uint32_t tbmask;    // this lane's column inside the image ? rowvalid : 0
@@ -649,15 +650,17 @@ template <int K> constexpr int tap_hi() {
     return i;
 }
 
-// One 64 x 64 tile per workgroup of 8 waves, each over 8 rows.  (A 64-wide, 128-row band of 16 waves, its
-// 2R-row vertical halo read once per 128 rows: 3.61 vs 3.33 ms per config-5 launch, round 4.)
-template <int KC>
+// One 64-wide band of 8 waves per workgroup, each wave over RW rows: RW = 8, a 64 x 64 tile; RW = 16, a
+// 64 x 128 band (two contour tiles), its 2R-row vertical halo loaded and filtered once per 128 rows.  (A
+// 64 x 128 band of 16 waves of 8 rows: 3.61 vs 3.33 ms per config-5 launch, round 4.)
+template <int KC, int RW_ = RPWV>
 struct PW {
     static constexpr int NWB = 8;
+    static constexpr int RW = RW_;                 // rows per wave
     static constexpr int R = KC / 2;
     static constexpr int PC = 4 * ((R + 3) / 4);   // gray columns each side of the tile (quad aligned)
     static constexpr int NTB = 64 * NWB;           // threads
-    static constexpr int TH = RPWV * NWB;          // rows
+    static constexpr int TH = RW * NWB;            // rows
     static constexpr int GH = TH + 2 * R;          // gray rows (even)
     static constexpr int GQ = (TS + 2 * PC) / 4;   // gray quads per row
     static constexpr int NG = GH * GQ;             // gray jobs per frame
@@ -680,7 +683,7 @@ struct PW {
     static constexpr int np(int j) { return (j + HI + 2 - 2 * p0(j)) / 2; }
     static constexpr int np_max() {
         int m = 0;
-        for (int j = 0; j < RPWV; j++) m = p0(j) + np(j) > m ? p0(j) + np(j) : m;
+        for (int j = 0; j < RW; j++) m = p0(j) + np(j) > m ? p0(j) + np(j) : m;
         return m;
     }
     static constexpr int NP = np_max();            // pairs a wave's chain reads
@@ -705,21 +708,32 @@ template <int KC> constexpr uint32_t tapv2(int j, int i) {  // chain pair i of o
 // side the row parity needs, so no pair is rebuilt with v_alignbit
 // wv: the wave within its workgroup = its 8-row slice of the 64-row tile (flag rows: FLAG_T* from slice 0,
 // FLAG_B* from slice 7)
-template <int KC, bool KEEP, bool TAIL, bool SDWA>
-__device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RPWV],
+// pairs the chain of a RW-row wave reads
+template <int KC, int RW> constexpr int np_rows() {
+    int m = 0;
+    for (int j = 0; j < RW; j++) m = PW<KC>::p0(j) + PW<KC>::np(j) > m ? PW<KC>::p0(j) + PW<KC>::np(j) : m;
+    return m;
+}
+
+// RW: rows per wave (8, or 16 for k_pix5's 4-wave tiles and k_pixw's 128-row bands), NWT: waves per 64-row
+// contour tile, BAND: waves of the workgroup (wv counts the band's waves; wv % NWT is the tile's slice)
+template <int KC, bool KEEP, bool TAIL, bool SDWA, int RW = RPWV, int NWT = NW, int BAND = NWT>
+__device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t* Hp, const double* atab, double (&bg)[RW],
                                              int wv, int ln, int x0, int y0, const ChainCtx& cc, uint32_t& colbits,
                                              uint32_t& flags) {
     using G = PW<KC>;
-    uint32_t P[G::NP];
-    const uint32_t* col = Hp + (RPWV / 2 * wv) * TS + ln;
+    static_assert(RW * NWT == TS && (RW == 8 || RW == 16), "rows per wave");
+    constexpr int NPR = np_rows<KC, RW>();
+    uint32_t P[NPR];
+    const uint32_t* col = Hp + (RW / 2 * wv) * TS + ln;
 #pragma unroll
-    for (int i = 0; i < G::NP; i++) P[i] = col[i * TS];
+    for (int i = 0; i < NPR; i++) P[i] = col[i * TS];
     const int w = a.w;
     const double beta = a.beta;
     const int thr = min(max(a.thresh, -1), 255);
     const uint32_t bias = (uint32_t)(255 - thr);
-    uint32_t tb = 0;
-    static_for<RPWV>([&](auto jc) {
+    uint32_t tb = 0, tb2 = 0;  // rows 0..7 / 8..15 (one dot4 moves a row's bit into byte 1 of the word)
+    static_for<RW>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         uint32_t acc = 32768u;
         static_for<G::np(j)>([&](auto ic) {
@@ -727,7 +741,10 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
             acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, P[G::p0(j) + i]),
                                          __builtin_bit_cast(u16x2_t, tapv2<KC>(j, i)), acc, false);
         });
-        if (KEEP) acc &= (uint32_t)__builtin_amdgcn_sbfe(j < 4 ? (int)cc.keep_lo : (int)cc.keep_hi, 8 * (j & 3), 8);
+        if (KEEP) {
+            const uint32_t kw = j < 4 ? cc.keep_lo : j < 8 ? cc.keep_hi : j < 12 ? cc.keep_2 : cc.keep_3;
+            acc &= (uint32_t)__builtin_amdgcn_sbfe((int)kw, 8 * (j & 3), 8);
+        }
         // SDWA: the blur byte (byte 2: acc < 2^24) times 8, the table's byte offset, in ONE instruction
         // (the table must then be static LDS at address 0); else the blur value indexes the table
         uint32_t boff = 0, blur = 0;
@@ -739,25 +756,28 @@ __device__ __forceinline__ void chain_rows_w(const FusedArgs& a, const uint32_t*
         const double b = bg[j];
         const uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(fabsf(__double2float_rn(b)), 2, acc);
         const uint32_t r = __builtin_amdgcn_sad_u8(acc, q, bias);
-        tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
+        if constexpr (j < 8) tb = __builtin_amdgcn_udot4(r, (1u << j) << 8, tb, false);
+        else tb2 = __builtin_amdgcn_udot4(r, (1u << (j - 8)) << 8, tb2, false);
         const double bl = SDWA ? *reinterpret_cast<const double*>(reinterpret_cast<const char*>(atab) + boff)
                                : atab[blur];
         double nb = bg_fma(b, beta, bl);
         if (TAIL) {
-            const long long li = (long long)(y0 + RPWV * wv + j) * w + x0 + ln;
+            const long long li = (long long)(y0 + RW * wv + j) * w + x0 + ln;
             if (li >= a.acc_vec_end) nb = __dadd_rn(bl, __dmul_rn(b, beta));
         }
         bg[j] = nb;
     });
+    if constexpr (RW > 8) tb |= tb2 << 8;
     tb &= cc.tbmask;
     colbits = tb;
+    const int ws = BAND == NWT ? wv : wv % NWT;  // the wave's slice of its contour tile
     const uint64_t orr = __builtin_amdgcn_ballot_w64(tb != 0);
-    const uint64_t top = wv == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
-    const uint64_t bot = wv == NW - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RPWV - 2))) != 0) : 0ull;
+    const uint64_t top = ws == 0 ? __builtin_amdgcn_ballot_w64((tb & 3u) != 0) : 0ull;
+    const uint64_t bot = ws == NWT - 1 ? __builtin_amdgcn_ballot_w64((tb & (3u << (RW - 2))) != 0) : 0ull;
     uint32_t fl = 0;
     if (orr) fl = FLAG_ANY | ((orr & 3ull) ? FLAG_L : 0u) | ((orr >> 62) ? FLAG_R : 0u);
-    if (wv == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
-    if (wv == NW - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
+    if (ws == 0 && top) fl |= FLAG_T | ((top & 3ull) ? FLAG_TL : 0u) | ((top >> 62) ? FLAG_TR : 0u);
+    if (ws == NWT - 1 && bot) fl |= FLAG_B | ((bot & 3ull) ? FLAG_BL : 0u) | ((bot >> 62) ? FLAG_BR : 0u);
     flags = fl;
 }
 
@@ -832,20 +852,22 @@ __device__ __forceinline__ uint32_t hs_tap(const uint32_t (&q)[N], const uint32_
 // The chain runs on even-aligned pair windows (chain_rows_w); tap jobs cover 2 H rows x 4 columns and store
 // them as row pairs (one ds_write_b128), which the chain reads back as six dwords instead of twelve u16
 // reads and their merges; the horizontal taps take shifted constants (HS).
+template <int NWB_ = 8>
 struct P5G {
-    static constexpr int NWB = 8;                        // waves of a tile
+    static constexpr int NWB = NWB_;                     // waves of a tile (8 of 8 rows, or 4 of 16 rows)
+    static constexpr int RW = TS / NWB;                  // rows per wave
     static constexpr int NTB = 64 * NWB;                 // threads
-    static constexpr int TH = RPWV * NWB;                // tile rows
+    static constexpr int TH = RW * NWB;                  // tile rows
     static constexpr int GH = TH + 4;                    // gray rows y0-2 .. y0+TH+1
     static constexpr int GQ = 18;                        // gray quads per row: columns x0-4 .. x0+67
     static constexpr int NG = GH * GQ;                   // gray jobs per frame
     // Gray jobs go to waves in whole wave-slots of 64 jobs.  Waves 4..7 lose issue arbitration to waves
     // 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves 0..3 spent ~30 % of
     // their cycles in the barrier), so waves 0..3 take GFAST slots each and waves 4..7 the rest; the
-    // partial last slot goes to wave 3.  (GFAST A/B: 4 >= 3 > 5.)
+    // partial last slot goes to wave 3.  (GFAST A/B: 4 >= 3 > 5.)  Four waves: an even deal.
     static constexpr int GSLOTS = (NG + 63) / 64;
-    static constexpr int GFAST = 4;
-    static constexpr int GSLOW = (GSLOTS - 4 * GFAST + 3) / 4;
+    static constexpr int GFAST = NWB == 8 ? 4 : (GSLOTS + NWB - 1) / NWB;
+    static constexpr int GSLOW = NWB == 8 ? (GSLOTS - 4 * GFAST + 3) / 4 : 0;
     static constexpr int GJ = GFAST > GSLOW ? GFAST : GSLOW;  // load rounds per wave
     static constexpr int NH = (GH / 2) * (TS / 4);       // tap jobs per frame
     static constexpr int HJ = (NH + NTB - 1) / NTB;
@@ -856,7 +878,8 @@ struct P5G {
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
     static constexpr int dyn_bytes = bytes - 256 * 8;  // (the table is static LDS)
 };
-static_assert(P5G::GSLOW >= 0 && 4 * (P5G::GFAST + P5G::GSLOW) >= P5G::GSLOTS, "gray slots");
+static_assert(P5G<8>::GSLOW >= 0 && 4 * (P5G<8>::GFAST + P5G<8>::GSLOW) >= P5G<8>::GSLOTS, "gray slots");
+static_assert(4 * P5G<4>::GFAST >= P5G<4>::GSLOTS, "gray slots");
 
 template <int GJ>
 struct P5Raw {
@@ -871,9 +894,10 @@ struct P5Raw {
 // workgroup sharing the frame barrier, issue priority falling with progress, chain and producer waves
 // (DESIGN.md §3.1c); round 5: a wave-private variant without the frame barrier (k_pixq, each wave's own
 // gray and taps over its 12 rows: 345-357 vs 383-418 k frames/s) -- small images now take fm_small.hip.
-template <bool KEEP, bool TAIL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
-    using G = P5G;
+template <bool KEEP, bool TAIL, int NWB = 8>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pix5(FusedArgs a) {
+    using G = P5G<NWB>;
+    constexpr int RW = G::RW;
     constexpr int GJX = G::GJ, HJX = G::HJ;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int KC = 5, R = 2;
@@ -912,10 +936,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     uint32_t goff[GJX];   // byte offset of the job's quad in a frame (0 for jobs that load nothing)
     uint32_t gdst[GJX];   // its gray dword in a buffer (the lane's pad slot for idle jobs)
     // this wave's gray slots (wave-uniform): the 4 / 4 deal
-    const int gjobs = wv < 4 ? G::GFAST : G::GSLOW;
+    const int gjobs = NWB == 8 ? (wv < 4 ? G::GFAST : G::GSLOW) : min(G::GFAST, G::GSLOTS - wv * G::GFAST);
 #pragma unroll
     for (int i = 0; i < GJX; i++) {
-        const int slot = wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i;
+        const int slot = NWB != 8 ? wv * G::GFAST + i : wv >= 4 ? (wv - 4) * G::GSLOW + i : 4 * G::GSLOW + wv * G::GFAST + i;
         const int j = i < gjobs ? slot * 64 + ln : G::NG;  // rounds past the wave's slots: idle (dummy load)
         const int gr = j / G::GQ, gq = j - gr * G::GQ;
         const int x = x0 - 4 + 4 * gq;
@@ -946,32 +970,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     }
 
     // background of the wave's 8 rows x 64 columns -> registers (as k_pix)
-    double bg[RPWV];
+    double bg[RW];
     ChainCtx cc;
     {
         const double* bgi = a.bg_in + (size_t)s * plane;
         const int x = x0 + ln;
         cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
         cc.rowvalid = 0;
-        cc.keep_lo = cc.keep_hi = 0;
+        cc.keep_lo = cc.keep_hi = cc.keep_2 = cc.keep_3 = 0;
         cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;
 #pragma unroll
-        for (int j = 0; j < RPWV; j++) {
-            const int y = y0 + RPWV * wv + j;
+        for (int j = 0; j < RW; j++) {
+            const int y = y0 + RW * wv + j;
             const bool in = x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
             if (j < 4) cc.keep_lo |= kb << (8 * j);
-            else cc.keep_hi |= kb << (8 * (j - 4));
+            else if (j < 8) cc.keep_hi |= kb << (8 * (j - 4));
+            else if (j < 12) cc.keep_2 |= kb << (8 * (j - 8));
+            else cc.keep_3 |= kb << (8 * (j - 12));
         }
-        const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
+        const long long last = (long long)(y0 + RW * wv + RW - 1) * w + x0 + TS - 1;
         cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
         cc.tbmask = x < w ? cc.rowvalid : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
+    for (int j = 0; j < RW; j++) asm volatile("" : "+v"(bg[j]));
     asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
+    if constexpr (RW > 8) asm volatile("" : "+v"(cc.keep_2), "+v"(cc.keep_3));
 
     uint32_t hcs[HS<KC>::NC];
     hs_consts<KC>(hcs);
@@ -1052,11 +1079,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
             var = __builtin_amdgcn_readfirstlane(var);
             if constexpr (KEEP) asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+            if constexpr (KEEP && RW > 8) asm volatile("" : "+v"(ccf.keep_2), "+v"(ccf.keep_3));
             const uint32_t* Hp = reinterpret_cast<const uint32_t*>(Hs + b * G::HBUF);
             if (!TAIL || var == 0)
-                chain_rows_w<KC, KEEP, false, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, false, true, RW, NWB>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             else
-                chain_rows_w<KC, KEEP, true, true>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+                chain_rows_w<KC, KEEP, true, true, RW, NWB>(a, Hp, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
             if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
             // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
             // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
@@ -1065,8 +1093,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
             // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
             // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
             // the prefetch would be waited for with it
-            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            if constexpr (RW == 8) {
+                reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+                if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+            } else {  // bytes 2wv, 2wv + 1 of the column word; flag words 2wv (this wave's) and 2wv + 1 (none)
+                reinterpret_cast<uint16_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 4 + wv] = (uint16_t)colbits;
+                if (ln == 0) *reinterpret_cast<uint2*>(a.tflag + (f * a.ntiles + ti) * NW + 2 * wv) = make_uint2(fl, 0u);
+            }
             // unconditional (see load): past the batch's last frame it re-reads that frame
             load((size_t)min(t + 3, t1 - 1) * S + s);
     };
@@ -1075,8 +1108,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
 #pragma unroll
-    for (int j = 0; j < RPWV; j++) {
-        const int y = y0 + RPWV * wv + j;
+    for (int j = 0; j < RW; j++) {
+        const int y = y0 + RW * wv + j;
         if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
     kstamp_end(a.kstamp);
@@ -1107,9 +1140,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
 // Rows: reflect101 source rows, as k_pix5.  Needs w % 4 == 0 and w >= 2 * PC + 8.
 // 2 workgroups per CU (<= 128 VGPRs).  (8 chain + 4 producer waves per tile, as k_pix5's SPL: 57.8 vs
 // 79.0 k frames/s at config 5, round 4.)
-template <int KC, bool KEEP, bool TAIL>
+template <int KC, bool KEEP, bool TAIL, int RW = RPWV>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pixw(FusedArgs a) {
-    using G = PW<KC>;
+    using G = PW<KC, RW>;
+    constexpr int TPB = RW / RPWV;  // contour tiles per band (stacked vertically)
     constexpr int GJX = G::GJ, HJX = G::HJ;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int R = G::R, PC = G::PC, GQ = G::GQ;
@@ -1121,10 +1155,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int s = blockIdx.y;
     const int h = a.h, w = a.w, S = a.S;
-    const int ti = swizzle_tile(blockIdx.x, a.ntiles);  // contour tile
-    const int tx = ti % a.ntx;
-    const int y0 = (ti / a.ntx) * TS;
+    // the band (TPB == 1: the contour tile); this wave's contour tile (TPB == 2: the upper one for waves 0..3),
+    // past the grid in a last half band
+    const int bi = swizzle_tile(blockIdx.x, TPB == 1 ? a.ntiles : a.ntx * ((a.nty + TPB - 1) / TPB));
+    const int tx = bi % a.ntx;
+    const int y0 = (bi / a.ntx) * G::TH;
     const int x0 = tx * TS;
+    const int tyw = (bi / a.ntx) * TPB + (TPB == 1 ? 0 : (wv >> 2));
+    const bool tile_ok = TPB == 1 || tyw < a.nty;
+    const int ti = TPB == 1 ? bi : tyw * a.ntx + tx;
     const size_t plane = (size_t)h * w;
     const size_t fbytes = plane * 3;
     const bool hk = a.has_keep[s] != 0;
@@ -1160,32 +1199,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
     }
     const bool edge_tile = x0 - PC < 0 || x0 + TS + PC > w;  // workgroup-uniform
 
-    double bg[RPWV];
+    double bg[RW];
     ChainCtx cc;
     {
         const double* bgi = a.bg_in + (size_t)s * plane;
         const int x = x0 + ln;
         cc.colmask = __builtin_amdgcn_ballot_w64(x < w);
         cc.rowvalid = 0;
-        cc.keep_lo = cc.keep_hi = 0;
+        cc.keep_lo = cc.keep_hi = cc.keep_2 = cc.keep_3 = 0;
         cc.hk = __builtin_amdgcn_readfirstlane(hk ? 1 : 0) != 0;
 #pragma unroll
-        for (int j = 0; j < RPWV; j++) {
-            const int y = y0 + RPWV * wv + j;
+        for (int j = 0; j < RW; j++) {
+            const int y = y0 + RW * wv + j;
             const bool in = x < w && y < h;
             if (y < h) cc.rowvalid |= 1u << j;
             bg[j] = in ? bgi[(size_t)y * w + x] : 0.0;
             const uint32_t kb = (!hk || (in && keep[(size_t)y * w + x] != 0)) ? 0xFFu : 0u;
             if (j < 4) cc.keep_lo |= kb << (8 * j);
-            else cc.keep_hi |= kb << (8 * (j - 4));
+            else if (j < 8) cc.keep_hi |= kb << (8 * (j - 4));
+            else if (j < 12) cc.keep_2 |= kb << (8 * (j - 8));
+            else cc.keep_3 |= kb << (8 * (j - 12));
         }
-        const long long last = (long long)(y0 + RPWV * wv + RPWV - 1) * w + x0 + TS - 1;
+        const long long last = (long long)(y0 + RW * wv + RW - 1) * w + x0 + TS - 1;
         cc.vec = (uint32_t)__builtin_amdgcn_readfirstlane(last < a.acc_vec_end ? 1 : 0);
         cc.tbmask = x < w ? cc.rowvalid : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < RPWV; j++) asm volatile("" : "+v"(bg[j]));
+    for (int j = 0; j < RW; j++) asm volatile("" : "+v"(bg[j]));
     asm volatile("" : "+v"(cc.keep_lo), "+v"(cc.keep_hi));
+    if constexpr (RW > 8) asm volatile("" : "+v"(cc.keep_2), "+v"(cc.keep_3));
 
     uint32_t cpk[G::NGR];
 #pragma unroll
@@ -1263,22 +1305,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) 
         asm volatile("" : "+s"(ccf.colmask), "+s"(ccf.rowvalid), "+s"(x0f), "+s"(y0f), "+s"(wvf));
         var = __builtin_amdgcn_readfirstlane(var);
         asm volatile("" : "+v"(ccf.keep_lo), "+v"(ccf.keep_hi));
+        if constexpr (RW > 8) asm volatile("" : "+v"(ccf.keep_2), "+v"(ccf.keep_3));
         const uint32_t* Hb = Hs + b * G::HBUF;
+        constexpr int NWT = TS / RW;  // waves per contour tile
         if (!TAIL || var == 0)
-            chain_rows_w<KC, KEEP, false, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            chain_rows_w<KC, KEEP, false, true, RW, NWT, 8>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
         else
-            chain_rows_w<KC, KEEP, true, true>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
+            chain_rows_w<KC, KEEP, true, true, RW, NWT, 8>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
         if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         gray_stage(gray + b * G::GBUF);
-        reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
-        if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        if constexpr (RW == 8) {
+            reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
+            if (ln == 0) a.tflag[(f * a.ntiles + ti) * NW + wv] = fl;
+        } else if (tile_ok) {  // bytes 2 (wv & 3), +1 of the column word; flag words 2 (wv & 3) and the next (none)
+            const int ws = wv & 3;
+            reinterpret_cast<uint16_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 4 + ws] = (uint16_t)colbits;
+            if (ln == 0) *reinterpret_cast<uint2*>(a.tflag + (f * a.ntiles + ti) * NW + 2 * ws) = make_uint2(fl, 0u);
+        }
         load((size_t)min(t + 3, t1 - 1) * S + s);
     }
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
 #pragma unroll
-    for (int j = 0; j < RPWV; j++) {
-        const int y = y0 + RPWV * wv + j;
+    for (int j = 0; j < RW; j++) {
+        const int y = y0 + RW * wv + j;
         if (x < w && y < h) bgo[(size_t)y * w + x] = bg[j];
     }
     kstamp_end(a.kstamp);
@@ -1303,25 +1353,35 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
                   : a.ksize == 21 ? taps_match<21>(a) : false;
     if (!ok) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
+#ifndef FM_P5_NWB
+#define FM_P5_NWB 8
+#endif
     if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
-        px::P5G::bytes <= 64 * 1024) {
+        px::P5G<FM_P5_NWB>::bytes <= 64 * 1024) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        const size_t lds = px::P5G::dyn_bytes;
-        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true>), grid, dim3(512), lds, st, a);
-        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false>), grid, dim3(512), lds, st, a);
-        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true>), grid, dim3(512), lds, st, a);
-        else hipLaunchKernelGGL((px::k_pix5<false, false>), grid, dim3(512), lds, st, a);
+        constexpr int NWB = FM_P5_NWB;
+        const size_t lds = px::P5G<NWB>::dyn_bytes;
+        const dim3 blk(64 * NWB);
+        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, NWB>), grid, blk, lds, st, a);
+        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, NWB>), grid, blk, lds, st, a);
+        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, NWB>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((px::k_pix5<false, false, NWB>), grid, blk, lds, st, a);
         return hipGetLastError();
     }
     // k = 21 steady state (config 5) on k_pixw
     if (a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 && ((uintptr_t)a.src & 3) == 0) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        using G = px::PW<21>;
-        static_assert(G::bytes <= 160 * 1024, "k_pixw LDS");
+#ifndef FM_PIXW_RW
+#define FM_PIXW_RW 8
+#endif
+        constexpr int RW = FM_PIXW_RW;
+        using G = px::PW<21, RW>;
+        static_assert(2 * G::bytes <= 160 * 1024, "k_pixw LDS: two workgroups per CU");
+        const dim3 gridw(a.ntx * ((a.nty + RW / 8 - 1) / (RW / 8)), a.S);
 #define FM_PIXW_LAUNCH(K, T)                                                                                            \
     do {                                                                                                                \
-        (void)hipFuncSetAttribute((const void*)px::k_pixw<21, K, T>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-        hipLaunchKernelGGL((px::k_pixw<21, K, T>), grid, dim3(512), G::dyn_bytes, st, a);                                \
+        (void)hipFuncSetAttribute((const void*)px::k_pixw<21, K, T, RW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
+        hipLaunchKernelGGL((px::k_pixw<21, K, T, RW>), gridw, dim3(512), G::dyn_bytes, st, a);                           \
     } while (0)
         if (keep && tail) FM_PIXW_LAUNCH(true, true);
         else if (keep) FM_PIXW_LAUNCH(true, false);

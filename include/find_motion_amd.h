@@ -186,6 +186,13 @@ int fm_kernel_time_spread(fm_ctx* ctx, double* ms_sq, int cap);
  * stamped launches was running (the union of their windows; less than the summed launch times when launches
  * of one kernel overlap, e.g. the resizes of consecutive batches on the two input streams). */
 int fm_kernel_time_busy(fm_ctx* ctx, double* busy_ms, int cap);
+/* Everything above from ONE fold of the launch stamps (so the sums, the squares and the counts cover the same
+ * launches): per kernel ms and launches (stamped + event-timed), stamped_ms / stamped / ms_sq (the stamped
+ * launches alone: their sum, count and sum of squares, for the spread), busy_ms; *unstamped = launches that
+ * found the stamp ring full between two folds (event-timed on one launch in four, or untimed).  Any array may
+ * be NULL. */
+int fm_kernel_time_stats(fm_ctx* ctx, const char** names, double* ms, int64_t* launches, double* stamped_ms,
+                         int64_t* stamped, double* ms_sq, double* busy_ms, int64_t* unstamped, int cap);
 int fm_reset_kernel_times(fm_ctx* ctx);
 
 /* Rasterise mask polygons to a keep-mask (mask_off_areas, fm.py:611-636):

@@ -91,6 +91,15 @@ def bgr2gray(bgr: np.ndarray) -> np.ndarray:
     return ((b * 1868 + g * 9617 + r * 4899 + 8192) >> 14).astype(np.uint8)
 
 
+def fma(a: float, b: float, c: float) -> float:
+    """a * b + c rounded once, as C's fma (fm_oracle.c, OpenCV's mulAdd): math.fma where Python has it (3.13+),
+    else the exact rational result rounded to the nearest double (float(Fraction) rounds correctly)."""
+    if hasattr(math, "fma"):
+        return math.fma(a, b, c)
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
 def gauss_coeffs(k: int) -> np.ndarray:
     tables = {
         1: [1.0],
@@ -102,7 +111,7 @@ def gauss_coeffs(k: int) -> np.ndarray:
     if k in tables:
         kd = tables[k]
     else:
-        sigma = math.fma(k, 0.15, 0.35) if hasattr(math, "fma") else k * 0.15 + 0.35
+        sigma = fma(k, 0.15, 0.35)
         s2 = -0.125 / (sigma * sigma)
         n2 = (k - 1) // 2
         vals = [math.exp(float(x * x) * s2) for x in range(1 - k, 1 - k + 2 * n2, 2)]

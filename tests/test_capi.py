@@ -166,3 +166,6 @@ def test_cli_hw_queues_honours_env_and_validates():
     for bad in ("abc", "0", "33", "-1"):
         with pytest.raises(SystemExit, match="FM_HW_QUEUES"):
             hw_queues_from_env({"FM_HW_QUEUES": bad})
+        # an exported GPU_MAX_HW_QUEUES is kept only when HIP would accept it
+        with pytest.raises(SystemExit, match="GPU_MAX_HW_QUEUES"):
+            hw_queues_from_env({"GPU_MAX_HW_QUEUES": bad})

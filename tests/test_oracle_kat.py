@@ -66,6 +66,20 @@ def test_gauss_taps_all_odd_sizes_sum_256_symmetric_and_match_numpy():
         assert c.tolist() == onp.gauss_coeffs(k).tolist(), k
 
 
+def test_gauss_sigma_is_one_rounding_as_the_c_oracle():
+    """oracle_np's sigma = fma(k, 0.15, 0.35) with one rounding (fm_oracle.c:198 uses C's fma): without
+    math.fma (Python < 3.13) it is the exact product-sum rounded once, never k*0.15 + 0.35's two roundings;
+    and both restatements give the same taps for every odd k <= 199 (verdict r05)."""
+    from fractions import Fraction
+    for k in range(1, 200, 2):
+        exact = Fraction(k) * Fraction(0.15) + Fraction(0.35)
+        s = onp.fma(k, 0.15, 0.35)
+        # the nearest double: no double lies strictly between s and the exact value on the other side
+        assert abs(Fraction(s) - exact) <= abs(Fraction(np.nextafter(s, np.inf)) - exact), k
+        assert abs(Fraction(s) - exact) <= abs(Fraction(np.nextafter(s, -np.inf)) - exact), k
+        assert oracle.gauss_coeffs(k).tolist() == onp.gauss_coeffs(k).tolist(), k
+
+
 def _gauss_taps_variant(k, exp_ulps, sigma_ulps=0, reciprocal=False):
     """getGaussianKernelBitExact + the 8-bit error-diffusion rounding (smooth.dispatch.cpp), with
     every exp() result moved by exp_ulps[i] ulps, sigma by sigma_ulps, and the normalisation by a
