@@ -159,6 +159,10 @@ def cpu_baseline(cfg: dict, frames_host: np.ndarray, n_frames: int) -> dict:
     single = n_frames / (time.perf_counter() - t0)
     return {"value": round(threads * n_frames / dt, 2), "unit": "frames/s", "cores": used, "kind": "port",
             "single_stream_1_core": round(single, 2),
+            # SURVEY §8d asks for P = the affinity; on the GPU box the affinity lists the whole machine's CPUs while
+            # one GPU's share of them is OMP_NUM_THREADS (16), the largest worker pool the box allows per GPU
+            "cores_rule": (f"P = min(affinity {aff}, OMP_NUM_THREADS {cap}): the host CPUs one GPU's job may use"
+                           if cap < aff else f"P = affinity ({aff})"),
             "sample": f"{threads} workers x 1 stream x {n_frames} frames {cfg['W']}x{cfg['H']} box {cfg['box']} "
                       f"k {cfg['ksize']}, median of 5 runs after 10 warm-up frames ({aff} CPUs in affinity, "
                       f"OMP_NUM_THREADS cap {cap}); CPU restatement of the OpenCV chain, not OpenCV "

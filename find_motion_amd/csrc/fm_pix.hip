@@ -1353,40 +1353,62 @@ hipError_t launch_pix(hipStream_t st, const FusedArgs& a, bool planes, bool init
                   : a.ksize == 21 ? taps_match<21>(a) : false;
     if (!ok) return hipErrorInvalidValue;
     dim3 grid(a.ntiles, a.S);
-#ifndef FM_P5_NWB
-#define FM_P5_NWB 8
+    // k = 5 steady state on k_pix5: 8 waves of 8 rows per 64 x 64 tile, or 4 waves of 16 rows once the grid
+    // holds >= FM_P5_W4_MIN tile-streams (four 4-wave workgroups per CU still give 4 waves per SIMD, and each wave
+    // has twice the independent rows per frame barrier).  Measured (round 6, tools/ab_bench.sh, 2 alternating
+    // rounds): configs[2] (8 x 1080p, 4,080 tiles) 486 k vs 476 k frames/s, launch std 57-64 vs 50 us; configs[1]
+    // (510 tiles, two 4-wave workgroups per CU = 2 waves per SIMD) 365 k vs 418 k over 4 rounds: not there.
+#ifndef FM_P5_W4_MIN
+#define FM_P5_W4_MIN 1024
 #endif
-    if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0 &&
-        px::P5G<FM_P5_NWB>::bytes <= 64 * 1024) {
+    if (a.ksize == 5 && !planes && !init && (a.w & 3) == 0 && a.w >= 8 && ((uintptr_t)a.src & 3) == 0) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-        constexpr int NWB = FM_P5_NWB;
-        const size_t lds = px::P5G<NWB>::dyn_bytes;
-        const dim3 blk(64 * NWB);
-        if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, NWB>), grid, blk, lds, st, a);
-        else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, NWB>), grid, blk, lds, st, a);
-        else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, NWB>), grid, blk, lds, st, a);
-        else hipLaunchKernelGGL((px::k_pix5<false, false, NWB>), grid, blk, lds, st, a);
+        static_assert(px::P5G<8>::bytes <= 64 * 1024 && px::P5G<4>::bytes <= 64 * 1024, "k_pix5 LDS");
+        if ((long long)a.ntiles * a.S >= FM_P5_W4_MIN) {
+            const size_t lds = px::P5G<4>::dyn_bytes;
+            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, 4>), grid, dim3(256), lds, st, a);
+            else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, 4>), grid, dim3(256), lds, st, a);
+            else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, 4>), grid, dim3(256), lds, st, a);
+            else hipLaunchKernelGGL((px::k_pix5<false, false, 4>), grid, dim3(256), lds, st, a);
+        } else {
+            const size_t lds = px::P5G<8>::dyn_bytes;
+            if (keep && tail) hipLaunchKernelGGL((px::k_pix5<true, true, 8>), grid, dim3(512), lds, st, a);
+            else if (keep) hipLaunchKernelGGL((px::k_pix5<true, false, 8>), grid, dim3(512), lds, st, a);
+            else if (tail) hipLaunchKernelGGL((px::k_pix5<false, true, 8>), grid, dim3(512), lds, st, a);
+            else hipLaunchKernelGGL((px::k_pix5<false, false, 8>), grid, dim3(512), lds, st, a);
+        }
         return hipGetLastError();
     }
-    // k = 21 steady state (config 5) on k_pixw
+    // k = 21 steady state (config 5) on k_pixw: 64 x 128 bands of 8 waves of 16 rows once the grid holds
+    // >= FM_PIXW_BAND_MIN bands (two workgroups per CU), else 64 x 64 tiles of 8 waves of 8 rows.  Measured (round
+    // 6, 3 alternating rounds of configs[4]'s geometry): 3.03-3.11 vs 3.13-3.17 ms per launch, 81.4-83.5 k vs
+    // 79.7-80.9 k frames/s; with the Haar stage 66.3 k vs 63.4 k.
+#ifndef FM_PIXW_BAND_MIN
+#define FM_PIXW_BAND_MIN 512
+#endif
     if (a.ksize == 21 && !planes && !init && (a.w & 3) == 0 && a.w >= 2 * px::PW<21>::PC + 8 && ((uintptr_t)a.src & 3) == 0) {
         const bool keep = a.any_keep != 0, tail = a.acc_vec_end < (long long)a.h * a.w;
-#ifndef FM_PIXW_RW
-#define FM_PIXW_RW 8
-#endif
-        constexpr int RW = FM_PIXW_RW;
-        using G = px::PW<21, RW>;
-        static_assert(2 * G::bytes <= 160 * 1024, "k_pixw LDS: two workgroups per CU");
-        const dim3 gridw(a.ntx * ((a.nty + RW / 8 - 1) / (RW / 8)), a.S);
-#define FM_PIXW_LAUNCH(K, T)                                                                                            \
+        static_assert(2 * px::PW<21, 16>::bytes <= 160 * 1024, "k_pixw LDS: two workgroups per CU");
+        const int nbands = (a.nty + 1) / 2;
+        const bool band = (long long)a.ntx * nbands * a.S >= FM_PIXW_BAND_MIN;
+#define FM_PIXW_LAUNCH(K, T, RW)                                                                                        \
     do {                                                                                                                \
+        using G = px::PW<21, RW>;                                                                                       \
+        const dim3 gw(a.ntx * (RW == 16 ? nbands : a.nty), a.S);                                                        \
         (void)hipFuncSetAttribute((const void*)px::k_pixw<21, K, T, RW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::dyn_bytes); \
-        hipLaunchKernelGGL((px::k_pixw<21, K, T, RW>), gridw, dim3(512), G::dyn_bytes, st, a);                           \
+        hipLaunchKernelGGL((px::k_pixw<21, K, T, RW>), gw, dim3(512), G::dyn_bytes, st, a);                             \
     } while (0)
-        if (keep && tail) FM_PIXW_LAUNCH(true, true);
-        else if (keep) FM_PIXW_LAUNCH(true, false);
-        else if (tail) FM_PIXW_LAUNCH(false, true);
-        else FM_PIXW_LAUNCH(false, false);
+        if (band) {
+            if (keep && tail) FM_PIXW_LAUNCH(true, true, 16);
+            else if (keep) FM_PIXW_LAUNCH(true, false, 16);
+            else if (tail) FM_PIXW_LAUNCH(false, true, 16);
+            else FM_PIXW_LAUNCH(false, false, 16);
+        } else {
+            if (keep && tail) FM_PIXW_LAUNCH(true, true, 8);
+            else if (keep) FM_PIXW_LAUNCH(true, false, 8);
+            else if (tail) FM_PIXW_LAUNCH(false, true, 8);
+            else FM_PIXW_LAUNCH(false, false, 8);
+        }
 #undef FM_PIXW_LAUNCH
         return hipGetLastError();
     }

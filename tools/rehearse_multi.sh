@@ -15,3 +15,8 @@ check gpurun_out/n2_torchrun.log 2 || exit 1
 # (On a real node every rank has a card of its own and keeps its 8 queues.)
 FM_BENCH_HW_QUEUES=4 timeout -k 10 300 python bench.py --gpus 4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-fed --no-mjpeg > gpurun_out/n4_spawn.log 2>&1 || { tail -20 gpurun_out/n4_spawn.log; exit 1; }
 check gpurun_out/n4_spawn.log 4 || exit 1
+# configs[3]'s per-rank shape (8 x 1080p streams per rank, 128 frames per step, a 12.7 GB ring per rank) at two
+# ranks on the one card: the line must read "configs[3] family: 8 streams per GPU x 2 GPUs", world_size_seen 2
+FM_BENCH_HW_QUEUES=4 timeout -k 10 400 python bench.py --gpus 2 --streams 8 --batch 128 --steps 20 --warmup 3 --no-cpu-baseline --no-host-fed --no-mjpeg > gpurun_out/n2_c3.log 2>&1 || { tail -20 gpurun_out/n2_c3.log; exit 1; }
+check gpurun_out/n2_c3.log 2 || exit 1
+grep '^{' gpurun_out/n2_c3.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); w=d['config']['workload']; assert w.startswith('configs[3] family'), w; assert d['ranks']['world_size_seen'] == 2; print('configs[3] family', d['value'], d['ranks'])"
