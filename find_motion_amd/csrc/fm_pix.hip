@@ -671,7 +671,12 @@ struct PW {
     static constexpr int NH = NHP * (TS / 4);      // tap jobs
     static constexpr int HJ = (NH + NTB - 1) / NTB;
     static constexpr int HLASTW = (NH - (HJ - 1) * NTB + 63) / 64;  // waves with a job in the last round
-    static constexpr int GS = GQ;                  // gray row stride in LDS (dwords)
+#ifndef FM_PIXW_GS
+#define FM_PIXW_GS 24
+#endif
+    // gray row stride in LDS (dwords), 24 instead of GQ = 22: a tap job wave's four even gray rows start 48 dwords
+    // apart, so their 16-quad windows fall in disjoint LDS banks (round 6, as in k_pix5)
+    static constexpr int GS = FM_PIXW_GS > GQ ? FM_PIXW_GS : GQ;
     static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
     static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
     static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
@@ -860,6 +865,13 @@ struct P5G {
     static constexpr int TH = RW * NWB;                  // tile rows
     static constexpr int GH = TH + 4;                    // gray rows y0-2 .. y0+TH+1
     static constexpr int GQ = 18;                        // gray quads per row: columns x0-4 .. x0+67
+#ifndef FM_P5_GS
+#define FM_P5_GS 24
+#endif
+    // gray row stride in LDS (dwords): 24, not GQ = 18, so the four even gray rows a tap-job wave reads start 48
+    // dwords apart and their windows fall in disjoint banks: LDS bank conflicts 176.3 M -> 68.2 M per 10-step run
+    // (0.49 -> 0.19 per LDS-active cycle), throughput unchanged (round 6, profiles/r06/r06e_gray_stride_ab.txt)
+    static constexpr int GS = FM_P5_GS > GQ ? FM_P5_GS : GQ;
     static constexpr int NG = GH * GQ;                   // gray jobs per frame
     // Gray jobs go to waves in whole wave-slots of 64 jobs.  Waves 4..7 lose issue arbitration to waves
     // 0..3 (age order) and set every frame's barrier (FM_PTS phase stamps: waves 0..3 spent ~30 % of
@@ -873,7 +885,7 @@ struct P5G {
     static constexpr int HJ = (NH + NTB - 1) / NTB;
     // the last job round is partial: only its first waves have jobs there (a wave-uniform branch)
     static constexpr int HLASTW = (NH - (HJ - 1) * NTB + 63) / 64;
-    static constexpr int GBUF = NG + 64;                 // + a pad slot per lane for the idle jobs' stores (branch-free)
+    static constexpr int GBUF = GH * GS + 64;            // + a pad slot per lane for the idle jobs' stores (branch-free)
     static constexpr int HBUF = (GH + 2) * TS;           // u16; + the pad pair row idle tap jobs store to
     static constexpr int bytes = 2 * GBUF * 4 + 2 * HBUF * 2 + 256 * 8;
     static constexpr int dyn_bytes = bytes - 256 * 8;  // (the table is static LDS)
@@ -946,7 +958,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
         const bool live = j < G::NG && x >= 0 && x + 4 <= w;
         const int y = reflect101(y0 - R + gr, h);
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < G::NG ? (uint32_t)j : (uint32_t)(G::NG + ln);
+        gdst[i] = j < G::NG ? (uint32_t)(G::GS == G::GQ ? j : gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + ln);
     }
     uint32_t hsrc[HJX], hdst[HJX];
 #pragma unroll
@@ -954,7 +966,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
         const int j = tid + G::NTB * i;
         const bool live = j < G::NH;
         const int hr = live ? j / (TS / 4) : 0, hq = live ? j - hr * (TS / 4) : 0;
-        hsrc[i] = (uint32_t)(2 * hr * G::GQ + hq);
+        hsrc[i] = (uint32_t)(2 * hr * G::GS + hq);
         hdst[i] = (uint32_t)((live ? hr : G::GH / 2) * TS + 4 * hq);  // u32 index of the pair's 4 columns
     }
     // REFLECT_101 quads: left of column 0 (tile x0 = 0, tap quad 0 reads gray quad 0 = columns -4..-1:
@@ -965,7 +977,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
     uint32_t hfix[HJX];  // bit0: q0 := mirror of q1 (left); bit1: q1 := mirror of q0; bit2: q2 := mirror of q1
 #pragma unroll
     for (int i = 0; i < HJX; i++) {
-        const int hq = (int)(hsrc[i] % G::GQ);
+        const int hq = (int)(hsrc[i] % G::GS);
         hfix[i] = (x0 == 0 && hq == 0 ? 1u : 0u) | (hq + 1 == vq ? 2u : 0u) | (hq + 2 == vq ? 4u : 0u);
     }
 
@@ -1002,11 +1014,31 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
 
     uint32_t hcs[HS<KC>::NC];
     hs_consts<KC>(hcs);
+#ifndef FM_P5_PFD
+#define FM_P5_PFD 1  // frames of raw quads in flight in registers beyond the one gray(t+2) consumes (A/B: 2)
+#endif
     P5Raw<GJX> rw;
+#if FM_P5_PFD == 2
+    P5Raw<GJX> rw2;
+#endif
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
+#if FM_P5_PFD == 2
+    auto load_into = [&](P5Raw<GJX>& r, size_t f) __attribute__((always_inline)) {
+        const gbytes_t src = frame_base(a.src + f * fbytes);
+#pragma unroll
+        for (int i = 0; i < GJX; i++) load12(r.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
+    };
+    auto gray_from = [&](const P5Raw<GJX>& r, uint32_t* gb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < GJX; i++) {
+            if (i >= gjobs) break;  // wave-uniform
+            gb[gdst[i]] = gray4(r.v[i].x, r.v[i].y, r.v[i].z);
+        }
+    };
+#endif
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
@@ -1036,7 +1068,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
             const uint32_t h2 = hs_tap<KC, 2>(qv, hcs);
             const uint32_t h3 = hs_tap<KC, 3>(qv, hcs);
             // the next gray row, then both rows' sums as row pairs
-            uint32_t qw[4] = {gb[hsrc[i] + G::GQ], gb[hsrc[i] + G::GQ + 1], gb[hsrc[i] + G::GQ + 2], 0u};
+            uint32_t qw[4] = {gb[hsrc[i] + G::GS], gb[hsrc[i] + G::GS + 1], gb[hsrc[i] + G::GS + 2], 0u};
             if (edge_tile) {
                 if (hfix[i] & 1) qw[0] = __builtin_amdgcn_perm(qw[1], qw[1], 0x01020000u);
                 if (hfix[i] & 2) qw[1] = __builtin_amdgcn_perm(qw[0], qw[0], 0x00000102u);
@@ -1063,13 +1095,20 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
     load((size_t)min(t0 + 2, t1 - 1) * S + s);
+#if FM_P5_PFD == 2
+    load_into(rw2, (size_t)min(t0 + 3, t1 - 1) * S + s);
+#endif
 
     // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
     // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
+#if FM_P5_PFD == 2
+    auto frame = [&](int t, int b, P5Raw<GJX>& R) __attribute__((always_inline)) {
+#else
     auto frame = [&](int t, int b) __attribute__((always_inline)) {
+#endif
             const size_t f = (size_t)t * S + s;
             lds_barrier();
             uint32_t colbits = 0, fl = 0;
@@ -1089,7 +1128,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
             // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
             // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
             // makes every frame wait for the stores below before the next loads
+#if FM_P5_PFD == 2
+            gray_from(R, gray + b * G::GBUF);
+#else
             gray_stage(gray + b * G::GBUF);
+#endif
             // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
             // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
             // the prefetch would be waited for with it
@@ -1101,9 +1144,28 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
                 if (ln == 0) *reinterpret_cast<uint2*>(a.tflag + (f * a.ntiles + ti) * NW + 2 * wv) = make_uint2(fl, 0u);
             }
             // unconditional (see load): past the batch's last frame it re-reads that frame
+#if FM_P5_PFD == 2
+            load_into(R, (size_t)min(t + 4, t1 - 1) * S + s);
+#else
             load((size_t)min(t + 3, t1 - 1) * S + s);
+#endif
     };
+#if FM_P5_PFD == 2
+    {
+        // two register sets, frame t + 2 in rw (t - t0 even) or rw2 (odd): the loop body twice, the buffer
+        // index laundered so both bodies keep the one-body code's dynamic LDS offsets
+        int t = t0;
+        for (; t + 1 < t1; t += 2) {
+            int b0 = 0, b1 = 1;
+            asm volatile("" : "+s"(b0), "+s"(b1));
+            frame(t, b0, rw);
+            frame(t + 1, b1, rw2);
+        }
+        if (t < t1) frame(t, 0, rw);
+    }
+#else
     for (int t = t0; t < t1; t++) frame(t, (t - t0) & 1);
+#endif
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
@@ -1140,8 +1202,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
 // Rows: reflect101 source rows, as k_pix5.  Needs w % 4 == 0 and w >= 2 * PC + 8.
 // 2 workgroups per CU (<= 128 VGPRs).  (8 chain + 4 producer waves per tile, as k_pix5's SPL: 57.8 vs
 // 79.0 k frames/s at config 5, round 4.)
+#ifndef FM_PIXW_WPE
+#define FM_PIXW_WPE kPixWPE
+#endif
 template <int KC, bool KEEP, bool TAIL, int RW = RPWV>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(kPixWPE))) void k_pixw(FusedArgs a) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? FM_PIXW_WPE : kPixWPE))) void k_pixw(FusedArgs a) {
     using G = PW<KC, RW>;
     constexpr int TPB = RW / RPWV;  // contour tiles per band (stacked vertically)
     constexpr int GJX = G::GJ, HJX = G::HJ;
