@@ -1014,31 +1014,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
 
     uint32_t hcs[HS<KC>::NC];
     hs_consts<KC>(hcs);
-#ifndef FM_P5_PFD
-#define FM_P5_PFD 1  // frames of raw quads in flight in registers beyond the one gray(t+2) consumes (A/B: 2)
-#endif
     P5Raw<GJX> rw;
-#if FM_P5_PFD == 2
-    P5Raw<GJX> rw2;
-#endif
     // Every wave issues every job's load, idle jobs included (they read the frame's first
     // 12 B): a load under a branch makes its registers a phi of the loaded and the old
     // value, and the copies the compiler then inserts at the loop back-edge wait for the
     // load (vmcnt(0)), so the prefetch would not stay in flight across the frame barrier.
-#if FM_P5_PFD == 2
-    auto load_into = [&](P5Raw<GJX>& r, size_t f) __attribute__((always_inline)) {
-        const gbytes_t src = frame_base(a.src + f * fbytes);
-#pragma unroll
-        for (int i = 0; i < GJX; i++) load12(r.v[i], src, goff[i]);  // global_load_dwordx3 (4-B aligned)
-    };
-    auto gray_from = [&](const P5Raw<GJX>& r, uint32_t* gb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < GJX; i++) {
-            if (i >= gjobs) break;  // wave-uniform
-            gb[gdst[i]] = gray4(r.v[i].x, r.v[i].y, r.v[i].z);
-        }
-    };
-#endif
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const gbytes_t src = frame_base(a.src + f * fbytes);
 #pragma unroll
@@ -1095,20 +1075,13 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
     tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
     load((size_t)min(t0 + 2, t1 - 1) * S + s);
-#if FM_P5_PFD == 2
-    load_into(rw2, (size_t)min(t0 + 3, t1 - 1) * S + s);
-#endif
 
     // ONE frame loop: the chain variant (keep-mask, accumulateWeighted's scalar tail) is a
     // wave-uniform branch inside it, re-read every frame so that the loop is not unswitched.
     // Three loop copies would give the in-flight loads different registers in each, and the
     // wait pass would then wait for them at the top of every frame.
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;  // (cc.vec is wave-uniform)
-#if FM_P5_PFD == 2
-    auto frame = [&](int t, int b, P5Raw<GJX>& R) __attribute__((always_inline)) {
-#else
     auto frame = [&](int t, int b) __attribute__((always_inline)) {
-#endif
             const size_t f = (size_t)t * S + s;
             lds_barrier();
             uint32_t colbits = 0, fl = 0;
@@ -1128,11 +1101,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
             // unconditional like the loads (past the batch's end it fills a buffer nothing reads):
             // a skipped gray stage leaves the loads unwaited on that path, and the wait pass then
             // makes every frame wait for the stores below before the next loads
-#if FM_P5_PFD == 2
-            gray_from(R, gray + b * G::GBUF);
-#else
             gray_stage(gray + b * G::GBUF);
-#endif
             // the frame's bits and flag word, stored after gray(t+2) consumed the loads and before
             // the next ones: vmcnt counts stores and loads in issue order, so stores issued after
             // the prefetch would be waited for with it
@@ -1144,28 +1113,9 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(kPixWP
                 if (ln == 0) *reinterpret_cast<uint2*>(a.tflag + (f * a.ntiles + ti) * NW + 2 * wv) = make_uint2(fl, 0u);
             }
             // unconditional (see load): past the batch's last frame it re-reads that frame
-#if FM_P5_PFD == 2
-            load_into(R, (size_t)min(t + 4, t1 - 1) * S + s);
-#else
             load((size_t)min(t + 3, t1 - 1) * S + s);
-#endif
     };
-#if FM_P5_PFD == 2
-    {
-        // two register sets, frame t + 2 in rw (t - t0 even) or rw2 (odd): the loop body twice, the buffer
-        // index laundered so both bodies keep the one-body code's dynamic LDS offsets
-        int t = t0;
-        for (; t + 1 < t1; t += 2) {
-            int b0 = 0, b1 = 1;
-            asm volatile("" : "+s"(b0), "+s"(b1));
-            frame(t, b0, rw);
-            frame(t + 1, b1, rw2);
-        }
-        if (t < t1) frame(t, 0, rw);
-    }
-#else
     for (int t = t0; t < t1; t++) frame(t, (t - t0) & 1);
-#endif
 
     double* bgo = a.bg_out + (size_t)s * plane;
     const int x = x0 + ln;
