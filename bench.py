@@ -574,6 +574,27 @@ def side_leg(args, mode: str, S: int, T: int, pl, local: int, active: bool, back
     return out
 
 
+# mode D (-B 100 -b 20, the reference CLI's default, find_motion.py:1474); configs[2] (8 x 1080p streams on one
+# GPU, 128 frames per stream per step); configs[4]: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the polygon
+# masks, 64 frames per stream per step from a 64-frame ring cycling 16 synthetic frames, with the frontalface
+# cascade on every 15th written frame (faces drawn in), and the same geometry without the Haar stage
+_C4 = dict(shape=(3840, 2160), blur_scale=183, ring_frames=64, ring_period=16, steps=20, warmup=10)
+SIDE_LEGS = {"mode_d": ("D", 1, None, {}), "configs2": ("F", 8, 128, {}),
+             "configs4": ("F", 4, 64, dict(_C4, haar=True)), "configs4_no_haar": ("F", 4, 64, dict(_C4, masks=True))}
+
+
+def side_child(name: str, args) -> dict:
+    """Run side leg `name` in a child process (bench.py --side-leg NAME) and return its JSON object."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--side-leg", name, "--warmup", str(args.warmup),
+           "--batch", str(args.batch)] + (["--all-ktimes"] if args.all_ktimes else []) + (["--no-ktimes"] if args.no_ktimes else [])
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"side leg {name} exited {r.returncode}"}
+    return json.loads(lines[-1])
+
+
 def rank_devices(local: int, pl, active: bool) -> list:
     """[{rank, device, pci_bus_id, name}] of every rank, gathered on rank 0 through the process group (so
     the line records how many ranks the group really held and which device each ran on)."""
@@ -624,6 +645,8 @@ def main() -> None:
                          "of each stream (find_objects, fm.py:549-575, 703-731) inside the timed steps")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the mode D and configs[2] figures the default (1-GPU, configs[1]) line carries")
+    ap.add_argument("--side-leg", choices=sorted(SIDE_LEGS), default=None,
+                    help="(internal) run one side leg of the default line and print its JSON object")
     ap.add_argument("--all-ktimes", action="store_true",
                     help="HIP events around every kernel (perturbs the pipeline); default: pixel kernel only")
     args = ap.parse_args()
@@ -647,6 +670,10 @@ def main() -> None:
     torch.cuda.set_device(local)
     active = dist.init(pl, backend, torch.device("cuda", local))
 
+    if args.side_leg:  # one side leg of the default line, in a process of its own (side_child)
+        mode, S_, T_, kw = SIDE_LEGS[args.side_leg]
+        print(json.dumps(side_leg(args, mode, S_, T_ or args.batch, pl, local, active, backend, **kw)), flush=True)
+        return
     leg = run_leg(args, args.mode, args.streams, args.batch, args.steps, args.warmup, pl, local, active, backend,
                   haar=args.haar, masks=args.masks)
     cfg, eng, host, P, wall, elapsed = leg["cfg"], leg["eng"], leg["host"], leg["P"], leg["wall"], leg["elapsed"]
@@ -755,17 +782,14 @@ def main() -> None:
     # Side configurations in the same line (per-GPU figures, the 1-GPU run only, after the headline's
     # timed steps): mode D (-B 100 -b 20, the reference CLI's default, find_motion.py:1474) and configs[2]
     # (8 x 1080p streams batched on one GPU), each with its own roofline
+    # Each leg runs in a process of its own (started as a child, after this one's GPU work), as a job of that
+    # workload would: a process that already created and destroyed several engines' streams maps a new
+    # detector's stream onto hardware queues differently, and configs[4]'s Haar leg then read 32-57 k against
+    # 67 k in a fresh process (round 6, profiles/r06/r06c*_default_bench.log)
     side = None
     default_shape = args.mode == "F" and S == 1 and (W, H) == (1920, 1080) and not args.haar
     if world == 1 and default_shape and not args.no_side:
-        side = {"mode_d": side_leg(args, "D", 1, args.batch, pl, local, active, backend),
-                "configs2": side_leg(args, "F", 8, 128, pl, local, active, backend)}
-        # configs[4]: 4 x 3840x2160 streams, -B 3840 -b 183 (k 21), the polygon masks, 64 frames per stream per step
-        # from a 64-frame ring cycling 16 synthetic frames; with the frontalface cascade on every 15th written frame
-        # (faces drawn in), and the same geometry without the Haar stage
-        c4 = dict(shape=(3840, 2160), blur_scale=183, ring_frames=64, ring_period=16, steps=20, warmup=10)
-        side["configs4"] = side_leg(args, "F", 4, 64, pl, local, active, backend, haar=True, **c4)
-        side["configs4_no_haar"] = side_leg(args, "F", 4, 64, pl, local, active, backend, masks=True, **c4)
+        side = {name: side_child(name, args) for name in SIDE_LEGS}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
