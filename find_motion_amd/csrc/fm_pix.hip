@@ -677,15 +677,8 @@ struct PW {
     // gray row stride in LDS (dwords), 24 instead of GQ = 22: a tap job wave's four even gray rows start 48 dwords
     // apart, so their 16-quad windows fall in disjoint LDS banks (round 6, as in k_pix5)
     static constexpr int GS = FM_PIXW_GS > GQ ? FM_PIXW_GS : GQ;
-#ifndef FM_PIXW_HMMA
-#define FM_PIXW_HMMA 0
-#endif
-    // FM_PIXW_HMMA: the horizontal taps as i8 MFMAs over 16-row blocks (k_pixw below), so the gray and H
-    // buffers hold whole blocks: GH rounded up to 16 rows
-    static constexpr bool HM = FM_PIXW_HMMA != 0;
-    static constexpr int GHM = HM ? (GH + 15) / 16 * 16 : GH;
-    static constexpr int GBUF = GHM * GS + 64;     // + a pad slot per lane (idle gray jobs; the MFMA's last row overreads)
-    static constexpr int HBUF = HM ? GHM / 2 * TS : (NHP + 1) * TS;  // u32 pairs + the pad pair row (idle tap jobs)
+    static constexpr int GBUF = GH * GS + 64;      // + a pad slot per lane (idle gray jobs)
+    static constexpr int HBUF = (NHP + 1) * TS;    // u32 pairs + the pad pair row (idle tap jobs)
     static constexpr int LO = tap_lo<KC>(), HI = tap_hi<KC>();
     static constexpr int NGR = (HI - LO + 4) / 4;  // dot4 groups per output
     static constexpr int OFF = PC - R;             // byte of output k's tap 0 in its job's window: OFF + k
@@ -1205,7 +1198,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
         const bool live = j < G::NG && x >= 0 && x + 4 <= w;
         const int y = reflect101(y0 - R + gr, h);
         goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GHM * G::GS + ln);
+        gdst[i] = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + ln);
     }
     const int gjobs = __builtin_amdgcn_readfirstlane(gcnt_w);  // this wave's gray rounds
     uint32_t hsrc[HJX], hdst[HJX];
@@ -1266,70 +1259,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
 #pragma unroll
         for (int i = 0; i < GJX; i++) {
             if (i >= gjobs) break;  // wave-uniform
-            // (HM: stored as i8, gray - 128 = gray ^ 0x80, the MFMA's signed operand)
-            gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z) ^ (G::HM ? 0x80808080u : 0u);
+            gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z);
         }
     };
-    // The horizontal taps as v_mfma_i32_16x16x64_i8 (G::HM): H block (rb, n) = gray rows 16 rb .. +15 times the
-    // banded tap matrix Th[k][c] = tap[k - c - OFF] over gray columns 16 n .. 16 n + 63 (the 21 taps of output
-    // column 16 n + c lie in that K range; later columns carry zero taps, so what they read does not matter).
-    // Operand maps (tools/ubench/mfma_i8_layout.cpp, checked on the GPU with exact integers): lane l (c = l & 15,
-    // q = l >> 4) holds A[c][16 q + j] = the 16 i8 gray bytes of row 16 rb + c from column 16 n + 16 q (one
-    // ds_read_b128), B[16 q + j][c] = Th (one constant per lane), and D[4 q + i][c] in register i.  Gray is
-    // stored as gray - 128, so D = H - 128 * 256 exactly (the taps sum to 256): H's u16 is D ^ 0x8000, and two
-    // rows' u16 make the chain's pair word with one v_perm and one xor.  40 blocks (10 x 4) per band-frame,
-    // 5 per wave, instead of 1,184 dot4 tap jobs.
-    typedef int v4i_t __attribute__((ext_vector_type(4)));
-    v4i_t thm;  // B operand: Th[16 q + j][c], byte j
-    if constexpr (G::HM) {
-        const int c = ln & 15, q = ln >> 4;
-        uint32_t wd[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int t = 16 * q + j - c - G::OFF;
-            const int v = (t >= 0 && t < KC) ? Taps<KC>::c[t < 0 ? 0 : t >= KC ? 0 : t] : 0;
-            wd[j >> 2] |= (uint32_t)(v & 0xFF) << (8 * (j & 3));
-        }
-        thm = v4i_t{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
-    }
-    auto hmma_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
-        constexpr int NRB = G::GHM / 16, NBLK = NRB * (TS / 16), PERW = NBLK / G::NWB;
-        static_assert(!G::HM || NBLK % G::NWB == 0, "H blocks per wave");
-        const int c = ln & 15, q = ln >> 4;
-        const uint8_t* g8 = reinterpret_cast<const uint8_t*>(gb);
-#pragma unroll
-        for (int k = 0; k < PERW; k++) {
-            const int blk = k * G::NWB + wv;             // wave-uniform
-            const int rb = blk >> 2, n = blk & 3;
-            const int row = 16 * rb + c, col0 = 16 * n + 16 * q;
-            v4i_t av = *reinterpret_cast<const v4i_t*>(g8 + row * (4 * G::GS) + col0);
-            if (edge_tile) {
-                // REFLECT_101 columns: bytes of gray columns outside the image (never loaded) from their mirror
-                // columns (x0 - PC + col -> reflect101 -> back to a loaded column)
-                int xe = x0 - PC + col0;
-                asm volatile("" : "+v"(xe));
-                if (xe < 0 || xe + 16 > w) {
-                    uint32_t wd[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const int ic = xe + j;
-                        const int m = (ic >= 0 && ic < w) ? ic : reflect101(ic, w);
-                        const int kc = min(max(m - (x0 - PC), 0), 4 * G::GQ - 1);
-                        wd[j >> 2] |= (uint32_t)g8[row * (4 * G::GS) + kc] << (8 * (j & 3));
-                    }
-                    av = v4i_t{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
-                }
-            }
-            v4i_t d = {0, 0, 0, 0};
-            d = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, thm, d, 0, 0, 0);
-            // rows 16 rb + 4 q + {0, 1} and {2, 3} of column 16 n + c: pair rows 8 rb + 2 q + {0, 1}
-            const uint32_t p0 = __builtin_amdgcn_perm((uint32_t)d[1], (uint32_t)d[0], 0x05040100u) ^ 0x80008000u;
-            const uint32_t p1 = __builtin_amdgcn_perm((uint32_t)d[3], (uint32_t)d[2], 0x05040100u) ^ 0x80008000u;
-            uint32_t* hp = Hb + (8 * rb + 2 * q) * TS + 16 * n + c;
-            hp[0] = p0;
-            hp[TS] = p1;
-        }
-    };
+    // (The horizontal taps as v_mfma_i32_16x16x64_i8 -- 5 blocks of 16 H rows x 16 columns per wave-frame instead of
+    // the dot4 tap jobs, bit-exact on the GPU suite -- ran 6 % longer per configs[4] launch; round 6,
+    // profiles/r06/r06g_mfma_taps_ab.txt.)
     // one row of a tap job: the quad's 4 horizontal sums from WQ gray dwords (edge tiles: the
     // mirrored quads rebuilt first)
     auto hrow = [&](const uint32_t* row, int hq, uint32_t (&o)[4]) __attribute__((always_inline)) {
@@ -1373,8 +1308,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
     gray_stage(gray);
     load((size_t)min(t0 + 1, t1 - 1) * S + s);
     __syncthreads();  // atab, gray(t0)
-    if constexpr (G::HM) hmma_stage(gray, Hs);
-    else tap_stage(gray, Hs);
+    tap_stage(gray, Hs);
     if (t0 + 1 < t1) gray_stage(gray + G::GBUF);
     load((size_t)min(t0 + 2, t1 - 1) * S + s);
     const int var0 = TAIL ? (int)(cc.vec == 0) : 0;
@@ -1396,10 +1330,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
             chain_rows_w<KC, KEEP, false, true, RW, NWT, 8>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
         else
             chain_rows_w<KC, KEEP, true, true, RW, NWT, 8>(a, Hb, atab, bg, wvf, ln, x0f, y0f, ccf, colbits, fl);
-        if (t + 1 < t1) {
-            if constexpr (G::HM) hmma_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
-            else tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
-        }
+        if (t + 1 < t1) tap_stage(gray + (b ^ 1) * G::GBUF, Hs + (b ^ 1) * G::HBUF);
         gray_stage(gray + b * G::GBUF);
         if constexpr (RW == 8) {
             reinterpret_cast<uint8_t*>(a.bits)[((f * a.ntiles + ti) * TS + ln) * 8 + wv] = (uint8_t)colbits;
