@@ -232,9 +232,13 @@ typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
 // 12 bytes at a 4-B aligned global address (global_load_dwordx3)
 // (the compiler keeps base + offset as one 64-bit add per load: passing the offset through an empty
 // asm to get SGPR base + 32-bit VGPR offset cost a copy per load and a vmcnt wait at the back-edge)
+#ifndef FM_P5_NT
+#define FM_P5_NT 0  // (A/B) the frame loads non-temporal
+#endif
 __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) {
     typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
-    d = *(const __attribute__((address_space(1))) u3a*)(base + off);
+    if constexpr (FM_P5_NT) d = __builtin_nontemporal_load((const __attribute__((address_space(1))) u3a*)(base + off));
+    else d = *(const __attribute__((address_space(1))) u3a*)(base + off);
 }
 // k_pixw's quad loads are buffer loads through a per-frame descriptor built from wave-uniform values
 // (frame base and size in SGPRs): the lane's 32-bit offset is the whole per-lane address, so the 64-bit
