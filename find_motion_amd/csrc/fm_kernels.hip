@@ -173,9 +173,8 @@ __global__ __launch_bounds__(RS_T) void k_resize_area_rows(const uint8_t* __rest
 // k_resize_area's: buf = sum_x S*alpha in xtab order, sum = beta_0*buf_0 + beta_1*buf_1 + ...
 // in ytab order, then saturate_cast (rne).
 typedef float rs_f2 __attribute__((ext_vector_type(2)));
-#ifndef FM_RS_AUX
-#define FM_RS_AUX 0  // cache policy of the resize's frame loads (A/B: 2 = non-temporal)
-#endif
+// (Non-temporal frame loads: mode D 492 vs 822 k frames/s -- neighbouring windows re-read a column; round 6,
+// profiles/r06/r06i_nontemporal_ab.txt.)
 constexpr int RN_T = 256;
 template <int NT>
 __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -219,16 +218,16 @@ __global__ __launch_bounds__(RN_T) void k_resize_area_nt(const uint8_t* __restri
             if (a + 4u * ND <= lim) {
 #pragma unroll
                 for (int q = 0; q < NQ; q++) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(a + 16u * q), 0, FM_RS_AUX);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(a + 16u * q), 0, 0);
                     d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
                 }
                 if constexpr (NR == 1) {
-                    d[4 * NQ] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a + 16u * NQ), 0, FM_RS_AUX);
+                    d[4 * NQ] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a + 16u * NQ), 0, 0);
                 } else if constexpr (NR == 2) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u * NQ), 0, FM_RS_AUX);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u * NQ), 0, 0);
                     d[4 * NQ] = v[0]; d[4 * NQ + 1] = v[1];
                 } else if constexpr (NR == 3) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(a + 16u * NQ), 0, FM_RS_AUX);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(a + 16u * NQ), 0, 0);
                     d[4 * NQ] = v[0]; d[4 * NQ + 1] = v[1]; d[4 * NQ + 2] = v[2];
                 }
             } else {  // the window runs past the frame (its last columns / a row past the walk): dwords

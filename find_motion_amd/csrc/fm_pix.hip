@@ -232,13 +232,10 @@ typedef uint32_t u32x3_t __attribute__((ext_vector_type(3)));
 // 12 bytes at a 4-B aligned global address (global_load_dwordx3)
 // (the compiler keeps base + offset as one 64-bit add per load: passing the offset through an empty
 // asm to get SGPR base + 32-bit VGPR offset cost a copy per load and a vmcnt wait at the back-edge)
-#ifndef FM_P5_NT
-#define FM_P5_NT 0  // (A/B) the frame loads non-temporal
-#endif
+// (non-temporal: 345 vs 412 k frames/s -- the halo lines are re-read from L2; round 6, r06i_nontemporal_ab.txt)
 __device__ __forceinline__ void load12(u32x3_t& d, gbytes_t base, uint32_t off) {
     typedef uint32_t __attribute__((ext_vector_type(3), aligned(4))) u3a;
-    if constexpr (FM_P5_NT) d = __builtin_nontemporal_load((const __attribute__((address_space(1))) u3a*)(base + off));
-    else d = *(const __attribute__((address_space(1))) u3a*)(base + off);
+    d = *(const __attribute__((address_space(1))) u3a*)(base + off);
 }
 // k_pixw's quad loads are buffer loads through a per-frame descriptor built from wave-uniform values
 // (frame base and size in SGPRs): the lane's 32-bit offset is the whole per-lane address, so the 64-bit
@@ -1190,32 +1187,41 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
     if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
     kstamp_begin(a.kstamp);
 
-    // ---- per-thread job plans (frame invariant)
-    uint32_t goff[GJX], gdst[GJX];
+    // ---- per-thread job plans (frame invariant).  FM_PIXW_REPLAN (A/B, bands only): recomputed where they are
+    // used, from a laundered lane id, instead of 23 registers held for the whole launch
+#ifndef FM_PIXW_REPLAN
+#define FM_PIXW_REPLAN 0
+#endif
+    constexpr bool REPLAN = FM_PIXW_REPLAN != 0 && RW == 16;
     const int gcnt_w = G::gcnt(wv);
-#pragma unroll
-    for (int i = 0; i < GJX; i++) {
+    auto gplan = [&](int i, int lnv, uint32_t& go, uint32_t& gd) __attribute__((always_inline)) {
         const int slot = i * G::NWB + wv;
-        const int j = (i < gcnt_w && slot < G::GSLOTS) ? slot * 64 + ln : G::NG;  // idle: dummy load
+        const int j = (i < gcnt_w && slot < G::GSLOTS) ? slot * 64 + lnv : G::NG;  // idle: dummy load
         const int gr = j / GQ, gq = j - gr * GQ;
         const int x = x0 - PC + 4 * gq;
         const bool live = j < G::NG && x >= 0 && x + 4 <= w;
         const int y = reflect101(y0 - R + gr, h);
-        goff[i] = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
-        gdst[i] = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + ln);
-    }
-    const int gjobs = __builtin_amdgcn_readfirstlane(gcnt_w);  // this wave's gray rounds
-    uint32_t hsrc[HJX], hdst[HJX];
-    int hqv[HJX];
-#pragma unroll
-    for (int i = 0; i < HJX; i++) {
-        const int j = tid + G::NTB * i;
+        go = live ? (uint32_t)(((size_t)y * w + x) * 3) : 0u;
+        gd = j < G::NG ? (uint32_t)(gr * G::GS + gq) : (uint32_t)(G::GH * G::GS + lnv);
+    };
+    auto hplan = [&](int i, int tidv, uint32_t& hs, uint32_t& hd, int& hq_) __attribute__((always_inline)) {
+        const int j = tidv + G::NTB * i;
         const bool live = j < G::NH;
         const int hp = live ? j / (TS / 4) : 0, hq = live ? j - hp * (TS / 4) : 0;
-        hqv[i] = hq;
-        hsrc[i] = (uint32_t)(2 * hp * G::GS + hq);
-        hdst[i] = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);
+        hq_ = hq;
+        hs = (uint32_t)(2 * hp * G::GS + hq);
+        hd = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);
+    };
+    uint32_t goff[REPLAN ? 1 : GJX], gdst[REPLAN ? 1 : GJX];
+    uint32_t hsrc[REPLAN ? 1 : HJX], hdst[REPLAN ? 1 : HJX];
+    int hqv[REPLAN ? 1 : HJX];
+    if constexpr (!REPLAN) {
+#pragma unroll
+        for (int i = 0; i < GJX; i++) gplan(i, ln, goff[i], gdst[i]);
+#pragma unroll
+        for (int i = 0; i < HJX; i++) hplan(i, tid, hsrc[i], hdst[i], hqv[i]);
     }
+    const int gjobs = __builtin_amdgcn_readfirstlane(gcnt_w);  // this wave's gray rounds
     const bool edge_tile = x0 - PC < 0 || x0 + TS + PC > w;  // workgroup-uniform
 
     double bg[RW];
@@ -1256,14 +1262,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
+        int lnv = ln;
+        if constexpr (REPLAN) asm volatile("" : "+v"(lnv));
 #pragma unroll
-        for (int i = 0; i < GJX; i++) load12b(rw[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
+        for (int i = 0; i < GJX; i++) {
+            uint32_t go = 0, gd = 0;
+            if constexpr (REPLAN) gplan(i, lnv, go, gd);
+            else go = goff[i];
+            load12b(rw[i], rs, go);  // buffer_load_dwordx3, SGPR descriptor
+        }
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
+        int lnv = ln;
+        if constexpr (REPLAN) asm volatile("" : "+v"(lnv));
 #pragma unroll
         for (int i = 0; i < GJX; i++) {
             if (i >= gjobs) break;  // wave-uniform
-            gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z);
+            uint32_t go = 0, gd = 0;
+            if constexpr (REPLAN) gplan(i, lnv, go, gd);
+            else gd = gdst[i];
+            gb[gd] = gray4(rw[i].x, rw[i].y, rw[i].z);
         }
     };
     // (The horizontal taps as v_mfma_i32_16x16x64_i8 -- 5 blocks of 16 H rows x 16 columns per wave-frame instead of
@@ -1296,15 +1314,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
         o[3] = htap<3, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
     };
     auto tap_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
+        int tidv = tid;
+        if constexpr (REPLAN) asm volatile("" : "+v"(tidv));
 #pragma unroll
         for (int i = 0; i < HJX; i++) {
             if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
-            const uint32_t* r0 = gb + (hsrc[i] - hqv[i]);
+            uint32_t hs, hd;
+            int hq;
+            if constexpr (REPLAN) hplan(i, tidv, hs, hd, hq);
+            else hs = hsrc[i], hd = hdst[i], hq = hqv[i];
+            const uint32_t* r0 = gb + (hs - hq);
             uint32_t u[4], v[4];
-            hrow(r0, hqv[i], u);
-            hrow(r0 + G::GS, hqv[i], v);
-            *reinterpret_cast<uint4*>(Hb + hdst[i]) = make_uint4(u[0] | (v[0] << 16), u[1] | (v[1] << 16),
-                                                                  u[2] | (v[2] << 16), u[3] | (v[3] << 16));
+            hrow(r0, hq, u);
+            hrow(r0 + G::GS, hq, v);
+            *reinterpret_cast<uint4*>(Hb + hd) = make_uint4(u[0] | (v[0] << 16), u[1] | (v[1] << 16),
+                                                             u[2] | (v[2] << 16), u[3] | (v[3] << 16));
         }
     };
     const int t0 = a.t_begin, t1 = a.t_end;
