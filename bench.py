@@ -120,6 +120,14 @@ def config_name(S: int, W: int, H: int, mode: str, k: int, haar: bool = False, w
     return "custom shape"
 
 
+def workload_name(S: int, W: int, H: int, mode: str, box: int, blur_scale: int, k: int, T: int, R: int,
+                  ring_period: int, haar: bool = False, world: int = 1) -> str:
+    """The line's config.workload (also the key of the workload's PMC entry in profiles/traffic.json)."""
+    return (f"{config_name(S, W, H, mode, k, haar, world)}: {S}x{W}x{H} stream(s) per GPU, mode {mode} "
+            f"(-B {box} -b {blur_scale}, k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
+            + (f" cycling {ring_period} synthetic frames" if ring_period < R else ""))
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -403,9 +411,7 @@ def run_leg(args, mode: str, S: int, T: int, steps: int, warmup: int, pl, local:
     ring_frames = args.ring if ring_frames is None else ring_frames
     ring_period = args.ring_period if ring_period is None else ring_period
     R = max(ring_frames - ring_frames % T, T)
-    cfg = {"workload": f"{config_name(S, W, H, mode, k, haar, world)}: {S}x{W}x{H} stream(s) per GPU, mode {mode} "
-                       f"(-B {box} -b {blur_scale}, k {k}), {T} frames/stream/step from a {R}-frame device-resident ring"
-                       + (f" cycling {ring_period} synthetic frames" if ring_period < R else ""),
+    cfg = {"workload": workload_name(S, W, H, mode, box, blur_scale, k, T, R, ring_period, haar, world),
            "streams_per_gpu": S, "frames_per_step": T, "W": W, "H": H, "box": box, "ksize": k,
            "h": work_height(H, W, box), "w": box, "threshold": 12, "avg": 0.1, "parallelism": f"streams x {world} GPUs"}
 
