@@ -191,6 +191,22 @@ def test_k21_tall_bands_odd_tile_rows():
     run_pair(1024, 900, 1024, ksize=21, S=9, T=2, n_batches=2, masks=masks, keep_planes=False, start=40)
 
 
+@pytest.mark.parametrize("W,H,masks", [(256, 256, False), (252, 250, True)])
+def test_k5_four_wave_tiles(W, H, masks):
+    """k = 5 on k_pix5's 4-wave, 16-row tiles (a grid of >= 1,024 tile-streams: 64 streams x 16 tiles): without
+    masks, and with masks on every stream plus accumulateWeighted's scalar tail (252 x 250: h*w % 16 = 8), a right
+    tile 60 px wide and a bottom tile 58 rows tall (round 6)."""
+    m = [((0, 0), (W // 5, H // 4)), ((W - 1, H - 1), (W // 2, H - 1), (W - 1, H // 2))] if masks else None
+    run_pair(W, H, W, ksize=5, S=64, T=3, n_batches=2, masks=m, keep_planes=False, start=30)
+
+
+def test_k21_bands_scalar_tail_and_masks():
+    """k = 21 on 128-row bands (4 streams x 16 x 8 bands = 512) with accumulateWeighted's scalar tail
+    (1000 x 901: h*w % 16 = 8), 15 tile rows (the last band's lower waves store nothing), masks (round 6)."""
+    masks = [((0, 0), (200, 150)), ((999, 900), (700, 900), (999, 600))]
+    run_pair(1000, 901, 1000, ksize=21, S=4, T=3, n_batches=2, masks=masks, keep_planes=False, start=60)
+
+
 @pytest.mark.parametrize("W,H,S", [(200, 131, 2), (40, 30, 1), (1000, 70, 1), (320, 240, 3), (203, 90, 1)])
 def test_k21_wide_kernel_geometries(W, H, S):
     """k = 21 steady state (k_pixw, no planes): a right tile 8 px wide, both REFLECT_101 edges in one tile
