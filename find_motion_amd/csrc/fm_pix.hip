@@ -1187,12 +1187,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
     if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
     kstamp_begin(a.kstamp);
 
-    // ---- per-thread job plans (frame invariant).  FM_PIXW_REPLAN (A/B, bands only): recomputed where they are
-    // used, from a laundered lane id, instead of 23 registers held for the whole launch
-#ifndef FM_PIXW_REPLAN
-#define FM_PIXW_REPLAN 0
-#endif
-    constexpr bool REPLAN = FM_PIXW_REPLAN != 0 && RW == 16;
+    // ---- per-thread job plans (frame invariant).  (Recomputed where used instead of held in 23 registers -- 99
+    // instead of 119 VGPRs, so a detector or contour wave fits beside two band workgroups -- the launch took 25 %
+    // longer: round 6, profiles/r06/r06j_replan_ab.txt.)
     const int gcnt_w = G::gcnt(wv);
     auto gplan = [&](int i, int lnv, uint32_t& go, uint32_t& gd) __attribute__((always_inline)) {
         const int slot = i * G::NWB + wv;
@@ -1212,15 +1209,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
         hs = (uint32_t)(2 * hp * G::GS + hq);
         hd = (uint32_t)((live ? hp : G::NHP) * TS + 4 * hq);
     };
-    uint32_t goff[REPLAN ? 1 : GJX], gdst[REPLAN ? 1 : GJX];
-    uint32_t hsrc[REPLAN ? 1 : HJX], hdst[REPLAN ? 1 : HJX];
-    int hqv[REPLAN ? 1 : HJX];
-    if constexpr (!REPLAN) {
+    uint32_t goff[GJX], gdst[GJX], hsrc[HJX], hdst[HJX];
+    int hqv[HJX];
 #pragma unroll
-        for (int i = 0; i < GJX; i++) gplan(i, ln, goff[i], gdst[i]);
+    for (int i = 0; i < GJX; i++) gplan(i, ln, goff[i], gdst[i]);
 #pragma unroll
-        for (int i = 0; i < HJX; i++) hplan(i, tid, hsrc[i], hdst[i], hqv[i]);
-    }
+    for (int i = 0; i < HJX; i++) hplan(i, tid, hsrc[i], hdst[i], hqv[i]);
     const int gjobs = __builtin_amdgcn_readfirstlane(gcnt_w);  // this wave's gray rounds
     const bool edge_tile = x0 - PC < 0 || x0 + TS + PC > w;  // workgroup-uniform
 
@@ -1262,26 +1256,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
     // branch would make its registers a phi and the prefetch would be waited for at the back-edge
     auto load = [&](size_t f) __attribute__((always_inline)) {
         const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.src + f * fbytes, (uint32_t)fbytes);
-        int lnv = ln;
-        if constexpr (REPLAN) asm volatile("" : "+v"(lnv));
 #pragma unroll
-        for (int i = 0; i < GJX; i++) {
-            uint32_t go = 0, gd = 0;
-            if constexpr (REPLAN) gplan(i, lnv, go, gd);
-            else go = goff[i];
-            load12b(rw[i], rs, go);  // buffer_load_dwordx3, SGPR descriptor
-        }
+        for (int i = 0; i < GJX; i++) load12b(rw[i], rs, goff[i]);  // buffer_load_dwordx3, SGPR descriptor
     };
     auto gray_stage = [&](uint32_t* gb) __attribute__((always_inline)) {
-        int lnv = ln;
-        if constexpr (REPLAN) asm volatile("" : "+v"(lnv));
 #pragma unroll
         for (int i = 0; i < GJX; i++) {
             if (i >= gjobs) break;  // wave-uniform
-            uint32_t go = 0, gd = 0;
-            if constexpr (REPLAN) gplan(i, lnv, go, gd);
-            else gd = gdst[i];
-            gb[gd] = gray4(rw[i].x, rw[i].y, rw[i].z);
+            gb[gdst[i]] = gray4(rw[i].x, rw[i].y, rw[i].z);
         }
     };
     // (The horizontal taps as v_mfma_i32_16x16x64_i8 -- 5 blocks of 16 H rows x 16 columns per wave-frame instead of
@@ -1314,15 +1296,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RW == 16 ? 
         o[3] = htap<3, G::OFF + G::LO, G::NGR, 0, G::WQ>(qv, cpk, 0u);
     };
     auto tap_stage = [&](const uint32_t* gb, uint32_t* Hb) __attribute__((always_inline)) {
-        int tidv = tid;
-        if constexpr (REPLAN) asm volatile("" : "+v"(tidv));
 #pragma unroll
         for (int i = 0; i < HJX; i++) {
             if (i == G::HJ - 1 && wv >= G::HLASTW) break;  // wave-uniform
-            uint32_t hs, hd;
-            int hq;
-            if constexpr (REPLAN) hplan(i, tidv, hs, hd, hq);
-            else hs = hsrc[i], hd = hdst[i], hq = hqv[i];
+            const uint32_t hs = hsrc[i], hd = hdst[i];
+            const int hq = hqv[i];
             const uint32_t* r0 = gb + (hs - hq);
             uint32_t u[4], v[4];
             hrow(r0, hq, u);
