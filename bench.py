@@ -594,7 +594,8 @@ def side_child(name: str, args) -> dict:
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--side-leg", name, "--warmup", str(args.warmup),
            "--batch", str(args.batch)] + (["--all-ktimes"] if args.all_ktimes else []) + (["--no-ktimes"] if args.no_ktimes else [])
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
+    env = {k: v for k, v in os.environ.items() if k != "FM_BENCH_PG"}  # no group of its own beside the parent's
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600, env=env)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": f"side leg {name} exited {r.returncode}"}
@@ -674,7 +675,8 @@ def main() -> None:
         local = int(os.environ["FM_BENCH_DEVICE"])
     backend = os.environ.get("FM_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
-    active = dist.init(pl, backend, torch.device("cuda", local))
+    # FM_BENCH_PG=1: a process group even at one rank (the N>1 path's RCCL calls on a one-GPU box)
+    active = dist.init(pl, backend, torch.device("cuda", local), force=os.environ.get("FM_BENCH_PG") == "1")
 
     if args.side_leg:  # one side leg of the default line, in a process of its own (side_child)
         mode, S_, T_, kw = SIDE_LEGS[args.side_leg]
@@ -809,7 +811,8 @@ def main() -> None:
                "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "side_configs": side,
                # launches that found the stamp ring full between two folds (timed by events on one in four, or not)
                "unstamped_launches": leg["unstamped"],
-               "ranks": {"world_size_seen": dist.world_size(active), "devices": ranks}, "host_fed_per_gpu": host_fed,
+               "ranks": {"world_size_seen": dist.world_size(active), "devices": ranks,
+                         "group_backend": backend if active else None}, "host_fed_per_gpu": host_fed,
                "mjpeg_fed_per_gpu": mjpeg, "footprint_per_gpu": footprint,
                "hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                "haar_stage": None if det is None else haar_summary(haar, wall),

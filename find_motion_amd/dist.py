@@ -34,9 +34,14 @@ def rank_streams(p: Placement, streams_per_rank: int) -> list:
     return list(range(p.rank * streams_per_rank, (p.rank + 1) * streams_per_rank))
 
 
-def init(p: Placement, backend: str, device=None) -> bool:
-    """Initialise the process group when world > 1 (rendezvous from MASTER_ADDR/PORT)."""
-    if p.world <= 1:
+def init(p: Placement, backend: str, device=None, force: bool = False) -> bool:
+    """Initialise the process group when world > 1 (rendezvous from MASTER_ADDR/PORT).
+
+    `force` also builds a one-rank group, so that the RCCL calls an 8-GPU run makes (the
+    `device_id` binding, barrier, all-reduce of a device tensor, gather_object) run on a
+    one-GPU box too (bench.py's FM_BENCH_PG=1); RCCL refuses two ranks on one device.
+    """
+    if p.world <= 1 and not force:
         return False
     import torch.distributed as dist
 

@@ -127,12 +127,16 @@ def test_side_legs_run_in_child_processes(bench, monkeypatch):
         def __init__(self, rc, out):
             self.returncode, self.stdout = rc, out
 
-    def fake_run(cmd, stdout=None, text=None, timeout=None):
-        seen.append(cmd)
+    def fake_run(cmd, stdout=None, text=None, timeout=None, env=None):
+        seen.append((cmd, env))
         return R(0, "noise\n" + json.dumps({"value": 1.0}) + "\n") if "mode_d" in cmd else R(1, "")
 
     monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setenv("FM_BENCH_PG", "1")
     args = type("A", (), {"warmup": 5, "batch": 256, "all_ktimes": False, "no_ktimes": False})()
     assert bench.side_child("mode_d", args) == {"value": 1.0}
     assert "error" in bench.side_child("configs4", args)
-    assert seen[0][1].endswith("bench.py") and seen[0][2:4] == ["--side-leg", "mode_d"]
+    cmd, env = seen[0]
+    assert cmd[1].endswith("bench.py") and cmd[2:4] == ["--side-leg", "mode_d"]
+    # the parent's one-rank process group is not rebuilt by the child on the parent's rendezvous
+    assert "FM_BENCH_PG" not in env and env.get("PATH") == os.environ.get("PATH")

@@ -76,6 +76,33 @@ def test_two_rank_sharding_equals_single_process(tmp_path):
     assert any(g[3] for g in gathered)
 
 
+def _one_rank_worker(port, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    from find_motion_amd import dist
+
+    p = dist.placement_from_env()
+    active = dist.init(p, "gloo", force=True)
+    dist.barrier(active)
+    out = (active, dist.world_size(active), dist.max_over_ranks(2.5, active), dist.gather_to_root("r0", p, active))
+    dist.finalize(active)
+    q.put(out)
+
+
+def test_forced_one_rank_group():
+    """bench.py's FM_BENCH_PG=1: a one-rank group runs every call the N>1 path makes (gloo here; RCCL on the box)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_one_rank_worker, args=(_free_port(), q))
+    pr.start()
+    out = q.get(timeout=120)
+    pr.join(timeout=60)
+    assert pr.exitcode == 0
+    assert out == (True, 1, 2.5, ["r0"])
+
+
 def test_placement_and_shards():
     from find_motion_amd import dist
 
