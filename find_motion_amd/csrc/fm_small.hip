@@ -49,20 +49,25 @@ __device__ __forceinline__ uint32_t gray_px(uint32_t b, uint32_t g, uint32_t r) 
     return (b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14;
 }
 
-// LDS of k_small_blur: gray u8 [h][w], H u32 [h][w], reflected column / row indices
+// H's row stride in dwords: odd, so that the vertical pass's 64 lanes (consecutive rows of one column)
+// read 64 distinct banks (at w = 100 the unpadded stride put them on 16 banks: 4-way conflicts)
+__host__ __device__ constexpr int h_stride(int w) { return w | 1; }
+
+// LDS of k_small_blur: gray u8 [h][w], H u32 [h][h_stride(w)], reflected column / row indices
 __host__ __device__ constexpr size_t blur_lds_bytes(int h, int w, int R) {
-    return ((size_t)h * w + 3) / 4 * 4 + (size_t)h * w * 4 + (size_t)(w + 2 * R) * 4 + (size_t)(h + 2 * R) * 4;
+    return ((size_t)h * w + 3) / 4 * 4 + (size_t)h * h_stride(w) * 4 + (size_t)(w + 2 * R) * 4 +
+           (size_t)(h + 2 * R) * 4;
 }
 
 __global__ __launch_bounds__(BT) void k_small_blur(FusedArgs a, uint8_t* __restrict__ sblur, int CS) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int h = a.h, w = a.w, S = a.S, K = a.ksize, R = K >> 1;
-    const int n = h * w;
+    const int n = h * w, HS = h_stride(w);
     const size_t f = (size_t)a.t_begin * S + blockIdx.x;  // frame of this workgroup (t_begin * S + t * S + s)
     const int s = (int)(f % S);
     uint8_t* g = lds;
     uint32_t* H = reinterpret_cast<uint32_t*>(lds + (n + 3) / 4 * 4);
-    int* xi = reinterpret_cast<int*>(H + n);  // [w + 2R]: reflected source column of x - R
+    int* xi = reinterpret_cast<int*>(H + (size_t)h * HS);  // [w + 2R]: reflected source column of x - R
     int* yi = xi + w + 2 * R;                 // [h + 2R]
     const int tid = threadIdx.x;
     kstamp_begin_grid(a.kstamp);
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(BT) void k_small_blur(FusedArgs a, uint8_t* __restr
         const uint8_t* row = g + y * w;
         uint32_t acc = 0;
         for (int t = 0; t < K; t++) acc += (uint32_t)a.coef[t] * row[xi[x + t]];
-        H[i] = acc;
+        H[y * HS + x] = acc;
     }
     __syncthreads();
     // vertical taps, rounding, keep-mask; written column-major: thread i -> (x, y) with y fastest
@@ -106,7 +111,7 @@ __global__ __launch_bounds__(BT) void k_small_blur(FusedArgs a, uint8_t* __restr
     for (int i = tid; i < n; i += BT) {
         const int x = i / h, y = i - x * h;
         uint32_t acc = 32768u;
-        for (int t = 0; t < K; t++) acc += (uint32_t)a.coef[t] * H[yi[y + t] * w + x];
+        for (int t = 0; t < K; t++) acc += (uint32_t)a.coef[t] * H[yi[y + t] * HS + x];
         uint32_t blur = acc >> 16;
         if (hk && keep[y * w + x] == 0) blur = 0;
         out[x * CS + y] = (uint8_t)blur;
@@ -116,11 +121,9 @@ __global__ __launch_bounds__(BT) void k_small_blur(FusedArgs a, uint8_t* __restr
 
 template <bool TAILK>
 __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* __restrict__ sblur, int CS) {
-    __shared__ double atab[256];  // blur * alpha (the same correctly rounded product)
     const int tid = threadIdx.x, ln = tid & 63;
     const int h = a.h, w = a.w, S = a.S;
-    if (tid < 256) atab[tid] = __dmul_rn((double)tid, a.alpha);
-    __syncthreads();
+    const double alpha = a.alpha;
     kstamp_begin_grid(a.kstamp);
     const int job = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (ST / 64) + (tid >> 6)));
     const int njobs = S * w * a.nty;
@@ -183,7 +186,10 @@ __global__ __launch_bounds__(ST) void k_small_scan(FusedArgs a, const uint8_t* _
                 const int q = min(max(__float2int_rn(fabsf(__double2float_rn(bv))), 0), 255);
                 const int d = abs((int)blur - q);
                 const uint64_t word = __builtin_amdgcn_ballot_w64(d > thr) & vmask;
-                const double bl = atab[blur];
+                // blur * alpha on the VALU (the pixel kernels' LDS table holds the same correctly rounded
+                // product): a 256-entry f64 table read by 64 unrelated bytes averaged 1.95 bank-conflict
+                // cycles per LDS cycle here, and the product is off the background's dependency chain
+                const double bl = __dmul_rn((double)blur, alpha);
                 bg = tail ? __dadd_rn(bl, __dmul_rn(bv, beta)) : __fma_rn(bv, beta, bl);
                 const int kb = (t - t0) & 63;
                 const bool mine = ln == kb;
