@@ -447,17 +447,25 @@ __global__ __launch_bounds__(256) void k_heval_tail(const uint32_t* __restrict__
 
 // The whole window sweep for one tile of TW x TH windows of one scale of one image: the tile's
 // integral patch (and the tilted one) is staged in LDS once, so every feature's corner reads are
-// LDS reads instead of gathers from L2; every window runs the first `split` stages (one thread
-// each), the survivors are compacted to the workgroup's first threads and run the rest in dense
-// waves.  Same windows, same arithmetic, same res values as k_heval + k_heval_tail.
+// LDS reads instead of gathers from L2; the stages run in phases, each on the previous phase's
+// survivors compacted into the workgroup's first threads (round 6: the tail packed instead of spread
+// over the four waves, detector device time -25 %; tests/haar_wave_model.py prices the layouts).
+// Same windows, same arithmetic, same res values as k_heval + k_heval_tail.
 constexpr int TW = 16, TH = 16;  // windows per tile (256 threads)
+#ifndef FM_HAAR_HEADC
+#define FM_HAAR_HEADC 1  // compact the survivors after stages 1 and 2 as well
+#endif
+#ifndef FM_HAAR_TAIL_SPREAD
+#define FM_HAAR_TAIL_SPREAD 0  // 1: the last phase's survivors spread over the four waves
+#endif
 
 __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
                                                      const uint32_t* __restrict__ T, int8_t* __restrict__ res, int split,
                                                      CascadeDev c, Geo g, int pw_max) {
     extern __shared__ uint32_t patch[];  // S patch [ph][pw], then T patch (tilted cascades)
-    __shared__ int s_live[TW * TH];
-    __shared__ int s_n;
+    __shared__ int s_live[2][TW * TH];   // the windows (thread ids) a phase runs, double-buffered
+    __shared__ int s_n[4];               // their count, per phase
+    __shared__ float s_vnf[TW * TH];
     const int img = blockIdx.y;
     const int s = find_scale(g.toff, g.n, blockIdx.x);
     const int tile = blockIdx.x - g.toff[s];
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict_
     const int pw = min((TW - 1) * step + c.win_w + 1, st - px0), ph = min((TH - 1) * step + c.win_h + 1, ih - py0);
     const size_t base = (size_t)img * g.I + g.ioff[s];
     const int tid = threadIdx.x;
-    if (tid == 0) s_n = 0;
+    if (tid < 4) s_n[tid] = 0;
     for (int i = tid; i < pw * ph; i += TW * TH) {
         const int y = i / pw, x = i - y * pw;
         const size_t gi = base + (size_t)(py0 + y) * st + px0 + x;
@@ -476,68 +484,74 @@ __global__ __launch_bounds__(TW * TH) void k_hdetect(const uint32_t* __restrict_
         if (c.has_tilted) patch[ph * pw_max + y * pw_max + x] = T[gi];
     }
     __syncthreads();
-    const int gx = gx0 + (tid % TW), gy = gy0 + tid / TW;
-    const bool in = gx < g.gw[s] && gy < g.gh[s];
-    const long long wi = (long long)img * g.NW + g.woff[s] + (long long)gy * g.gw[s] + gx;
-    Win w;
-    w.st = pw_max;
-    w.x = (gx - gx0) * step;
-    w.y = (gy - gy0) * step;
-    w.S = patch;
-    w.T = c.has_tilted ? patch + ph * pw_max : nullptr;
-    int8_t out = -1;
-    bool live = false;
-    if (in) {
-        // HaarEvaluator::setWindow: sum from the patch, squared sum from Q
-        const int nr[4] = {1, 1, c.win_w - 2, c.win_h - 2};
-        const int32_t valsum = rsum(w.S, w.st, w.x, w.y, nr, false);
-        const int gxp = gx * step, gyp = gy * step;
-        const uint32_t valsq = (uint32_t)rsum(Q + base, st, gxp, gyp, nr, false);
-        const double area = (double)((c.win_w - 2) * (c.win_h - 2));
-        double nf = area * (double)valsq - (double)valsum * (double)valsum;
-        bool ok = nf > 0.;
-        if (ok) {
-            nf = sqrt(nf);
-            w.vnf = (float)(1. / nf);
-            ok = area * (double)w.vnf < 1e-1;
+    const uint32_t* PT = c.has_tilted ? patch + ph * pw_max : nullptr;
+    {
+        // HaarEvaluator::setWindow of this thread's window: sum from the patch, squared sum from Q; a window
+        // that is not flat joins the first phase's list
+        const int gx = gx0 + (tid % TW), gy = gy0 + tid / TW;
+        if (gx < g.gw[s] && gy < g.gh[s]) {
+            const int nr[4] = {1, 1, c.win_w - 2, c.win_h - 2};
+            const int32_t valsum = rsum(patch, pw_max, (gx - gx0) * step, (gy - gy0) * step, nr, false);
+            const uint32_t valsq = (uint32_t)rsum(Q + base, st, gx * step, gy * step, nr, false);
+            const double area = (double)((c.win_w - 2) * (c.win_h - 2));
+            double nf = area * (double)valsq - (double)valsum * (double)valsum;
+            bool ok = nf > 0.;
+            float vnf = 1.f;
+            if (ok) {
+                nf = sqrt(nf);
+                vnf = (float)(1. / nf);
+                ok = area * (double)vnf < 1e-1;
+            }
+            if (ok) {
+                s_live[0][atomicAdd(&s_n[0], 1)] = tid;
+                s_vnf[tid] = vnf;
+            } else {
+                res[(long long)img * g.NW + g.woff[s] + (long long)gy * g.gw[s] + gx] = -1;
+            }
         }
-        if (ok) {
-            const int f = (FM_HAAR_REC && c.recs) ? run_stages_rec(c, patch + w.y * pw_max + w.x,
-                                                                   w.T ? w.T + w.y * pw_max + w.x : nullptr, w.vnf, 0, split)
-                                                  : run_stages(c, w, 0, split);
-            if (f >= 0) out = f == 0 ? 0 : -1;
-            else if (split < c.n_stages) live = true;
-            else out = 1;
-        }
-        if (!live) res[wi] = out;
-    }
-    __shared__ float s_vnf[TW * TH];
-    if (live) {
-        s_live[atomicAdd(&s_n, 1)] = tid;
-        s_vnf[tid] = w.vnf;
     }
     __syncthreads();
-    const int n = s_n;
-    // survivors spread over the workgroup's waves (survivor k -> wave k % 4): a few deep windows
-    // finish in parallel instead of one after another in one wave's lanes
-    constexpr int NWV = TW * TH / 64;
-    const int k = (tid & 63) * NWV + (tid >> 6);
-    if (k < n) {
-        const int t2 = s_live[k];
-        const int gx2 = gx0 + (t2 % TW), gy2 = gy0 + t2 / TW;
-        Win v;
-        v.st = pw_max;
-        v.x = (gx2 - gx0) * step;
-        v.y = (gy2 - gy0) * step;
-        v.S = patch;
-        v.T = w.T;
-        v.vnf = s_vnf[t2];
-        const long long wi2 = (long long)img * g.NW + g.woff[s] + (long long)gy2 * g.gw[s] + gx2;
-        const int f = (FM_HAAR_REC && c.recs) ? run_stages_rec(c, patch + v.y * pw_max + v.x,
-                                                               v.T ? v.T + v.y * pw_max + v.x : nullptr, v.vnf, split,
-                                                               c.n_stages)
-                                              : run_stages(c, v, split, c.n_stages);
-        res[wi2] = f >= 0 ? -1 : 1;
+    // Phases of stages: each runs on the windows the previous one left alive, compacted into the first threads
+    // (one window each), so the lanes a wave issues for are mostly live ones: stages [0, 1), [1, 2), [2, split)
+    // and [split, n_stages) with FM_HAAR_HEADC, else [0, split) and [split, n_stages).  Each window's stages,
+    // stumps and sums are the same in any phase split (only which thread runs them changes).
+    int bnd[4], nb = 0;  // end stage of each phase (workgroup-uniform)
+    if (FM_HAAR_HEADC) {
+        bnd[nb++] = 1;
+        if (split > 1) bnd[nb++] = min(2, split);
+        if (split > 2) bnd[nb++] = split;
+    } else {
+        bnd[nb++] = split;
+    }
+    if (split < c.n_stages) bnd[nb++] = c.n_stages;
+    int sb = 0;
+    for (int p = 0; p < nb; ++p) {
+        const int e = bnd[p], n = s_n[p];
+        const bool last = e >= c.n_stages;
+        // the last phase's windows packed into the first waves (FM_HAAR_TAIL_SPREAD: window k -> wave k % 4,
+        // a few deep windows in parallel on the four SIMDs)
+        constexpr int NWV = TW * TH / 64;
+        const int k = (last && FM_HAAR_TAIL_SPREAD) ? (tid & 63) * NWV + (tid >> 6) : tid;
+        if (k < n) {
+            const int t2 = s_live[p & 1][k];
+            const int gx2 = gx0 + (t2 % TW), gy2 = gy0 + t2 / TW;
+            Win v;
+            v.st = pw_max;
+            v.x = (gx2 - gx0) * step;
+            v.y = (gy2 - gy0) * step;
+            v.S = patch;
+            v.T = PT;
+            v.vnf = s_vnf[t2];
+            const long long wi2 = (long long)img * g.NW + g.woff[s] + (long long)gy2 * g.gw[s] + gx2;
+            const int f = (FM_HAAR_REC && c.recs) ? run_stages_rec(c, patch + v.y * pw_max + v.x,
+                                                                   PT ? PT + v.y * pw_max + v.x : nullptr, v.vnf, sb, e)
+                                                  : run_stages(c, v, sb, e);
+            if (f >= 0) res[wi2] = f == 0 ? 0 : -1;  // 0: rejected by stage 0 (the row walk's skip)
+            else if (!last) s_live[(p + 1) & 1][atomicAdd(&s_n[p + 1], 1)] = t2;
+            else res[wi2] = 1;
+        }
+        if (p + 1 < nb) __syncthreads();  // (uniform: nb and bnd depend on split and the cascade only)
+        sb = e;
     }
 }
 
